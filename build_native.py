@@ -1,0 +1,89 @@
+"""Build libgpk.so (HIP kernels + C ABI) for gfx950 in-tree.
+
+Usage: python build_native.py [--force]
+The .so lands in fine_grained_gaussian_process_forcasting_amd/_lib/ (git-ignored, but it
+travels to the GPU box with the gpurun snapshot).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "fine_grained_gaussian_process_forcasting_amd")
+CSRC = os.path.join(PKG, "csrc")
+OUT_DIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(OUT_DIR, "libgpk.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",
+         "-Wno-unused-variable", "-Wno-unused-function", "-munsafe-fp-atomics"]
+
+
+def sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs.append(os.path.join(ROOT, "include", "gpk.h"))
+    return sorted(hs)
+
+
+def _digest(paths, extra=""):
+    h = hashlib.sha256(extra.encode())
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(OUT_DIR, exist_ok=True)
+    hdr_digest = _digest(headers(), " ".join(FLAGS))
+    objs = []
+    jobs = []
+    for src in sources():
+        obj = os.path.join(OUT_DIR, os.path.basename(src) + ".o")
+        stamp = obj + ".sha"
+        dig = _digest([src], hdr_digest)
+        objs.append(obj)
+        if not force and os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == dig:
+            continue
+        jobs.append((src, obj, stamp, dig))
+
+    def compile_one(job):
+        src, obj, stamp, dig = job
+        cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        if verbose:
+            print("[build]", " ".join(os.path.basename(c) if c.startswith(ROOT) else c for c in cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+        if r.stderr.strip() and verbose:
+            print(r.stderr, file=sys.stderr)
+        with open(stamp, "w") as f:
+            f.write(dig)
+
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        list(ex.map(compile_one, jobs))
+    if jobs or not os.path.exists(LIB):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(LIB + ".tmp", LIB)
+        if verbose:
+            print("[build] linked", os.path.relpath(LIB, ROOT), flush=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    args = ap.parse_args()
+    build(force=args.force)

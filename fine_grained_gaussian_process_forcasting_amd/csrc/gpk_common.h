@@ -1,0 +1,81 @@
+// Shared device helpers for the gfx950 GP kernels.
+//
+// Tile convention used by every kernel in this library ("acc layout"):
+// a 16x16 fp32 tile P is held by one wave, 4 registers per lane, exactly as
+// the accumulator of v_mfma_f32_16x16x4_f32 lays it out:
+//     lane l = 16*g + c  (g = l >> 4, c = l & 15),  reg r  <->  P[4g + r][c].
+// With the k-order pi(s, g) = 4g + s, a tile held in acc layout is directly a
+// legal A or B operand of the same MFMA (reg s in MFMA step s):
+//     sum_s mfma(Q.reg[s], P.reg[s])  ==  Q^T * P
+// so Cholesky panels, trailing updates, TRSMs and the RBF Gram all run on
+// register tiles with no transposes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+#define GPK_DEVICE __device__ __forceinline__
+
+// D += Q^T P for 16x16 tiles given in acc layout (4 MFMAs, K = 16).
+GPK_DEVICE f32x4 mma_tn(const f32x4 q, const f32x4 p, f32x4 d) {
+  d = __builtin_amdgcn_mfma_f32_16x16x4f32(q[0], p[0], d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x4f32(q[1], p[1], d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x4f32(q[2], p[2], d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x4f32(q[3], p[3], d, 0, 0, 0);
+  return d;
+}
+
+// Make this wave's LDS writes visible to its own other lanes before reading.
+GPK_DEVICE void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+GPK_DEVICE float readlane_f(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+
+GPK_DEVICE int wave_id_uniform() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+GPK_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+GPK_DEVICE double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Select element 4*g + r of a 16-entry register array with a per-lane g (0..3)
+// without dynamic register indexing (which would go to scratch).
+GPK_DEVICE f32x4 pick_group4(const float (&v)[16], int g) {
+  f32x4 o;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float a = v[r], b = v[4 + r], c = v[8 + r], d = v[12 + r];
+    o[r] = g == 0 ? a : (g == 1 ? b : (g == 2 ? c : d));
+  }
+  return o;
+}
+
+// Tile enumeration for an upper-triangular tile set of NB block rows/cols plus
+// an optional right-hand-side block column (index NB):
+//   t <  NB(NB+1)/2 : (i, j) with i <= j < NB, column-major  t = j(j+1)/2 + i
+//   t >= NB(NB+1)/2 : (t - NB(NB+1)/2, NB)
+GPK_DEVICE void tile_of(int t, int NB, int& i, int& j) {
+  const int tu = NB * (NB + 1) / 2;
+  if (t >= tu) { i = t - tu; j = NB; return; }
+  int jj = (int)((__builtin_sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+  while ((jj + 1) * (jj + 2) / 2 <= t) ++jj;
+  while (jj * (jj + 1) / 2 > t) --jj;
+  j = jj;
+  i = t - jj * (jj + 1) / 2;
+}

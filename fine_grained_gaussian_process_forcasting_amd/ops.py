@@ -1,0 +1,114 @@
+"""Torch-facing launchers for the gfx950 GP kernels (no compute happens here).
+
+Each function validates shapes/dtypes/devices on the host, allocates outputs with
+torch (device memory, caller stream), and enqueues ONE C-ABI call on
+``torch.cuda.current_stream()``. Tensors must live on a ROCm device; there is
+no CPU path.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _native
+from .errors import NanError, NotPSDError, NumericalWarning
+
+
+def _require_device(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if not t.is_cuda:
+            raise ValueError("gpk ops run only on a ROCm device (tensor.is_cuda must be True); "
+                             "there is no CPU fallback")
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _scalar_tensor(v, device) -> torch.Tensor:
+    if isinstance(v, torch.Tensor):
+        return v.detach().reshape(-1).to(device=device, dtype=torch.float32)
+    return torch.tensor([float(v)], device=device, dtype=torch.float32)
+
+
+def pack_exact_hyper(outputscale, noise, mean_constant, lengthscale, device) -> torch.Tensor:
+    """Device vector {s2, noise, c, lengthscale...} consumed by gpk_exact_mll_f32."""
+    parts = [_scalar_tensor(outputscale, device)[:1], _scalar_tensor(noise, device)[:1],
+             _scalar_tensor(mean_constant, device)[:1], _scalar_tensor(lengthscale, device)]
+    return torch.cat(parts).contiguous()
+
+
+@dataclass
+class ExactMLLOut:
+    mll: torch.Tensor            # (B,)
+    L: Optional[torch.Tensor]    # (B, N, N) lower Cholesky factor of K + noise I (+ jitter)
+    z: Optional[torch.Tensor]    # (B, N)   L^{-1}(y - c)
+    info: torch.Tensor           # (B,) int32 (0 / -t / k, see include/gpk.h)
+
+
+def exact_mll(X: torch.Tensor, y: torch.Tensor, lengthscale, outputscale, mean_constant, noise,
+              jitter: float = 1e-6, max_tries: int = 3, want_L: bool = True,
+              want_z: bool = False, hyper: Optional[torch.Tensor] = None) -> ExactMLLOut:
+    """Fused exact-GP log marginal likelihood per window (one gfx950 kernel launch).
+
+    X: (B, N, D) float32, y: (B, N) float32 on the same ROCm device. ``lengthscale``
+    is a scalar or a length-D vector (ARD). Hyperparameters may be python floats or
+    device tensors (no host sync either way). See include/gpk.h::gpk_exact_mll_f32.
+    """
+    if X.dim() != 3:
+        raise ValueError(f"X must be (B, N, D), got {tuple(X.shape)}")
+    B, N, D = X.shape
+    if y.shape != (B, N):
+        raise ValueError(f"y must be (B, N) = {(B, N)}, got {tuple(y.shape)}")
+    _require_device(X, y)
+    X = X.contiguous().float()
+    y = y.contiguous().float()
+    dev = X.device
+    if hyper is None:
+        hyper = pack_exact_hyper(outputscale, noise, mean_constant, lengthscale, dev)
+    n_ls = hyper.numel() - 3
+    if n_ls not in (1, D):
+        raise ValueError(f"lengthscale must have 1 or D={D} entries, got {n_ls}")
+    mll = torch.empty(B, device=dev, dtype=torch.float32)
+    info = torch.empty(B, device=dev, dtype=torch.int32)
+    L = torch.empty(B, N, N, device=dev, dtype=torch.float32) if want_L else None
+    z = torch.empty(B, N, device=dev, dtype=torch.float32) if want_z else None
+    rc = _native.lib().gpk_exact_mll_f32(
+        X.data_ptr(), y.data_ptr(), hyper.data_ptr(), n_ls, B, N, D, float(jitter), int(max_tries),
+        L.data_ptr() if L is not None else None, z.data_ptr() if z is not None else None,
+        mll.data_ptr(), info.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_exact_mll_f32")
+    return ExactMLLOut(mll, L, z, info)
+
+
+def check_cholesky_info(info: torch.Tensor, jitter: float, inputs=(), what: str = "cholesky") -> None:
+    """GPyTorch's psd_safe_cholesky bookkeeping, from the per-window info codes.
+
+    One device->host sync (GPyTorch pays the same: ``torch.any(info)``). Emits the
+    same NumericalWarning text per ladder step and raises NanError / NotPSDError.
+    """
+    info_h = info.detach().to("cpu")
+    if not bool((info_h != 0).any()):
+        return
+    if bool((info_h > 0).any()):
+        for t in inputs:
+            if t is not None and bool(torch.isnan(t).any()):
+                raise NanError(f"{what}: {int(torch.isnan(t).sum())} of {t.numel()} elements of the "
+                               f"{tuple(t.shape)} tensor are NaN.")
+    steps = int((-info_h[info_h < 0]).max()) if bool((info_h < 0).any()) else 0
+    if bool((info_h > 0).any()):
+        steps = max(steps, 0)
+    for i in range(steps):
+        warnings.warn(f"A not p.d., added jitter of {jitter * (10 ** i):.1e} to the diagonal",
+                      NumericalWarning)
+    if bool((info_h > 0).any()):
+        raise NotPSDError(
+            f"Matrix not positive definite after repeatedly adding jitter up to "
+            f"{jitter * 10 ** 2:.1e}. Failing windows: {torch.nonzero(info_h > 0).flatten().tolist()[:16]}")
+
+
+LOG_2PI = math.log(2 * math.pi)
