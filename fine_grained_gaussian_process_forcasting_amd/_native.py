@@ -29,6 +29,11 @@ SIGNATURES = {
                                   c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
 }
+DEBUG_SIGNATURES = {
+    "gpk_debug_exact_stamps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                       c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p]),
+}
 
 
 class NativeLibraryError(RuntimeError):
@@ -59,7 +64,7 @@ def lib():
             handle = ctypes.CDLL(_LIB_PATH)
         except OSError as e:  # pragma: no cover - depends on the box
             raise NativeLibraryError(f"failed to load {_LIB_PATH}: {e}") from e
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in {**SIGNATURES, **DEBUG_SIGNATURES}.items():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

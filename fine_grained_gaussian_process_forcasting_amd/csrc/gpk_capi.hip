@@ -41,4 +41,13 @@ int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp, int n_le
   return gpk_launch_exact(a, (hipStream_t)stream);
 }
 
+// Diagnostic (not part of the product ABI): same as gpk_exact_mll_f32 for N in
+// (240, 256], plus per-workgroup phase clocks (16 x u64 per window) in `stamps`.
+int gpk_debug_exact_stamps(const float* X, const float* y, const float* hyp, int n_lengthscale,
+                           int B, int N, int D, double jitter, int max_tries, float* L, float* z,
+                           float* mll, int* info, unsigned long long* stamps, void* stream) {
+  GpkExactArgs a{X, y, hyp, n_lengthscale, B, N, D, jitter, max_tries, L, z, mll, info};
+  return gpk_launch_exact_stamps(a, stamps, (hipStream_t)stream);
+}
+
 }  // extern "C"

@@ -9,17 +9,24 @@
 //   mll   = -0.5 * (||L^{-1}(y-c)||^2 + 2 sum log L_ii + N log 2pi) / N
 //           (upstream mlls/exact_marginal_log_likelihood.py, MVN.log_prob)
 //
-// Design: one workgroup of W waves per window. The padded
-// K_hat (NB x NB tiles of 16x16, upper triangle, plus one right-hand-side
-// block column holding y - c) lives in REGISTERS as MFMA accumulators (acc
-// layout, see gpk_common.h); tile t is owned by wave t % W. The blocked
-// right-looking Cholesky works on R = L^T:
-//   A(k): owner of (k,k) factors its tile (readlane-broadcast column steps)
-//         and publishes -R_kk^{-1} (acc layout) through LDS.
-//   B(k): owners of (k,j) compute R_kj = R_kk^{-T} T_kj with 4 MFMAs and
-//         publish R_kj through an LDS panel; the RHS block yields z.
-//   C(k): every owner of (i,j), i > k, accumulates  R_ki^T R_kj  (4 MFMAs).
-// The MFMA accumulators hold -T, so every update is a plain MFMA accumulate.
+// Design: one workgroup of W waves per window, two workgroups per
+// CU. The padded K_hat (NB x NB tiles of 16x16, upper triangle, plus one
+// right-hand-side block column holding y - c) lives in REGISTERS as MFMA
+// accumulators (acc layout, see gpk_common.h). Tiles are dealt to waves in
+// row-descending order (ExactPlan), so at step k the tiles a wave still has to
+// update are a PREFIX of its slots. The blocked right-looking Cholesky works on
+// R = L^T (all accumulators hold -T, so every update is a plain MFMA accumulate):
+//   B(k): owners of (k,j) compute R_kj = R_kk^{-T} T_kj (4 MFMAs) and publish
+//         R_kj through an LDS panel; the RHS block yields z = L^{-1}(y - c).
+//   C(k): every owner of (i,j), i > k, accumulates R_ki^T R_kj (4 MFMAs, two
+//         independent chains per pair of slots). The owner of (k+1,k+1) updates
+//         that tile first and factors it right away (look-ahead), overlapping
+//         the diagonal factorisation with everybody else's trailing update.
+// Diagonal tiles are factored by one wave in one sweep: lanes 0-15 hold columns
+// of R, lanes 16-31 columns of R^{-T}, and both are produced by the SAME
+// readlane-broadcast instruction stream.
+// Barriers wait on LDS only (s_waitcnt lgkmcnt(0); s_barrier): the L stores
+// stream out behind the factorisation instead of being drained at each step.
 #include "gpk_common.h"
 #include "gpk_internal.h"
 
@@ -27,173 +34,267 @@ namespace {
 
 constexpr float kLog2Pi = 1.8378770664093453f;
 
-// (i | j << 8) for upper tiles i <= j < 16 in column-major order t = j(j+1)/2 + i.
-struct TileTable {
-  int v[136];
-  constexpr TileTable() : v() {
+// Static tile -> (wave, slot) plan. Tiles are listed row-descending (i = NB-1
+// .. 0), j = i..NB inside a row (j = NB is the right-hand side), and dealt
+// cyclically: tile t -> wave t % W, slot t / W. Then
+//   tiles with i > k            = { t < P(k) },  P(k) = (NB-k)(NB-k+1)/2 - 1
+//   diagonal tile (k,k)         = t = P(k)
+//   off-diagonal row-k tiles    = P(k) < t <= P(k) + NB - k
+template <int NB>
+struct ExactPlan {
+  static constexpr int NT = NB * (NB + 1) / 2 + NB;
+  int ij[NT];   // i | j << 8
+  constexpr ExactPlan() : ij() {
     int t = 0;
-    for (int j = 0; j < 16; ++j)
-      for (int i = 0; i <= j; ++i) v[t++] = i | (j << 8);
+    for (int i = NB - 1; i >= 0; --i)
+      for (int j = i; j <= NB; ++j) ij[t++] = i | (j << 8);
   }
 };
-__constant__ TileTable c_tile_tbl = TileTable();
-#define c_tile_ij (c_tile_tbl.v)
+
+template <int NB>
+__constant__ ExactPlan<NB> c_plan = ExactPlan<NB>();
+
+template <int NB>
+GPK_DEVICE constexpr int plan_P(int k) {
+  return (NB - k) * (NB - k + 1) / 2 - 1;
+}
 
 struct ExactLds {
   // offsets in floats
-  int xf, nrm, rv, panel, rinv, dsc, red, total;
+  int xf, xh, xl, nrm, rv, panel, wbuf, dsc, cpart, red, total;
 };
 
 __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
+  const int DC32 = (DC + 1) / 2;
   ExactLds o;
-  o.xf = 0;
-  o.nrm = o.xf + NB * DC * 256;
+  o.xf = 0;                              // fp32 staging, later f16 hi/lo images (aliased)
+  o.xh = 0;
+  o.xl = 0;
+  o.nrm = o.xf + NB * (2 * DC32) * 256;
   o.rv = o.nrm + NB * 16;
   o.panel = o.rv + NB * 16;
-  int panel_sz = (NB + 1) * 256;
-  if (panel_sz < 64 * W) panel_sz = 64 * W;  // reused for centring partials
-  o.rinv = o.panel + panel_sz;
-  o.dsc = o.rinv + 256;
-  o.red = o.dsc + 256;
-  o.total = o.red + 4 * W + 16;
+  o.wbuf = o.panel + (NB + 1) * 256;
+  o.dsc = o.wbuf + 256;
+  o.cpart = o.dsc + 256;
+  o.red = o.cpart + 64 * W + 256;
+  o.total = o.red + 4 * W + 32;
   return o;
 }
 
-GPK_DEVICE int frag_index(int n, int d, int DC) {
+// fp32 staging of X (16x16x4 fragment layout, CHUNK-major so that 16-column
+// chunks 2q and 2q+1 occupy exactly the bytes of the f16 hi / lo images of
+// 32-column chunk q, which overwrite them in place).
+GPK_DEVICE int frag_index(int n, int d, int NB) {
   const int blk = n >> 4, c = n & 15, dd = d >> 4, g = (d >> 2) & 3, r = d & 3;
-  return ((blk * DC + dd) * 64 + 16 * g + c) * 4 + r;
+  return ((dd * NB + blk) * 64 + 16 * g + c) * 4 + r;
 }
 
-// Factor one 16x16 diagonal tile (given as -T in acc layout) in a single wave.
-// Writes L's diagonal block (row-major, ld = N) when Lrow != nullptr, publishes
-// -R^{-1} in acc layout to rinv_out, returns the 1-based failing column or 0.
-GPK_DEVICE int diag_factor(const f32x4 a, float* dsc, float* rinv_out, float* Lblk,
-                           int N, int row0, float& logdet) {
-  // Launder the lane id so the per-lane compare masks below are not hoisted out
-  // of the caller's loops (they would each pin an SGPR pair for the whole kernel).
+// f16 hi (part 0) / lo (part 1) images of 32-column chunk q, 16x16x32 fragment
+// layout: lane 16g + c of block b holds x[16b + c][32q + 8g + j], j = 0..7.
+// Returned as a half index from the start of the staging area.
+GPK_DEVICE int hfrag_index(int n, int d, int NB, int part) {
+  const int blk = n >> 4, c = n & 15, q = d >> 5, g = (d >> 3) & 3, j = d & 7;
+  return (2 * q + part) * NB * 512 + ((blk * 64) + 16 * g + c) * 8 + j;
+}
+
+GPK_DEVICE int launder_s(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+// Workgroup barrier that orders LDS only; outstanding global stores keep flowing.
+GPK_DEVICE void barrier_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+GPK_DEVICE void store4(float* p, int N, int row, int colg, const f32x4 v) {
+  if (row >= N) return;
+  if (((N & 3) == 0) && colg + 3 < N) {
+    *(f32x4*)&p[(size_t)row * N + colg] = v;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (colg + r < N) p[(size_t)row * N + colg + r] = v[r];
+  }
+}
+
+template <int I>
+GPK_DEVICE void pin_row(float (&sb)[16]);
+
+// pin_row<I>: one asm statement consuming sb[I..15] as SGPR operands.
+template <> GPK_DEVICE void pin_row<1>(float (&sb)[16]) { asm volatile("" : "+s"(sb[1]), "+s"(sb[2]), "+s"(sb[3]), "+s"(sb[4]), "+s"(sb[5]), "+s"(sb[6]), "+s"(sb[7]), "+s"(sb[8]), "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<2>(float (&sb)[16]) { asm volatile("" : "+s"(sb[2]), "+s"(sb[3]), "+s"(sb[4]), "+s"(sb[5]), "+s"(sb[6]), "+s"(sb[7]), "+s"(sb[8]), "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<3>(float (&sb)[16]) { asm volatile("" : "+s"(sb[3]), "+s"(sb[4]), "+s"(sb[5]), "+s"(sb[6]), "+s"(sb[7]), "+s"(sb[8]), "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<4>(float (&sb)[16]) { asm volatile("" : "+s"(sb[4]), "+s"(sb[5]), "+s"(sb[6]), "+s"(sb[7]), "+s"(sb[8]), "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<5>(float (&sb)[16]) { asm volatile("" : "+s"(sb[5]), "+s"(sb[6]), "+s"(sb[7]), "+s"(sb[8]), "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<6>(float (&sb)[16]) { asm volatile("" : "+s"(sb[6]), "+s"(sb[7]), "+s"(sb[8]), "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<7>(float (&sb)[16]) { asm volatile("" : "+s"(sb[7]), "+s"(sb[8]), "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<8>(float (&sb)[16]) { asm volatile("" : "+s"(sb[8]), "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<9>(float (&sb)[16]) { asm volatile("" : "+s"(sb[9]), "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<10>(float (&sb)[16]) { asm volatile("" : "+s"(sb[10]), "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<11>(float (&sb)[16]) { asm volatile("" : "+s"(sb[11]), "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<12>(float (&sb)[16]) { asm volatile("" : "+s"(sb[12]), "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<13>(float (&sb)[16]) { asm volatile("" : "+s"(sb[13]), "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<14>(float (&sb)[16]) { asm volatile("" : "+s"(sb[14]), "+s"(sb[15])); }
+template <> GPK_DEVICE void pin_row<15>(float (&sb)[16]) { asm volatile("" : "+s"(sb[15])); }
+
+// Software-pipelined right-looking sweep of the fused R / R^{-T} factorisation
+// (see diag_factor). Step m is split into
+//   crit(m): pivot broadcast, scaling of row m, and the ONE update that the next
+//            pivot depends on (v[m+1]);
+//   rest(m): the other 14-m column updates of step m,
+// emitted as crit(0) crit(1) rest(0) crit(2) rest(1) ... so the broadcast / FMA
+// stream of rest(m-1) fills the rsq latency of crit(m). The readlanes of a group
+// land in distinct SGPRs pinned by one asm statement, and the FMAs run as
+// packed pairs (v_pk_fma_f32) on SGPR pairs.
+template <int M>
+GPK_DEVICE void diag_crit(float (&v)[16]) {
+  const float piv = readlane_f(v[M], M);
+  const float rs = __builtin_amdgcn_rsqf(piv);
+  v[M] = v[M] * rs;
+  if constexpr (M < 15) {
+    float s1 = readlane_f(v[M], M + 1);
+    asm volatile("" : "+s"(s1));
+    v[M + 1] = __builtin_fmaf(-s1, v[M], v[M + 1]);
+  }
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int M>
+GPK_DEVICE void diag_rest(float (&v)[16]) {
+  constexpr int I0 = M + 2;
+  if constexpr (I0 < 16) {
+    float sb[16];
+#pragma unroll
+    for (int i = I0; i < 16; ++i) sb[i] = readlane_f(v[M], i);
+    pin_row<I0>(sb);
+    const f32x2 vm = {v[M], v[M]};
+    int i = I0;
+    if constexpr ((16 - I0) & 1) {
+      v[i] = __builtin_fmaf(-sb[i], v[M], v[i]);
+      ++i;
+    }
+#pragma unroll
+    for (; i < 16; i += 2) {
+      f32x2 a = {v[i], v[i + 1]};
+      const f32x2 sv = {-sb[i], -sb[i + 1]};
+      a = __builtin_elementwise_fma(sv, vm, a);
+      v[i] = a[0];
+      v[i + 1] = a[1];
+    }
+  }
+}
+
+template <int M>
+GPK_DEVICE void diag_sweep(float (&v)[16]) {
+  __builtin_amdgcn_sched_barrier(0);
+  diag_crit<M>(v);
+  if constexpr (M > 0) diag_rest<M - 1>(v);
+#pragma unroll
+  for (int i = M; i < 16; ++i) asm volatile("" : "+v"(v[i]));
+  if constexpr (M < 15) diag_sweep<M + 1>(v);
+}
+
+// Factor one 16x16 diagonal tile T (given as -T in acc layout) in ONE wave.
+//   lanes  0-15 (column c): v[m] <- R[m][c]             (R^T R = T, upper)
+//   lanes 16-31 (column c): v[m] <- W[m][c], W = R^{-T}  (lower), started from I
+// from one instruction stream: at step m every lane does
+//   v[m] *= rsqrt(pivot);   v[i] -= R[m][i] * v[m]   (i > m)
+// with R[m][i] broadcast from R-lane i by readlane. A non-positive or NaN pivot
+// turns every later diagonal entry into NaN, so the first failing column is
+// found once at the end from the diagonal of R.
+// Outputs: L diagonal block rows (global), -W transposed into wbuf
+// (wbuf[c*16 + m] = -W[m][c]), logdet += log|T|; returns 1-based fail column.
+GPK_DEVICE int diag_factor(const f32x4 a, float* dsc, float* wbuf, float* Lb, int N,
+                           int row0, float& logdet) {
+  // The factorisation is the critical path of the window: let this wave win
+  // issue arbitration over the MFMA-streaming waves sharing its SIMD.
+  __builtin_amdgcn_s_setprio(3);
   int lane = threadIdx.x & 63;
-  asm volatile("" : "+v"(lane));
+  asm volatile("" : "+v"(lane));  // keep per-lane masks local to this call
   const int c = lane & 15, grp = lane >> 4;
   *(f32x4*)&dsc[lane * 4] = a;
   wave_lds_sync();
-  float col[16];
+  float v[16];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const f32x4 v = *(const f32x4*)&dsc[(16 * g + c) * 4];
+    const f32x4 t = *(const f32x4*)&dsc[(16 * g + c) * 4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) col[4 * g + r] = -v[r];
-  }
-  int fail = 0;
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    __builtin_amdgcn_sched_barrier(0);
-    const float piv = readlane_f(col[m], m);
-    if (!(piv > 0.f) && fail == 0) fail = m + 1;
-    const float rowv = col[m] * __builtin_amdgcn_rsqf(piv);
-    col[m] = rowv;
-#pragma unroll
-    for (int i = m + 1; i < 16; ++i) {
-      const float s = readlane_f(rowv, i);
-      col[i] = __builtin_fmaf(-s, rowv, col[i]);
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * g + r;
+      v[i] = (grp == 0) ? -t[r] : ((grp == 1 && i == c) ? 1.f : 0.f);
     }
-    // Pin the right-looking order: materialise every column update now so the
-    // compiler does not sink the FMAs (which keeps 100+ readlane SGPRs live).
-#pragma unroll
-    for (int i = m; i < 16; ++i) asm volatile("" : "+v"(col[i]));
-    asm volatile("" : "+v"(fail));
   }
-  // log|T| = sum_c log R[c][c]^2 (GPyTorch: _chol_diag.pow(2).log().sum())
-  {
-    float dg = col[0];
+  diag_sweep<0>(v);
+  // diagonal of R, failure detection, log|T| = sum_c log R[c][c]^2
+  float dg = v[0];
 #pragma unroll
-    for (int i = 1; i < 16; ++i) dg = (c == i) ? col[i] : dg;
+  for (int i = 1; i < 16; ++i) dg = (c == i) ? v[i] : dg;
+  const bool okd = (dg > 0.f) && (dg < __builtin_huge_valf());
+  const unsigned long long badm = __ballot(lane < 16 && !okd);
+  const int fail = badm ? __builtin_ctzll(badm) + 1 : 0;
+  {
     float lg = (lane < 16) ? __builtin_amdgcn_logf(dg * dg) : 0.f;
 #pragma unroll
     for (int off = 8; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
     logdet += readlane_f(lg, 0) * 0.69314718055994531f;  // v_log_f32 is log2
   }
+  if (grp == 1) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (i > c) col[i] = 0.f;
-  // L diagonal block: L[row0 + c][row0 + i] = R[i][c] = col[i]
-  if (Lblk != nullptr) {
-    const f32x4 o = pick_group4(col, grp);
-    const int row = row0 + c, colg = row0 + 4 * grp;
-    if (row < N) {
-      if (((N & 3) == 0) && colg + 3 < N) {
-        *(f32x4*)&Lblk[(size_t)row * N + colg] = o;
-      } else {
+    for (int g = 0; g < 4; ++g)
+      *(f32x4*)&wbuf[c * 16 + 4 * g] = f32x4{-v[4 * g], -v[4 * g + 1], -v[4 * g + 2], -v[4 * g + 3]};
+  } else if (grp == 0) {
+    // R lanes: zero below-diagonal garbage, write L[row0 + c][row0 + m] = R[m][c]
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (colg + r < N) Lblk[(size_t)row * N + colg + r] = o[r];
-      }
+    for (int i = 0; i < 16; ++i)
+      if (i > c) v[i] = 0.f;
+    if (Lb != nullptr) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(Lb, N, row0 + c, row0 + 4 * g, f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
     }
   }
-  // In-place upper-triangular inverse, column c per lane: X = R^{-1}.
-#pragma unroll
-  for (int i = 15; i >= 0; --i) {
-    __builtin_amdgcn_sched_barrier(0);
-    const float rii = readlane_f(col[i], i);
-    float acc = (c == i) ? 1.f : 0.f;
-#pragma unroll
-    for (int p = i + 1; p < 16; ++p) {
-      const float s = readlane_f(col[i], p);  // R[i][p]
-      acc = __builtin_fmaf(-s, col[p], acc);
-    }
-    col[i] = acc * __builtin_amdgcn_rcpf(rii);
-    asm volatile("" : "+v"(col[i]));
-  }
-  f32x4 q = pick_group4(col, grp);
-  q = -q;
-  *(f32x4*)&rinv_out[lane * 4] = q;
+  __builtin_amdgcn_s_setprio(0);
   return fail;
 }
 
-// Tile held by slot s of wave wv (t = wv + W*s, see tile_of in gpk_common.h).
-// Called with a laundered wave id inside every phase so the compiler cannot
-// hoist per-slot coordinates/addresses out of the factorisation loop (they
-// would pin ~2 SGPRs + 2 VGPRs per slot for the whole kernel).
-template <int NB, int W>
-GPK_DEVICE void slot_tile(int wv, int s, int& i, int& j) {
-  constexpr int NTU = NB * (NB + 1) / 2, NT = NTU + NB;
-  const int t = wv + W * s;
-  if (t < NTU) { const int v = c_tile_ij[t]; i = v & 255; j = v >> 8; }
-  else if (t < NT) { i = t - NTU; j = NB; }
-  else { i = -1; j = -1; }
-}
-
-GPK_DEVICE int launder_s(int v) { asm volatile("" : "+s"(v)); return v; }
-
-GPK_DEVICE void store_block(float* L, int N, int row, int colg, const f32x4 v) {
-  if (row >= N) return;
-  if (((N & 3) == 0) && colg + 3 < N) {
-    *(f32x4*)&L[(size_t)row * N + colg] = v;
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (colg + r < N) L[(size_t)row * N + colg + r] = v[r];
-  }
-}
-
-template <int NB, int W>
-__global__ void __launch_bounds__(64 * W, 4)
+template <int NB, int W, bool STAMPS = false>
+__global__ void __launch_bounds__(64 * W, (2 * W) / 4)
 gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
                  const float* __restrict__ hyp, int n_ls, int N, int D, int DC,
                  double jitter0, int max_tries, float* __restrict__ Lout,
                  float* __restrict__ zout, float* __restrict__ mll,
-                 int* __restrict__ info) {
-  constexpr int NTU = NB * (NB + 1) / 2;
-  constexpr int NT = NTU + NB;
+                 int* __restrict__ info, unsigned long long* __restrict__ stamps = nullptr) {
+  constexpr int NT = ExactPlan<NB>::NT;
   constexpr int SLOTS = (NT + W - 1) / W;
   constexpr int T = 64 * W;
+  // Diagnostic-only phase clocks (STAMPS build): wave 0 lane 0 of each workgroup.
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0, st_t0 = 0, st_rt0 = 0;
+#define GPK_STAMP(slot)                                         \
+  if constexpr (STAMPS) {                                       \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+    st_acc[slot] += _n - st_last;                               \
+    st_last = _n;                                               \
+    __builtin_amdgcn_sched_barrier(0);                          \
+  }
+  if constexpr (STAMPS) {
+    st_rt0 = __builtin_amdgcn_s_memrealtime();
+    st_t0 = __builtin_amdgcn_s_memtime();
+    st_last = st_t0;
+  }
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const ExactLds lay = exact_lds_layout(NB, DC, W);
   float* xf = smem + lay.xf;
   float* nrm = smem + lay.nrm;
   float* rv = smem + lay.rv;
   float* panel = smem + lay.panel;
-  float* rinv = smem + lay.rinv;
+  float* wbuf = smem + lay.wbuf;
   float* dsc = smem + lay.dsc;
+  float* cpart = smem + lay.cpart;
   float* red = smem + lay.red;
   int* flag = (int*)(red + 4 * W);
 
@@ -207,63 +308,119 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   const float s2 = hyp[0];
   const float noise = hyp[1];
   const float cmean = hyp[2];
+  const float* Xb = X + (size_t)b * N * D;
+  float* Lb = Lout ? Lout + (size_t)b * N * N : nullptr;
 
   // ---- 1. stage X / l into LDS in fragment layout (zero padded) ----------
-  const float* Xb = X + (size_t)b * N * D;
-  for (int idx = tid; idx < NP * DP; idx += T) {
-    const int n = idx / DP, d = idx - n * DP;
-    float v = 0.f;
-    if (n < N && d < D) v = Xb[(size_t)n * D + d] / hyp[3 + (n_ls == 1 ? 0 : d)];
-    xf[frag_index(n, d, DC)] = v;
-  }
-  __syncthreads();
-  // ---- 2. centre columns by the mean over the N real rows (GPyTorch _sq_dist)
+  // Each thread owns 16-column chunks of rows; all of its global loads are
+  // issued before any is consumed.
   {
-    const int parts = T / DP;  // DP divides T (host guarantees DP <= T, power-of-2 chunking)
-    const int part = tid / DP, d = tid - part * DP;
-    if (part < parts) {
-      float s = 0.f;
-      for (int n = part; n < N; n += parts) s += xf[frag_index(n, d, DC)];
-      panel[part * DP + d] = s;
-    }
-    __syncthreads();
-    if (tid < DP) {
-      float s = 0.f;
-      for (int p = 0; p < parts; ++p) s += panel[p * DP + tid];
-      rinv[tid] = s / (float)N;
-    }
-    __syncthreads();
-    for (int idx = tid; idx < N * DP; idx += T) {
-      const int n = idx / DP, d = idx - n * DP;
-      if (d < D) xf[frag_index(n, d, DC)] -= rinv[d];
-    }
-    __syncthreads();
-  }
-  // ---- 3. squared norms and residual r = y - c ---------------------------
-  for (int n = tid; n < NP; n += T) {
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) {
-      const float v = xf[frag_index(n, d, DC)];
-      s = __builtin_fmaf(v, v, s);
-    }
-    nrm[n] = s;
-    rv[n] = (n < N) ? (y[(size_t)b * N + n] - cmean) : 0.f;
-  }
-
-  float* Lb = Lout ? Lout + (size_t)b * N * N : nullptr;
-  // ---- zero the strictly-upper 16x16 blocks of L once (never rewritten) ----
-  if (Lb != nullptr) {
-    const int vec = ((N & 3) == 0);
-    for (int row = wave; row < N; row += W) {
-      const int c0 = ((row >> 4) + 1) << 4;  // first column of the next block column
-      if (vec) {
-        for (int cc = c0 + 4 * lane; cc < N; cc += 256)
-          *(f32x4*)&Lb[(size_t)row * N + cc] = f32x4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        for (int cc = c0 + lane; cc < N; cc += 64) Lb[(size_t)row * N + cc] = 0.f;
+    const int chunks = NP * DC;  // (row, 16-col chunk) pairs
+    for (int base = 0; base < chunks; base += T) {
+      const int q = base + tid;
+      float v[16];
+      const int n = q / DC, dd = q - n * DC;
+      if (q < chunks) {
+        const int d0 = dd * 16;
+        if (n < N && (D & 3) == 0 && d0 + 16 <= D) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const f32x4 t = *(const f32x4*)&Xb[(size_t)n * D + d0 + 4 * u];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[4 * u + r] = t[r];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            v[e] = (n < N && d0 + e < D) ? Xb[(size_t)n * D + d0 + e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int d = d0 + e;
+          if (d < D && n < N) v[e] = v[e] / hyp[3 + (n_ls == 1 ? 0 : d)];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          *(f32x4*)&xf[frag_index(n, d0 + 4 * u, NB)] = f32x4{v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]};
       }
     }
   }
+  barrier_lds();
+  // ---- 2. centre columns by the mean over the N real rows (GPyTorch _sq_dist)
+  {
+    const int parts = T / DP;
+    const int part = tid / DP, d = tid - part * DP;
+    if (part < parts) {
+      float sacc[4] = {0.f, 0.f, 0.f, 0.f};
+      int n = part;
+      for (; n + 3 * parts < N; n += 4 * parts) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sacc[u] += xf[frag_index(n + u * parts, d, NB)];
+      }
+      for (; n < N; n += parts) sacc[0] += xf[frag_index(n, d, NB)];
+      cpart[part * DP + d] = (sacc[0] + sacc[1]) + (sacc[2] + sacc[3]);
+    }
+    barrier_lds();
+    if (tid < DP) {
+      float s = 0.f;
+      for (int p = 0; p < parts; ++p) s += cpart[p * DP + tid];
+      cpart[64 * W + tid] = s / (float)N;
+    }
+    barrier_lds();
+  }
+  // ---- 3. subtract the mean, squared norms, residual r = y - c -----------
+  // The centred rows are split into f16 hi + lo parts (x = hi + lo + O(2^-22 x))
+  // for the 3-pass f16 MFMA Gram; the images overwrite the
+  // fp32 staging chunk pair they were read from (read all -> barrier -> write).
+  {
+    const float* cmean_d = cpart + 64 * W;
+    _Float16* xh16 = (_Float16*)(smem + lay.xf);
+    const int DC32 = (DC + 1) / 2;
+    const int n = tid;  // NP <= 256 <= T: one row per thread
+    float s = 0.f;
+    for (int q = 0; q < DC32; ++q) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int d0 = 32 * q + 4 * u;
+        f32x4 t = {0.f, 0.f, 0.f, 0.f};
+        if (n < NP && d0 < 16 * DC) {
+          t = *(const f32x4*)&xf[frag_index(n, d0, NB)];
+          if (n < N) {
+            const f32x4 m4 = *(const f32x4*)&cmean_d[d0];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[r] = (d0 + r < D) ? t[r] - m4[r] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[4 * u + r] = t[r];
+      }
+      barrier_lds();
+      if (n < NP) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          half4_t hi, lo;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t = v[4 * u + r];
+            s = __builtin_fmaf(t, t, s);
+            hi[r] = (_Float16)t;
+            lo[r] = (_Float16)(t - (float)hi[r]);
+          }
+          *(half4_t*)&xh16[hfrag_index(n, 32 * q + 4 * u, NB, 0)] = hi;
+          *(half4_t*)&xh16[hfrag_index(n, 32 * q + 4 * u, NB, 1)] = lo;
+        }
+      }
+      barrier_lds();
+    }
+    if (n < NP) {
+      nrm[n] = s;
+      rv[n] = (n < N) ? (y[(size_t)b * N + n] - cmean) : 0.f;
+    }
+  }
+  barrier_lds();
+  GPK_STAMP(0)
+
   const float nhalf_log2e = -0.72134752044448170f;  // -0.5 * log2(e)
   float diagval = s2 + noise;
   double jit_prev = 0.0;
@@ -278,79 +435,93 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       diagval = diagval + (float)(jn - jit_prev);
       jit_prev = jn;
     }
-    if (tid == 0) flag[0] = 0;
-    __syncthreads();
 
     // ---- 4. RBF tiles straight into the accumulators (negated) -----------
-    const int wv0 = launder_s(wave);
+    {
+      const int wv = launder_s(wave);
 #pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      int i, j;
-      slot_tile<NB, W>(wv0, s, i, j);
-      if (i < 0) continue;
-      if (j < NB) {
-        f32x4 g = {0.f, 0.f, 0.f, 0.f};
-        for (int dd = 0; dd < DC; ++dd) {
-          const f32x4 xa = *(const f32x4*)&xf[((i * DC + dd) * 64 + lane) * 4];
-          const f32x4 xb = *(const f32x4*)&xf[((j * DC + dd) * 64 + lane) * 4];
-          g = mma_tn(xa, xb, g);
-        }
-        const f32x4 nr = *(const f32x4*)&nrm[16 * i + 4 * grp];
-        const int col = 16 * j + c;
-        const float nc = nrm[col];
-        f32x4 o;
+      for (int s = 0; s < SLOTS; ++s) {
+        const int t = wv + W * s;
+        if (t >= NT) continue;
+        const int pk = c_plan<NB>.ij[t];
+        const int i = pk & 255, j = pk >> 8;
+        if (j < NB) {
+          f32x4 g = {0.f, 0.f, 0.f, 0.f};
+          const int DC32 = (DC + 1) / 2;
+          const half8_t* x8 = (const half8_t*)(smem + lay.xf);
+          for (int dd = 0; dd < DC32; ++dd) {
+            const half8_t* xhv = x8 + (2 * dd) * NB * 64;
+            const half8_t* xlv = x8 + (2 * dd + 1) * NB * 64;
+            const half8_t ah = xhv[i * 64 + lane], al = xlv[i * 64 + lane];
+            const half8_t bh = xhv[j * 64 + lane], bl = xlv[j * 64 + lane];
+            g = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, g, 0, 0, 0);
+            g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, g, 0, 0, 0);
+            g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, g, 0, 0, 0);
+          }
+          const f32x4 nr = *(const f32x4*)&nrm[16 * i + 4 * grp];
+          const int col = 16 * j + c;
+          const float nc = nrm[col];
+          f32x4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * i + 4 * grp + r;
-          float dist = nr[r] + nc - 2.f * g[r];
-          dist = dist < 0.f ? 0.f : dist;  // clamp_min(0), NaN-propagating like torch
-          float v = s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);
-          if (row == col) v = diagval;
-          if (row >= N || col >= N) v = (row == col) ? 1.f : 0.f;
-          o[r] = -v;
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * i + 4 * grp + r;
+            float dist = nr[r] + nc - 2.f * g[r];
+            dist = dist < 0.f ? 0.f : dist;  // clamp_min(0), NaN-propagating like torch
+            float v = s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);
+            if (row == col) v = diagval;
+            if (row >= N || col >= N) v = (row == col) ? 1.f : 0.f;
+            o[r] = -v;
+          }
+          acc[s] = o;
+        } else {
+          const f32x4 rr = *(const f32x4*)&rv[16 * i + 4 * grp];
+          acc[s] = (c == 0) ? -rr : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        acc[s] = o;
-      } else {
-        const f32x4 rr = *(const f32x4*)&rv[16 * i + 4 * grp];
-        acc[s] = (c == 0) ? -rr : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
+    GPK_STAMP(1)
 
     float logdet = 0.f, sumz2 = 0.f;
-    int failed = 0;
-    for (int k = 0; k < NB; ++k) {
-      // ---- A(k): factor the diagonal tile --------------------------------
-      {
-        const int t = k * (k + 1) / 2 + k;
-        if (wave == t % W) {
-          f32x4 a = {0.f, 0.f, 0.f, 0.f};
-          const int slot = t / W;
+    if (tid == 0) flag[0] = 0;
+    if constexpr (STAMPS) {
+      if (tid == 0) ((unsigned long long*)(red + 4 * W + 4))[0] = 0;
+    }
+    barrier_lds();
+    // ---- A(0): factor diagonal tile (0,0) ---------------------------------
+    {
+      constexpr int t0 = plan_P<NB>(0);
+      if (wave == t0 % W) {
+        f32x4 a = acc[0];
 #pragma unroll
-          for (int s = 0; s < SLOTS; ++s)
-            if (s == slot) a = acc[s];
-          const int f = diag_factor(a, dsc, rinv, Lb, N, 16 * k, logdet);
-          if (f != 0 && lane == 0) flag[0] = 16 * k + f;
-        }
+        for (int s = 0; s < SLOTS; ++s)
+          if (s == t0 / W) a = acc[s];
+        const int f = diag_factor(a, dsc, wbuf, Lb, N, 0, logdet);
+        if (f != 0 && lane == 0) flag[0] = f;
       }
-      __syncthreads();
-      if (flag[0] != 0) { failed = flag[0]; break; }
+    }
+    barrier_lds();
+    int failed = flag[0];
+    GPK_STAMP(2)
+
+    for (int k = 0; k < NB && !failed; ++k) {
+      const int Pk = plan_P<NB>(k);
       // ---- B(k): panel TRSM  R_kj = R_kk^{-T} T_kj ----------------------
       {
-        const f32x4 q = *(const f32x4*)&rinv[lane * 4];
+        f32x4 q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = wbuf[(4 * grp + r) * 16 + c];
         const int wv = launder_s(wave);
 #pragma unroll
         for (int s = 0; s < SLOTS; ++s) {
-          int i, j;
-          slot_tile<NB, W>(wv, s, i, j);
-          if (i != k || j <= k) continue;
+          const int t = wv + W * s;
+          if (t <= Pk || t > Pk + NB - k) continue;
+          const int j = c_plan<NB>.ij[t] >> 8;
           const f32x4 rkj = mma_tn(q, acc[s], f32x4{0.f, 0.f, 0.f, 0.f});
           acc[s] = rkj;
           *(f32x4*)&panel[j * 256 + lane * 4] = rkj;
           if (j < NB) {
-            if (Lb != nullptr) {
-              // L[16j + c][16k + 4g + r] = R_kj[4g + r][c]; zero mirror block.
-              store_block(Lb, N, 16 * j + c, 16 * k + 4 * grp, rkj);
-            }
+            // L[16j + c][16k + 4g + r] = R_kj[4g + r][c]
+            if (Lb != nullptr) store4(Lb, N, 16 * j + c, 16 * k + 4 * grp, rkj);
           } else if (c == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) sumz2 = __builtin_fmaf(rkj[r], rkj[r], sumz2);
@@ -363,20 +534,81 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
           }
         }
       }
-      __syncthreads();
-      // ---- C(k): trailing update  -T_ij += R_ki^T R_kj ---------------------
+      barrier_lds();
+      GPK_STAMP(3)
+      // ---- C(k): trailing update  -T_ij += R_ki^T R_kj  (+ look-ahead A(k+1))
       {
-      const int wv = launder_s(wave);
+        const int wv = launder_s(wave);
+        // zero L's strictly-upper part of block-row k (streams out behind the MFMAs)
+        if (Lb != nullptr) {
+          constexpr int RPW = 16 / W;  // rows per wave
+          const int c0 = 16 * (k + 1);
 #pragma unroll
-      for (int s = 0; s < SLOTS; ++s) {
-        int i, j;
-        slot_tile<NB, W>(wv, s, i, j);
-        if (i <= k) continue;
-        const f32x4 pi = *(const f32x4*)&panel[i * 256 + lane * 4];
-        const f32x4 pj = *(const f32x4*)&panel[j * 256 + lane * 4];
-        acc[s] = mma_tn(pi, pj, acc[s]);
+          for (int q = 0; q < RPW; ++q) {
+            const int row = 16 * k + RPW * wv + q;
+            if (row < N) {
+              if ((N & 3) == 0) {
+                for (int cc = c0 + 4 * lane; cc < N; cc += 256)
+                  *(f32x4*)&Lb[(size_t)row * N + cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+              } else {
+                for (int cc = c0 + lane; cc < N; cc += 64) Lb[(size_t)row * N + cc] = 0.f;
+              }
+            }
+          }
+        }
+        const int nact = Pk > wv ? (Pk - wv + W - 1) / W : 0;  // active slots: s < nact
+        int dslot = -1;
+        if (k + 1 < NB) {
+          const int td = plan_P<NB>(k + 1);
+          if (wv == td % W) dslot = td / W;
+        }
+        if (dslot >= 0) {
+          // look-ahead: update (k+1,k+1) first, then factor it while the others
+          // are still busy with their trailing updates.
+          const f32x4 pk1 = *(const f32x4*)&panel[(k + 1) * 256 + lane * 4];
+          f32x4 a = acc[0];
+#pragma unroll
+          for (int s = 0; s < SLOTS; ++s)
+            if (s == dslot) { acc[s] = mma_tn(pk1, pk1, acc[s]); a = acc[s]; }
+          unsigned long long dt0 = 0;
+          if constexpr (STAMPS) dt0 = __builtin_amdgcn_s_memtime();
+          const int f = diag_factor(a, dsc, wbuf, Lb, N, 16 * (k + 1), logdet);
+          if (f != 0 && lane == 0) flag[0] = 16 * (k + 1) + f;
+          if constexpr (STAMPS) {
+            if (lane == 0) ((unsigned long long*)(red + 4 * W + 4))[0] += __builtin_amdgcn_s_memtime() - dt0;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < SLOTS; s += 2) {
+          if (s >= nact) continue;
+          const int p0 = c_plan<NB>.ij[wv + W * s];
+          f32x4 pi0 = *(const f32x4*)&panel[(p0 & 255) * 256 + lane * 4];
+          const f32x4 pj0 = *(const f32x4*)&panel[(p0 >> 8) * 256 + lane * 4];
+          if (s == dslot) pi0 = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (s + 1 < SLOTS) {
+            const bool a1 = (s + 1 < nact) && (s + 1 != dslot);
+            const int t1 = wv + W * (s + 1);
+            const int p1 = c_plan<NB>.ij[t1 < NT ? t1 : 0];
+            f32x4 pi1 = *(const f32x4*)&panel[(p1 & 255) * 256 + lane * 4];
+            const f32x4 pj1 = *(const f32x4*)&panel[(p1 >> 8) * 256 + lane * 4];
+            if (!a1) pi1 = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 d0 = acc[s], d1 = acc[s + 1];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(pi0[u], pj0[u], d0, 0, 0, 0);
+              d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(pi1[u], pj1[u], d1, 0, 0, 0);
+            }
+            acc[s] = d0;
+            acc[s + 1] = d1;
+          } else {
+            acc[s] = mma_tn(pi0, pj0, acc[s]);
+          }
+        }
       }
-      }
+      GPK_STAMP(6)
+      barrier_lds();
+      GPK_STAMP(4)
+      failed = flag[0];
     }
     if (!failed) {
       info_w = attempt > 0 ? -attempt : 0;
@@ -384,17 +616,27 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       if (lane == 0) red[wave] = logdet;
       const float z2 = wave_sum(sumz2);
       if (lane == 0) red[W + wave] = z2;
-      __syncthreads();
+      barrier_lds();
       if (tid == 0) {
         float ld = 0.f, zz = 0.f;
         for (int w = 0; w < W; ++w) { ld += red[w]; zz += red[W + w]; }
         mll[b] = -0.5f * (zz + ld + (float)N * kLog2Pi) / (float)N;
         info[b] = info_w;
       }
+      if constexpr (STAMPS) {
+        GPK_STAMP(5)
+        if (tid == 0) {
+          unsigned long long* o = stamps + (size_t)b * 16;
+          for (int q = 0; q < 8; ++q) o[q] = st_acc[q];
+          o[7] = ((unsigned long long*)(red + 4 * W + 4))[0];
+          o[8] = __builtin_amdgcn_s_memtime() - st_t0;
+          o[9] = __builtin_amdgcn_s_memrealtime() - st_rt0;
+        }
+      }
       return;
     }
     info_w = failed;
-    __syncthreads();
+    barrier_lds();
   }
   if (tid == 0) {
     info[b] = info_w;
@@ -402,33 +644,35 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   }
 }
 
-template <int NB>
-int launch_exact_nb(const GpkExactArgs& a, hipStream_t stream) {
-  constexpr int W = NB >= 6 ? 8 : 4;
+template <int NB, bool STAMPS>
+int launch_exact_nb(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
+  constexpr int W = 4;
   const int DC = (a.D + 15) / 16;
   const ExactLds lay = exact_lds_layout(NB, DC, W);
   const size_t lds = (size_t)lay.total * sizeof(float);
   if (DC * 16 > 64 * W || DC * 16 > 256) return -7;
   if (lds > 160 * 1024) return -7;
-  static bool attr_done = false;  // benign race: idempotent attribute set
-  if (!attr_done && lds > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)gpk_exact_kernel<NB, W>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_done = true;
-  }
-  hipLaunchKernelGGL((gpk_exact_kernel<NB, W>), dim3(a.B), dim3(64 * W), lds, stream,
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)gpk_exact_kernel<NB, W, STAMPS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((gpk_exact_kernel<NB, W, STAMPS>), dim3(a.B), dim3(64 * W), lds, stream,
                      a.X, a.y, a.hyp, a.n_ls, a.N, a.D, DC, a.jitter, a.max_tries,
-                     a.L, a.z, a.mll, a.info);
+                     a.L, a.z, a.mll, a.info, stamps);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
 
 }  // namespace
 
+int gpk_launch_exact_stamps(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
+  if ((a.N + 15) / 16 != 16) return -6;
+  return launch_exact_nb<16, true>(a, stamps, stream);
+}
+
 int gpk_launch_exact(const GpkExactArgs& a, hipStream_t stream) {
   const int NB = (a.N + 15) / 16;
   switch (NB) {
-#define GPK_CASE(nb) case nb: return launch_exact_nb<nb>(a, stream);
+#define GPK_CASE(nb) case nb: return launch_exact_nb<nb, false>(a, nullptr, stream);
     GPK_CASE(1) GPK_CASE(2) GPK_CASE(3) GPK_CASE(4) GPK_CASE(5) GPK_CASE(6)
     GPK_CASE(7) GPK_CASE(8) GPK_CASE(9) GPK_CASE(10) GPK_CASE(11) GPK_CASE(12)
     GPK_CASE(13) GPK_CASE(14) GPK_CASE(15) GPK_CASE(16)

@@ -17,3 +17,4 @@ struct GpkExactArgs {
 };
 
 int gpk_launch_exact(const GpkExactArgs& a, hipStream_t stream);
+int gpk_launch_exact_stamps(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream);

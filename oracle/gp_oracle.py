@@ -330,3 +330,50 @@ def deep_elbo(y, mean, var, noise, m, s, num_data, beta=1.0):
     ell = expected_log_prob(np.asarray(y, np.float64), np.asarray(mean, np.float64),
                             np.asarray(var, np.float64), float(noise)).sum(-1) / n
     return ell - kl_meanfield(m, s) / (num_data / beta)
+
+
+# ---------------------------------------------------------------------------
+# Torch-CPU restatement of the same exact-MLL path. GPyTorch itself dispatches
+# to exactly these torch CPU kernels (MKL/LAPACK): the _sq_dist GEMM form,
+# torch.linalg.cholesky_ex (+ the jitter ladder), torch.cholesky_solve for the
+# inverse quadratic (linear_operator CholLinearOperator.inv_quad_logdet) and
+# _chol_diag.pow(2).log().sum() for the log-determinant. Used as the timed CPU
+# baseline ("port") in bench.py and cross-checked against the NumPy oracle in
+# tests/test_oracle.py. CPU only.
+# ---------------------------------------------------------------------------
+def exact_mll_torch_cpu(X, y, lengthscale, outputscale, mean_constant, noise,
+                        jitter=1e-6, max_tries=3):
+    import torch
+    X = torch.as_tensor(X)
+    y = torch.as_tensor(y)
+    assert X.device.type == "cpu"
+    ls = torch.as_tensor(lengthscale, dtype=X.dtype)
+    x = X / ls
+    adj = x.mean(-2, keepdim=True)
+    x1 = x - adj
+    n1 = x1.pow(2).sum(-1, keepdim=True)
+    ones = torch.ones_like(n1)
+    res = torch.cat([-2.0 * x1, n1, ones], -1) @ torch.cat([x1, ones, n1], -1).transpose(-1, -2)
+    res.diagonal(dim1=-2, dim2=-1).fill_(0)
+    res.clamp_min_(0)
+    K = res.div_(-2).exp_().mul_(outputscale)
+    K.diagonal(dim1=-2, dim2=-1).add_(noise)
+    L, info = torch.linalg.cholesky_ex(K)
+    if bool(torch.any(info)):
+        Kp = K.clone()
+        prev = 0.0
+        for i in range(max_tries):
+            new = jitter * (10 ** i)
+            Kp.diagonal(dim1=-2, dim2=-1).add_(((info > 0).to(K.dtype) * (new - prev)).unsqueeze(-1))
+            prev = new
+            L, info = torch.linalg.cholesky_ex(Kp)
+            if not bool(torch.any(info)):
+                break
+        else:
+            raise NotPSDError("Matrix not positive definite after repeatedly adding jitter")
+    r = (y - mean_constant).unsqueeze(-1)
+    sol = torch.cholesky_solve(r, L)
+    inv_quad = (r * sol).sum((-1, -2))
+    logdet = L.diagonal(dim1=-2, dim2=-1).pow(2).log().sum(-1)
+    n = X.shape[-2]
+    return L, -0.5 * (inv_quad + logdet + n * LOG_2PI) / n

@@ -1,0 +1,30 @@
+"""Diagnostic: per-phase clocks of the exact kernel (STAMPS build), N=256 D=32."""
+import math, sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+from fine_grained_gaussian_process_forcasting_amd import _native, ops
+
+B, N, D = int(sys.argv[1]) if len(sys.argv) > 1 else 512, 256, 32
+dev = torch.device("cuda:0")
+X = (torch.randn(B, N, D) / math.sqrt(D)).to(dev)
+y = torch.randn(B, N).to(dev)
+LN2 = math.log(2)
+hyp = ops.pack_exact_hyper(LN2, LN2 + 1e-4, 0.0, LN2, dev)
+L = torch.empty(B, N, N, device=dev); mll = torch.empty(B, device=dev)
+info = torch.empty(B, dtype=torch.int32, device=dev)
+st = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+lib = _native.lib()
+for it in range(5):
+    rc = lib.gpk_debug_exact_stamps(X.data_ptr(), y.data_ptr(), hyp.data_ptr(), 1, B, N, D, 1e-6, 3,
+                                    L.data_ptr(), None, mll.data_ptr(), info.data_ptr(), st.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+torch.cuda.synchronize()
+s = st.cpu().numpy().astype(np.float64)
+names = ["prologue", "RBF", "A(0)+bar", "B(k)+bar", "barrier after C(k)", "final", "C(k) own work (wave0)", "diag_factor (lookahead) total"]
+tot = s[:, 8]
+print(f"B={B} total cycles: mean {tot.mean():.0f} min {tot.min():.0f} max {tot.max():.0f}")
+print(f"clock GHz (memtime/realtime): {np.mean(s[:, 8] / (s[:, 9] / 100e6)) / 1e9:.3f}")
+for i, n in enumerate(names):
+    print(f"  {n:22s} {s[:, i].mean():10.0f}  ({100 * s[:, i].mean() / tot.mean():5.1f}%)")
