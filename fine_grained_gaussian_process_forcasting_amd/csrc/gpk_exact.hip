@@ -73,7 +73,7 @@ __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
   o.nrm = o.xf + NB * (2 * DC32) * 256;
   o.rv = o.nrm + NB * 16;
   o.panel = o.rv + NB * 16;
-  o.wbuf = o.panel + (NB + 1) * 256;
+  o.wbuf = o.panel + 2 * (NB + 1) * 256;  // double-buffered R panel
   o.dsc = o.wbuf + 256;
   o.cpart = o.dsc + 256;
   o.red = o.cpart + 64 * W + 256;
@@ -261,6 +261,156 @@ GPK_DEVICE int diag_factor(const f32x4 a, float* dsc, float* wbuf, float* Lb, in
   return fail;
 }
 
+// ---------------------------------------------------------------------------
+// Worker-wave factorisation steps, unrolled at compile time. Step K's active
+// tile set is a slot PREFIX whose full part NALL(K) = P(K-1) / WK is a
+// compile-time constant, so the bulk trailing update is straight-line MFMA
+// code with in-place accumulators (no per-slot branches, no phi copies).
+// ---------------------------------------------------------------------------
+template <int I>
+struct IC { static constexpr int value = I; };
+
+template <int N, typename F>
+GPK_DEVICE void static_for_desc(F&& f) {
+  if constexpr (N > 0) {
+    f(IC<N - 1>{});
+    static_for_desc<N - 1>(f);
+  }
+}
+
+template <int A, int B, typename F>
+GPK_DEVICE void static_for_range(F&& f) {  // A..B inclusive, ascending
+  if constexpr (A <= B) {
+    f(IC<A>{});
+    static_for_range<A + 1, B>(f);
+  }
+}
+
+struct WorkerCtx {
+  float* panel;
+  float* dsc;
+  float* wbuf;
+  volatile int* vflag;
+  float* Lb;
+  float* zout;
+  int N, b, lane, c, grp, wv;
+  float sumz2;
+};
+
+template <int NB, int WK, int SLOTS, int K>
+GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
+  constexpr int Pk = plan_P<NB>(K);
+  constexpr int DS = Pk / WK, DW = Pk % WK;  // diagonal tile (K,K): slot / wave
+  // launder per step: keeps the per-slot plan loads / LDS addresses of this
+  // step from being hoisted (and pinned in registers) across all NB steps
+  const int wv = launder_s(x.wv);
+  int lane = x.lane;
+  asm volatile("" : "+v"(lane));
+  const int c = lane & 15, grp = lane >> 4;
+  const float* pprev = x.panel + ((K + 1) & 1) * (NB + 1) * 256;  // panel K-1
+  float* pcur = x.panel + (K & 1) * (NB + 1) * 256;                // panel K
+  auto handoff = [&](const f32x4& a) {
+    *(f32x4*)&x.dsc[lane * 4] = a;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0) x.vflag[1] = K;
+  };
+  auto upd = [&](f32x4& d, int s) {
+    const int p = c_plan<NB>.ij[wv + WK * s];
+    const f32x4 pi = *(const f32x4*)&pprev[(p & 255) * 256 + lane * 4];
+    const f32x4 pj = *(const f32x4*)&pprev[(p >> 8) * 256 + lane * 4];
+    d = mma_tn(pi, pj, d);
+  };
+  if constexpr (K == 0) {
+    if (wv == DW) handoff(acc[DS]);
+  } else {
+    // trailing update from panel K-1 over tiles with i >= K (t < P(K-1)),
+    // highest slot first so the row-K tiles -- (K,K) among them -- come first.
+    constexpr int Pkm1 = plan_P<NB>(K - 1);
+    constexpr int NALL = Pkm1 / WK;
+    if constexpr (NALL < SLOTS && (Pkm1 % WK) != 0) {
+      if (wv < Pkm1 % WK) {
+        upd(acc[NALL], NALL);
+        if constexpr (DS == NALL) {
+          if (wv == DW) handoff(acc[NALL]);
+        }
+      }
+    }
+    static_for_desc<NALL>([&](auto I) {
+      constexpr int s = decltype(I)::value;
+      upd(acc[s], s);
+      if constexpr (s == DS) {
+        if (wv == DW) handoff(acc[s]);
+      }
+    });
+  }
+  // zero L's strictly-upper part of block-row K (streams out behind the MFMAs)
+  if (x.Lb != nullptr) {
+    const int N = x.N;
+    const int c0 = 16 * (K + 1);
+    for (int q = wv; q < 16; q += WK) {
+      const int row = 16 * K + q;
+      if (row < N) {
+        if ((N & 3) == 0) {
+          for (int cc = c0 + 4 * lane; cc < N; cc += 256)
+            *(f32x4*)&x.Lb[(size_t)row * N + cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+          for (int cc = c0 + lane; cc < N; cc += 64) x.Lb[(size_t)row * N + cc] = 0.f;
+        }
+      }
+    }
+  }
+  // TRSM of the row-K off-diagonal tiles (P(K) < t <= P(K) + NB - K)
+  constexpr int TLO = Pk + 1, THI = Pk + NB - K;
+  constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
+  constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
+  const int tfirst = TLO + (((wv - TLO) % WK) + WK) % WK;
+  if (tfirst <= THI) {
+    while (x.vflag[2] < K) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    f32x4 q;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q[r] = x.wbuf[(4 * grp + r) * 16 + c];
+    static_for_range<SLO, SHI>([&](auto I) {
+      constexpr int s = decltype(I)::value;
+      const int t = wv + WK * s;
+      if (t >= TLO && t <= THI) {
+        const int j = c_plan<NB>.ij[t] >> 8;
+        const f32x4 rkj = mma_tn(q, acc[s], f32x4{0.f, 0.f, 0.f, 0.f});
+        acc[s] = rkj;
+        *(f32x4*)&pcur[j * 256 + lane * 4] = rkj;
+        if (j < NB) {
+          // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c]
+          if (x.Lb != nullptr) store4(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj);
+        } else if (c == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(rkj[r], rkj[r], x.sumz2);
+          if (x.zout != nullptr) {
+            const int row = 16 * K + 4 * grp;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (row + r < x.N) x.zout[(size_t)x.b * x.N + row + r] = rkj[r];
+          }
+        }
+      }
+    });
+  }
+}
+
+// Steps K..NB-1, one LDS barrier after each; stops after the barrier of a step
+// whose diagonal factorisation failed (the diagonal wave does the same).
+template <int NB, int WK, int SLOTS, int K>
+GPK_DEVICE int worker_steps(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
+  if constexpr (K < NB) {
+    worker_step<NB, WK, SLOTS, K>(acc, x);
+    barrier_lds();
+    const int failed = x.vflag[0];
+    if (failed) return failed;
+    return worker_steps<NB, WK, SLOTS, K + 1>(acc, x);
+  } else {
+    return 0;
+  }
+}
+
 template <int NB, int W, bool STAMPS = false>
 __global__ void __launch_bounds__(64 * W, (2 * W) / 4)
 gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
@@ -269,7 +419,8 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
                  float* __restrict__ zout, float* __restrict__ mll,
                  int* __restrict__ info, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int NT = ExactPlan<NB>::NT;
-  constexpr int SLOTS = (NT + W - 1) / W;
+  constexpr int WK = W - 1;                  // worker waves; wave WK is the diagonal wave
+  constexpr int SLOTS = (NT + WK - 1) / WK;
   constexpr int T = 64 * W;
   // Diagnostic-only phase clocks (STAMPS build): wave 0 lane 0 of each workgroup.
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0, st_t0 = 0, st_rt0 = 0;
@@ -422,26 +573,59 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   GPK_STAMP(0)
 
   const float nhalf_log2e = -0.72134752044448170f;  // -0.5 * log2(e)
-  float diagval = s2 + noise;
-  double jit_prev = 0.0;
-  int info_w = 0;
-  f32x4 acc[SLOTS];
-
-  for (int attempt = 0; attempt <= max_tries; ++attempt) {
-    if (attempt > 0) {
-      double p10 = 1.0;
-      for (int q = 1; q < attempt; ++q) p10 *= 10.0;
-      const double jn = jitter0 * p10;
-      diagval = diagval + (float)(jn - jit_prev);
-      jit_prev = jn;
+  int info_w = 0, failed = 0;
+  float logdet = 0.f, sumz2 = 0.f;
+  volatile int* vflag = flag;  // [0] fail column, [1] tile hand-off step, [2] factor-done step
+  // The diagonal wave and the worker waves run separate programs (so the
+  // workers' accumulator array is not live across the factorisation code);
+  // they meet at the same sequence of barriers: B0 per attempt, one per step,
+  // and B_retry after a failed attempt.
+  if (wave == WK) {
+    // ================================================= diagonal wave program
+    for (int attempt = 0; attempt <= max_tries; ++attempt) {
+      logdet = 0.f;
+      barrier_lds();  // B0
+      failed = 0;
+      for (int k = 0; k < NB && !failed; ++k) {
+        // ------------------------------------------------ diagonal wave
+        while (vflag[1] < k) __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        const f32x4 a = *(const f32x4*)&dsc[lane * 4];
+        unsigned long long dt0 = 0;
+        if constexpr (STAMPS) dt0 = __builtin_amdgcn_s_memtime();
+        const int f = diag_factor(a, dsc + 256, wbuf, Lb, N, 16 * k, logdet);
+        if constexpr (STAMPS) {
+          if (lane == 0) ((unsigned long long*)(red + 4 * W + 4))[0] += __builtin_amdgcn_s_memtime() - dt0;
+        }
+        if (f != 0 && lane == 0) vflag[0] = 16 * k + f;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (lane == 0) vflag[2] = k;
+        barrier_lds();
+        failed = vflag[0];
+      }
+      if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
+      info_w = failed;
+      barrier_lds();  // B_retry
     }
-
+  } else {
+    // ================================================= worker program
+    float diagval = s2 + noise;
+    double jit_prev = 0.0;
+    f32x4 acc[SLOTS];
+    for (int attempt = 0; attempt <= max_tries; ++attempt) {
+      if (attempt > 0) {
+        double p10 = 1.0;
+        for (int q = 1; q < attempt; ++q) p10 *= 10.0;
+        const double jn = jitter0 * p10;
+        diagval = diagval + (float)(jn - jit_prev);
+        jit_prev = jn;
+      }
     // ---- 4. RBF tiles straight into the accumulators (negated) -----------
     {
       const int wv = launder_s(wave);
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
-        const int t = wv + W * s;
+        const int t = wv + WK * s;
         if (t >= NT) continue;
         const int pk = c_plan<NB>.ij[t];
         const int i = pk & 255, j = pk >> 8;
@@ -479,166 +663,46 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         }
       }
     }
-    GPK_STAMP(1)
-
-    float logdet = 0.f, sumz2 = 0.f;
-    if (tid == 0) flag[0] = 0;
-    if constexpr (STAMPS) {
-      if (tid == 0) ((unsigned long long*)(red + 4 * W + 4))[0] = 0;
-    }
-    barrier_lds();
-    // ---- A(0): factor diagonal tile (0,0) ---------------------------------
-    {
-      constexpr int t0 = plan_P<NB>(0);
-      if (wave == t0 % W) {
-        f32x4 a = acc[0];
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s)
-          if (s == t0 / W) a = acc[s];
-        const int f = diag_factor(a, dsc, wbuf, Lb, N, 0, logdet);
-        if (f != 0 && lane == 0) flag[0] = f;
-      }
-    }
-    barrier_lds();
-    int failed = flag[0];
-    GPK_STAMP(2)
-
-    for (int k = 0; k < NB && !failed; ++k) {
-      const int Pk = plan_P<NB>(k);
-      // ---- B(k): panel TRSM  R_kj = R_kk^{-T} T_kj ----------------------
-      {
-        f32x4 q;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) q[r] = wbuf[(4 * grp + r) * 16 + c];
-        const int wv = launder_s(wave);
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s) {
-          const int t = wv + W * s;
-          if (t <= Pk || t > Pk + NB - k) continue;
-          const int j = c_plan<NB>.ij[t] >> 8;
-          const f32x4 rkj = mma_tn(q, acc[s], f32x4{0.f, 0.f, 0.f, 0.f});
-          acc[s] = rkj;
-          *(f32x4*)&panel[j * 256 + lane * 4] = rkj;
-          if (j < NB) {
-            // L[16j + c][16k + 4g + r] = R_kj[4g + r][c]
-            if (Lb != nullptr) store4(Lb, N, 16 * j + c, 16 * k + 4 * grp, rkj);
-          } else if (c == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sumz2 = __builtin_fmaf(rkj[r], rkj[r], sumz2);
-            if (zout != nullptr) {
-              const int row = 16 * k + 4 * grp;
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (row + r < N) zout[(size_t)b * N + row + r] = rkj[r];
-            }
-          }
-        }
-      }
-      barrier_lds();
-      GPK_STAMP(3)
-      // ---- C(k): trailing update  -T_ij += R_ki^T R_kj  (+ look-ahead A(k+1))
-      {
-        const int wv = launder_s(wave);
-        // zero L's strictly-upper part of block-row k (streams out behind the MFMAs)
-        if (Lb != nullptr) {
-          constexpr int RPW = 16 / W;  // rows per wave
-          const int c0 = 16 * (k + 1);
-#pragma unroll
-          for (int q = 0; q < RPW; ++q) {
-            const int row = 16 * k + RPW * wv + q;
-            if (row < N) {
-              if ((N & 3) == 0) {
-                for (int cc = c0 + 4 * lane; cc < N; cc += 256)
-                  *(f32x4*)&Lb[(size_t)row * N + cc] = f32x4{0.f, 0.f, 0.f, 0.f};
-              } else {
-                for (int cc = c0 + lane; cc < N; cc += 64) Lb[(size_t)row * N + cc] = 0.f;
-              }
-            }
-          }
-        }
-        const int nact = Pk > wv ? (Pk - wv + W - 1) / W : 0;  // active slots: s < nact
-        int dslot = -1;
-        if (k + 1 < NB) {
-          const int td = plan_P<NB>(k + 1);
-          if (wv == td % W) dslot = td / W;
-        }
-        if (dslot >= 0) {
-          // look-ahead: update (k+1,k+1) first, then factor it while the others
-          // are still busy with their trailing updates.
-          const f32x4 pk1 = *(const f32x4*)&panel[(k + 1) * 256 + lane * 4];
-          f32x4 a = acc[0];
-#pragma unroll
-          for (int s = 0; s < SLOTS; ++s)
-            if (s == dslot) { acc[s] = mma_tn(pk1, pk1, acc[s]); a = acc[s]; }
-          unsigned long long dt0 = 0;
-          if constexpr (STAMPS) dt0 = __builtin_amdgcn_s_memtime();
-          const int f = diag_factor(a, dsc, wbuf, Lb, N, 16 * (k + 1), logdet);
-          if (f != 0 && lane == 0) flag[0] = 16 * (k + 1) + f;
-          if constexpr (STAMPS) {
-            if (lane == 0) ((unsigned long long*)(red + 4 * W + 4))[0] += __builtin_amdgcn_s_memtime() - dt0;
-          }
-        }
-#pragma unroll
-        for (int s = 0; s < SLOTS; s += 2) {
-          if (s >= nact) continue;
-          const int p0 = c_plan<NB>.ij[wv + W * s];
-          f32x4 pi0 = *(const f32x4*)&panel[(p0 & 255) * 256 + lane * 4];
-          const f32x4 pj0 = *(const f32x4*)&panel[(p0 >> 8) * 256 + lane * 4];
-          if (s == dslot) pi0 = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (s + 1 < SLOTS) {
-            const bool a1 = (s + 1 < nact) && (s + 1 != dslot);
-            const int t1 = wv + W * (s + 1);
-            const int p1 = c_plan<NB>.ij[t1 < NT ? t1 : 0];
-            f32x4 pi1 = *(const f32x4*)&panel[(p1 & 255) * 256 + lane * 4];
-            const f32x4 pj1 = *(const f32x4*)&panel[(p1 >> 8) * 256 + lane * 4];
-            if (!a1) pi1 = f32x4{0.f, 0.f, 0.f, 0.f};
-            f32x4 d0 = acc[s], d1 = acc[s + 1];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(pi0[u], pj0[u], d0, 0, 0, 0);
-              d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(pi1[u], pj1[u], d1, 0, 0, 0);
-            }
-            acc[s] = d0;
-            acc[s + 1] = d1;
-          } else {
-            acc[s] = mma_tn(pi0, pj0, acc[s]);
-          }
-        }
-      }
-      GPK_STAMP(6)
-      barrier_lds();
-      GPK_STAMP(4)
-      failed = flag[0];
-    }
-    if (!failed) {
-      info_w = attempt > 0 ? -attempt : 0;
-      // ---- 5. reduce logdet / |z|^2 over waves, write the MLL -----------
-      if (lane == 0) red[wave] = logdet;
-      const float z2 = wave_sum(sumz2);
-      if (lane == 0) red[W + wave] = z2;
-      barrier_lds();
-      if (tid == 0) {
-        float ld = 0.f, zz = 0.f;
-        for (int w = 0; w < W; ++w) { ld += red[w]; zz += red[W + w]; }
-        mll[b] = -0.5f * (zz + ld + (float)N * kLog2Pi) / (float)N;
-        info[b] = info_w;
-      }
+      GPK_STAMP(1)
+      sumz2 = 0.f;
+      if (tid == 0) { flag[0] = 0; flag[1] = -1; flag[2] = -1; }
       if constexpr (STAMPS) {
-        GPK_STAMP(5)
-        if (tid == 0) {
-          unsigned long long* o = stamps + (size_t)b * 16;
-          for (int q = 0; q < 8; ++q) o[q] = st_acc[q];
-          o[7] = ((unsigned long long*)(red + 4 * W + 4))[0];
-          o[8] = __builtin_amdgcn_s_memtime() - st_t0;
-          o[9] = __builtin_amdgcn_s_memrealtime() - st_rt0;
-        }
+        if (tid == 0) ((unsigned long long*)(red + 4 * W + 4))[0] = 0;
       }
-      return;
+      barrier_lds();  // B0
+      GPK_STAMP(2)
+      WorkerCtx wx{panel, dsc, wbuf, vflag, Lb, zout, N, b, lane, c, grp, launder_s(wave), 0.f};
+      failed = worker_steps<NB, WK, SLOTS, 0>(acc, wx);
+      sumz2 = wx.sumz2;
+      GPK_STAMP(4)
+      if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
+      info_w = failed;
+      barrier_lds();  // B_retry
     }
-    info_w = failed;
-    barrier_lds();
   }
-  if (tid == 0) {
+  if (!failed) {
+    // ---- 5. reduce logdet / |z|^2 over waves, write the MLL ---------------
+    if (lane == 0) red[wave] = logdet;
+    const float z2 = wave_sum(sumz2);
+    if (lane == 0) red[W + wave] = z2;
+    barrier_lds();
+    if (tid == 0) {
+      float ld = 0.f, zz = 0.f;
+      for (int w = 0; w < W; ++w) { ld += red[w]; zz += red[W + w]; }
+      mll[b] = -0.5f * (zz + ld + (float)N * kLog2Pi) / (float)N;
+      info[b] = info_w;
+    }
+    if constexpr (STAMPS) {
+      GPK_STAMP(5)
+      if (tid == 0) {
+        unsigned long long* o = stamps + (size_t)b * 16;
+        for (int q = 0; q < 8; ++q) o[q] = st_acc[q];
+        o[7] = ((unsigned long long*)(red + 4 * W + 4))[0];
+        o[8] = __builtin_amdgcn_s_memtime() - st_t0;
+        o[9] = __builtin_amdgcn_s_memrealtime() - st_rt0;
+      }
+    }
+  } else if (tid == 0) {
     info[b] = info_w;
     mll[b] = __builtin_nanf("");
   }
@@ -646,7 +710,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
 
 template <int NB, bool STAMPS>
 int launch_exact_nb(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
-  constexpr int W = 4;
+  constexpr int W = NB >= 6 ? 8 : 4;
   const int DC = (a.D + 15) / 16;
   const ExactLds lay = exact_lds_layout(NB, DC, W);
   const size_t lds = (size_t)lay.total * sizeof(float);

@@ -22,7 +22,7 @@ for it in range(5):
     assert rc == 0
 torch.cuda.synchronize()
 s = st.cpu().numpy().astype(np.float64)
-names = ["prologue", "RBF", "A(0)+bar", "B(k)+bar", "barrier after C(k)", "final", "C(k) own work (wave0)", "diag_factor (lookahead) total"]
+names = ["prologue", "RBF", "B0 barrier", "trailing upd (wave0, last step)", "steps total (wave0)", "final", "-", "diag_factor total (diag wave)"]
 tot = s[:, 8]
 print(f"B={B} total cycles: mean {tot.mean():.0f} min {tot.min():.0f} max {tot.max():.0f}")
 print(f"clock GHz (memtime/realtime): {np.mean(s[:, 8] / (s[:, 9] / 100e6)) / 1e9:.3f}")
