@@ -28,6 +28,11 @@ SIGNATURES = {
     "gpk_exact_mll_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
+    "gpk_kzz_chol_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_float, c_double, c_int,
+                                 c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gpk_variational_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                    c_void_p, c_void_p]),
 }
 DEBUG_SIGNATURES = {
     "gpk_debug_exact_stamps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

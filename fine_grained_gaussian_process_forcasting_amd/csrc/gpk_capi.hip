@@ -41,6 +41,41 @@ int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp, int n_le
   return gpk_launch_exact(a, (hipStream_t)stream);
 }
 
+int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitter,
+                     double chol_jitter, int max_tries, double* L, double* Linv, int* info,
+                     void* stream) {
+  if (Z == nullptr) return -1;
+  if (hyp == nullptr) return -2;
+  if (M < 1 || M > 256) return -3;
+  if (D < 1 || D > 256) return -4;
+  if (max_tries < 0 || max_tries > 12) return -7;
+  if (L == nullptr) return -8;
+  if (Linv == nullptr) return -9;
+  if (info == nullptr) return -10;
+  GpkKzzArgs a{Z, hyp, M, D, jitter, chol_jitter, max_tries, L, Linv, info};
+  return gpk_launch_kzz(a, (hipStream_t)stream);
+}
+
+int gpk_variational_f32(const float* X, const float* Z, const double* Linv, const float* vmean,
+                        const float* vstd, const float* hyp, const float* y, int B, int N, int M,
+                        int D, float* mean, float* var, float* ell, void* stream) {
+  if (X == nullptr) return -1;
+  if (Z == nullptr) return -2;
+  if (Linv == nullptr) return -3;
+  if (vmean == nullptr) return -4;
+  if (vstd == nullptr) return -5;
+  if (hyp == nullptr) return -6;
+  if (B < 0) return -8;
+  if (N < 1) return -9;
+  if (M < 1 || M > 256) return -10;
+  if (D < 1 || D > 64) return -11;
+  if (mean == nullptr) return -12;
+  if (var == nullptr) return -13;
+  if (B == 0) return 0;
+  GpkVarArgs a{X, Z, Linv, vmean, vstd, hyp, y, B, N, M, D, mean, var, ell};
+  return gpk_launch_var(a, (hipStream_t)stream);
+}
+
 // Diagnostic (not part of the product ABI): same as gpk_exact_mll_f32 for N in
 // (240, 256], plus per-workgroup phase clocks (16 x u64 per window) in `stamps`.
 int gpk_debug_exact_stamps(const float* X, const float* y, const float* hyp, int n_lengthscale,

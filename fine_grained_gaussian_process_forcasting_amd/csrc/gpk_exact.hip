@@ -77,7 +77,7 @@ __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
   o.dsc = o.wbuf + 256;
   o.cpart = o.dsc + 256;
   o.red = o.cpart + 64 * W + 256;
-  o.total = o.red + 4 * W + 32;
+  o.total = o.red + 4 * W + 40;
   return o;
 }
 
@@ -198,30 +198,27 @@ GPK_DEVICE void diag_sweep(float (&v)[16]) {
   if constexpr (M < 15) diag_sweep<M + 1>(v);
 }
 
-// Factor one 16x16 diagonal tile T (given as -T in acc layout) in ONE wave.
+// Factor one 16x16 diagonal tile T in ONE wave (the diagonal wave).
 //   lanes  0-15 (column c): v[m] <- R[m][c]             (R^T R = T, upper)
 //   lanes 16-31 (column c): v[m] <- W[m][c], W = R^{-T}  (lower), started from I
 // from one instruction stream: at step m every lane does
 //   v[m] *= rsqrt(pivot);   v[i] -= R[m][i] * v[m]   (i > m)
-// with R[m][i] broadcast from R-lane i by readlane. A non-positive or NaN pivot
+// with R[m][i] broadcast from R-lane i by readlane. `tile` holds -T in acc
+// layout (written by the tile's owner). -W (transposed: wbuf[c*16+m] = -W[m][c])
+// is published FIRST and the factor-done flag raised; only then the L diagonal
+// block, the failure check and log|T| are produced. A non-positive or NaN pivot
 // turns every later diagonal entry into NaN, so the first failing column is
-// found once at the end from the diagonal of R.
-// Outputs: L diagonal block rows (global), -W transposed into wbuf
-// (wbuf[c*16 + m] = -W[m][c]), logdet += log|T|; returns 1-based fail column.
-GPK_DEVICE int diag_factor(const f32x4 a, float* dsc, float* wbuf, float* Lb, int N,
-                           int row0, float& logdet) {
-  // The factorisation is the critical path of the window: let this wave win
-  // issue arbitration over the MFMA-streaming waves sharing its SIMD.
-  __builtin_amdgcn_s_setprio(3);
+// found once from the diagonal of R.
+GPK_DEVICE int diag_factor(const float* tile, float* wbuf, volatile int* done_flag, int epoch,
+                           float* Lb, int N, int row0, float& logdet) {
+  __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));  // keep per-lane masks local to this call
   const int c = lane & 15, grp = lane >> 4;
-  *(f32x4*)&dsc[lane * 4] = a;
-  wave_lds_sync();
   float v[16];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const f32x4 t = *(const f32x4*)&dsc[(16 * g + c) * 4];
+    const f32x4 t = *(const f32x4*)&tile[(16 * g + c) * 4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = 4 * g + r;
@@ -229,6 +226,14 @@ GPK_DEVICE int diag_factor(const f32x4 a, float* dsc, float* wbuf, float* Lb, in
     }
   }
   diag_sweep<0>(v);
+  if (grp == 1) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *(f32x4*)&wbuf[c * 16 + 4 * g] = f32x4{-v[4 * g], -v[4 * g + 1], -v[4 * g + 2], -v[4 * g + 3]};
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (lane == 0) *done_flag = epoch;
+  __builtin_amdgcn_s_setprio(0);
   // diagonal of R, failure detection, log|T| = sum_c log R[c][c]^2
   float dg = v[0];
 #pragma unroll
@@ -242,11 +247,7 @@ GPK_DEVICE int diag_factor(const f32x4 a, float* dsc, float* wbuf, float* Lb, in
     for (int off = 8; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
     logdet += readlane_f(lg, 0) * 0.69314718055994531f;  // v_log_f32 is log2
   }
-  if (grp == 1) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *(f32x4*)&wbuf[c * 16 + 4 * g] = f32x4{-v[4 * g], -v[4 * g + 1], -v[4 * g + 2], -v[4 * g + 3]};
-  } else if (grp == 0) {
+  if (grp == 0) {
     // R lanes: zero below-diagonal garbage, write L[row0 + c][row0 + m] = R[m][c]
 #pragma unroll
     for (int i = 0; i < 16; ++i)
@@ -257,7 +258,6 @@ GPK_DEVICE int diag_factor(const f32x4 a, float* dsc, float* wbuf, float* Lb, in
         store4(Lb, N, row0 + c, row0 + 4 * g, f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
     }
   }
-  __builtin_amdgcn_s_setprio(0);
   return fail;
 }
 
@@ -294,6 +294,7 @@ struct WorkerCtx {
   float* Lb;
   float* zout;
   int N, b, lane, c, grp, wv;
+  int epoch0;  // hand-off / factor-done flag value of step 0 in this attempt
   float sumz2;
 };
 
@@ -312,7 +313,7 @@ GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   auto handoff = [&](const f32x4& a) {
     *(f32x4*)&x.dsc[lane * 4] = a;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) x.vflag[1] = K;
+    if (lane == 0) x.vflag[1] = x.epoch0 + K;
   };
   auto upd = [&](f32x4& d, int s) {
     const int p = c_plan<NB>.ij[wv + WK * s];
@@ -320,9 +321,7 @@ GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     const f32x4 pj = *(const f32x4*)&pprev[(p >> 8) * 256 + lane * 4];
     d = mma_tn(pi, pj, d);
   };
-  if constexpr (K == 0) {
-    if (wv == DW) handoff(acc[DS]);
-  } else {
+  if constexpr (K > 0) {
     // trailing update from panel K-1 over tiles with i >= K (t < P(K-1)),
     // highest slot first so the row-K tiles -- (K,K) among them -- come first.
     constexpr int Pkm1 = plan_P<NB>(K - 1);
@@ -365,7 +364,7 @@ GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
   const int tfirst = TLO + (((wv - TLO) % WK) + WK) % WK;
   if (tfirst <= THI) {
-    while (x.vflag[2] < K) __builtin_amdgcn_s_sleep(1);
+    while (x.vflag[2] < x.epoch0 + K) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     f32x4 q;
 #pragma unroll
@@ -403,7 +402,7 @@ GPK_DEVICE int worker_steps(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   if constexpr (K < NB) {
     worker_step<NB, WK, SLOTS, K>(acc, x);
     barrier_lds();
-    const int failed = x.vflag[0];
+    const int failed = x.vflag[3 + x.epoch0 / 32];
     if (failed) return failed;
     return worker_steps<NB, WK, SLOTS, K + 1>(acc, x);
   } else {
@@ -497,6 +496,15 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     }
   }
   barrier_lds();
+  // flags: [1] tile hand-off epoch, [2] factor-done epoch (epoch = 32*attempt + k,
+  // monotone, so nothing is ever reset), [3 + attempt] failing column of attempt
+  if (tid == 0) {
+    flag[0] = 0;
+    flag[1] = -1;
+    flag[2] = -1;
+    for (int q = 3; q < 16; ++q) flag[q] = 0;
+    if constexpr (STAMPS) ((unsigned long long*)(red + 4 * W + 24))[0] = 0;
+  }
   // ---- 2. centre columns by the mean over the N real rows (GPyTorch _sq_dist)
   {
     const int parts = T / DP;
@@ -578,34 +586,35 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   volatile int* vflag = flag;  // [0] fail column, [1] tile hand-off step, [2] factor-done step
   // The diagonal wave and the worker waves run separate programs (so the
   // workers' accumulator array is not live across the factorisation code);
-  // they meet at the same sequence of barriers: B0 per attempt, one per step,
-  // and B_retry after a failed attempt.
+  // they meet at the same sequence of barriers: one per factorisation step.
+  // Hand-offs inside a step go through LDS flags holding monotone epochs.
   if (wave == WK) {
     // ================================================= diagonal wave program
     for (int attempt = 0; attempt <= max_tries; ++attempt) {
       logdet = 0.f;
-      barrier_lds();  // B0
       failed = 0;
       for (int k = 0; k < NB && !failed; ++k) {
-        // ------------------------------------------------ diagonal wave
-        while (vflag[1] < k) __builtin_amdgcn_s_sleep(1);
+        const int epoch = 32 * attempt + k;
+        while (vflag[1] < epoch) __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        const f32x4 a = *(const f32x4*)&dsc[lane * 4];
         unsigned long long dt0 = 0;
-        if constexpr (STAMPS) dt0 = __builtin_amdgcn_s_memtime();
-        const int f = diag_factor(a, dsc + 256, wbuf, Lb, N, 16 * k, logdet);
         if constexpr (STAMPS) {
-          if (lane == 0) ((unsigned long long*)(red + 4 * W + 4))[0] += __builtin_amdgcn_s_memtime() - dt0;
+          dt0 = __builtin_amdgcn_s_memtime();
+          if (lane == 0 && k == 0) {
+            flag[16] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID
+            flag[17] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+          }
         }
-        if (f != 0 && lane == 0) vflag[0] = 16 * k + f;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        if (lane == 0) vflag[2] = k;
+        const int f = diag_factor(dsc, wbuf, vflag + 2, epoch, Lb, N, 16 * k, logdet);
+        if constexpr (STAMPS) {
+          if (lane == 0) ((unsigned long long*)(red + 4 * W + 24))[0] += __builtin_amdgcn_s_memtime() - dt0;
+        }
+        if (f != 0 && lane == 0) vflag[3 + attempt] = 16 * k + f;
         barrier_lds();
-        failed = vflag[0];
+        failed = vflag[3 + attempt];
       }
       if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
       info_w = failed;
-      barrier_lds();  // B_retry
     }
   } else {
     // ================================================= worker program
@@ -620,64 +629,68 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         diagval = diagval + (float)(jn - jit_prev);
         jit_prev = jn;
       }
-    // ---- 4. RBF tiles straight into the accumulators (negated) -----------
+    // ---- 4. RBF tiles straight into the accumulators (negated), highest slot
+    // first; the owner of (0,0) hands it to the diagonal wave as soon as it
+    // exists, so factorisation step 0 overlaps the rest of the Gram build.
     {
       const int wv = launder_s(wave);
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s) {
+      constexpr int P0 = plan_P<NB>(0);
+      static_for_desc<SLOTS>([&](auto I) {
+        constexpr int s = decltype(I)::value;
         const int t = wv + WK * s;
-        if (t >= NT) continue;
-        const int pk = c_plan<NB>.ij[t];
-        const int i = pk & 255, j = pk >> 8;
-        if (j < NB) {
-          f32x4 g = {0.f, 0.f, 0.f, 0.f};
-          const int DC32 = (DC + 1) / 2;
-          const half8_t* x8 = (const half8_t*)(smem + lay.xf);
-          for (int dd = 0; dd < DC32; ++dd) {
-            const half8_t* xhv = x8 + (2 * dd) * NB * 64;
-            const half8_t* xlv = x8 + (2 * dd + 1) * NB * 64;
-            const half8_t ah = xhv[i * 64 + lane], al = xlv[i * 64 + lane];
-            const half8_t bh = xhv[j * 64 + lane], bl = xlv[j * 64 + lane];
-            g = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, g, 0, 0, 0);
-            g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, g, 0, 0, 0);
-            g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, g, 0, 0, 0);
-          }
-          const f32x4 nr = *(const f32x4*)&nrm[16 * i + 4 * grp];
-          const int col = 16 * j + c;
-          const float nc = nrm[col];
-          f32x4 o;
+        if (t < NT) {
+          const int pk = c_plan<NB>.ij[t];
+          const int i = pk & 255, j = pk >> 8;
+          if (j < NB) {
+            f32x4 g = {0.f, 0.f, 0.f, 0.f};
+            const int DC32 = (DC + 1) / 2;
+            const half8_t* x8 = (const half8_t*)(smem + lay.xf);
+            for (int dd = 0; dd < DC32; ++dd) {
+              const half8_t* xhv = x8 + (2 * dd) * NB * 64;
+              const half8_t* xlv = x8 + (2 * dd + 1) * NB * 64;
+              const half8_t ah = xhv[i * 64 + lane], al = xlv[i * 64 + lane];
+              const half8_t bh = xhv[j * 64 + lane], bl = xlv[j * 64 + lane];
+              g = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, g, 0, 0, 0);
+              g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, g, 0, 0, 0);
+              g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, g, 0, 0, 0);
+            }
+            const f32x4 nr = *(const f32x4*)&nrm[16 * i + 4 * grp];
+            const int col = 16 * j + c;
+            const float nc = nrm[col];
+            f32x4 o;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = 16 * i + 4 * grp + r;
-            float dist = nr[r] + nc - 2.f * g[r];
-            dist = dist < 0.f ? 0.f : dist;  // clamp_min(0), NaN-propagating like torch
-            float v = s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);
-            if (row == col) v = diagval;
-            if (row >= N || col >= N) v = (row == col) ? 1.f : 0.f;
-            o[r] = -v;
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * i + 4 * grp + r;
+              float dist = nr[r] + nc - 2.f * g[r];
+              dist = dist < 0.f ? 0.f : dist;  // clamp_min(0), NaN-propagating like torch
+              float v = s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);
+              if (row == col) v = diagval;
+              if (row >= N || col >= N) v = (row == col) ? 1.f : 0.f;
+              o[r] = -v;
+            }
+            acc[s] = o;
+          } else {
+            const f32x4 rr = *(const f32x4*)&rv[16 * i + 4 * grp];
+            acc[s] = (c == 0) ? -rr : f32x4{0.f, 0.f, 0.f, 0.f};
           }
-          acc[s] = o;
-        } else {
-          const f32x4 rr = *(const f32x4*)&rv[16 * i + 4 * grp];
-          acc[s] = (c == 0) ? -rr : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-      }
+        if constexpr (s == P0 / WK) {
+          if (wv == P0 % WK) {
+            *(f32x4*)&dsc[lane * 4] = acc[s];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (lane == 0) vflag[1] = 32 * attempt;
+          }
+        }
+      });
     }
       GPK_STAMP(1)
       sumz2 = 0.f;
-      if (tid == 0) { flag[0] = 0; flag[1] = -1; flag[2] = -1; }
-      if constexpr (STAMPS) {
-        if (tid == 0) ((unsigned long long*)(red + 4 * W + 4))[0] = 0;
-      }
-      barrier_lds();  // B0
-      GPK_STAMP(2)
-      WorkerCtx wx{panel, dsc, wbuf, vflag, Lb, zout, N, b, lane, c, grp, launder_s(wave), 0.f};
+      WorkerCtx wx{panel, dsc, wbuf, vflag, Lb, zout, N, b, lane, c, grp, launder_s(wave), 32 * attempt, 0.f};
       failed = worker_steps<NB, WK, SLOTS, 0>(acc, wx);
       sumz2 = wx.sumz2;
       GPK_STAMP(4)
       if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
       info_w = failed;
-      barrier_lds();  // B_retry
     }
   }
   if (!failed) {
@@ -697,7 +710,10 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       if (tid == 0) {
         unsigned long long* o = stamps + (size_t)b * 16;
         for (int q = 0; q < 8; ++q) o[q] = st_acc[q];
-        o[7] = ((unsigned long long*)(red + 4 * W + 4))[0];
+        o[7] = ((unsigned long long*)(red + 4 * W + 24))[0];
+        o[10] = (unsigned)flag[16];
+        o[11] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+        o[12] = (unsigned)flag[17];
         o[8] = __builtin_amdgcn_s_memtime() - st_t0;
         o[9] = __builtin_amdgcn_s_memrealtime() - st_rt0;
       }

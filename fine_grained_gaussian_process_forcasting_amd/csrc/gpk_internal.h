@@ -18,3 +18,32 @@ struct GpkExactArgs {
 
 int gpk_launch_exact(const GpkExactArgs& a, hipStream_t stream);
 int gpk_launch_exact_stamps(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream);
+
+struct GpkKzzArgs {
+  const float* Z;      // (M, D)
+  const float* hyp;    // device: [outputscale, lengthscale[D]]
+  int M, D;
+  float jitter_var;    // VariationalStrategy jitter added to K_ZZ in fp32 (1e-4)
+  double jitter_chol;  // fp64 psd_safe_cholesky ladder base (1e-8)
+  int max_tries;
+  double* L;           // (M, M) out
+  double* Linv;        // (M, M) out
+  int* info;           // (1,) out
+};
+
+struct GpkVarArgs {
+  const float* X;      // (B, N, D)
+  const float* Z;      // (M, D)
+  const double* Linv;  // (M, M)
+  const float* vmean;  // (M,)
+  const float* vstd;   // (M,)
+  const float* hyp;    // device: [outputscale, noise, jitter, bias, weights[D], lengthscale[D]]
+  const float* y;      // (B, N) or nullptr
+  int B, N, M, D;
+  float* mean;         // (B, N)
+  float* var;          // (B, N)
+  float* ell;          // (B,) or nullptr: sum_i expected log prob
+};
+
+int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream);
+int gpk_launch_var(const GpkVarArgs& a, hipStream_t stream);

@@ -1,0 +1,317 @@
+// Variational (DeepGP) hot path for gfx950.
+//
+// Reference (oracle/gp_oracle.py::variational_forward):
+//   ToyDeepGPHiddenLayer / DeepGPp (denoising_model/DeepGP.py:15-99) driven through
+//   upstream variational/variational_strategy.py (whitened):
+//     K_ZZ + jitter (fp32) -> fp64 -> L = psd_safe_cholesky (fp64 ladder 1e-8 x10^i)
+//     A    = L^{-1} K_ZX        (fp64, cast to fp32)
+//     mean = A^T m + x w + b0   (LinearMean, DeepGP.py:42-45)
+//     var  = s2 + jitter + sum_m A_mi^2 (s_m^2 - 1), clamped >= 1e-6 (MVN.variance)
+//     ELL  = sum_i -0.5 [((y_i - mean_i)^2 + var_i)/noise + log noise + log 2pi]
+//
+// Two launches per call:
+//   gpk_kzz_kernel: ONE workgroup builds K_ZZ for the shared inducing points and
+//     factors it in fp64 together with L^{-1} (forward elimination of [K | I]);
+//     the reference does this b times (Z is expanded over the batch), we do it once.
+//   gpk_var_kernel: one workgroup per window; each wave owns 16-point column
+//     blocks, builds K_ZX columns in fp32 directly in the B-operand layout of
+//     v_mfma_f64_16x16x4_f64 and accumulates A = L^{-1} K_ZX in fp64 tiles
+//     (triangular L^{-1}: only k-steps p <= m), then reduces mean / var / ELL.
+#include "gpk_common.h"
+#include "gpk_internal.h"
+
+namespace {
+
+constexpr float kLog2PiF = 1.8378770664093453f;
+
+GPK_DEVICE void barrier_all() { __syncthreads(); }
+
+// ---------------------------------------------------------------------------
+// K_ZZ build + fp64 Cholesky + inverse, one workgroup. L and Linv are the
+// caller's output buffers (M x M fp64) and double as the working matrices.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
+               float jitter_var, double jitter_chol, int max_tries, double* __restrict__ L,
+               double* __restrict__ Linv, int* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  float* zt = vsm;                 // M x D   Z / l, centred
+  float* zn = zt + M * D;          // M       squared norms
+  float* cm = zn + M;              // D       column means
+  double* bc = (double*)(((uintptr_t)(cm + D) + 15) & ~(uintptr_t)15);  // broadcast slots
+  int* st = (int*)(bc + 4);
+  const int tid = threadIdx.x, T = blockDim.x;
+  const float s2 = hyp[0];
+  const float* ls = hyp + 1;  // D lengthscales (ARD, DeepGP.py:46-49)
+
+  for (int e = tid; e < M * D; e += T) zt[e] = Z[e] / ls[e % D];
+  barrier_all();
+  for (int d = tid; d < D; d += T) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += zt[m * D + d];
+    cm[d] = s / (float)M;
+  }
+  barrier_all();
+  for (int e = tid; e < M * D; e += T) zt[e] -= cm[e % D];
+  barrier_all();
+  for (int m = tid; m < M; m += T) {
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s = __builtin_fmaf(zt[m * D + d], zt[m * D + d], s);
+    zn[m] = s;
+  }
+  barrier_all();
+
+  int status = 0;
+  for (int attempt = 0; attempt <= max_tries; ++attempt) {
+    // (re)build A = K_ZZ + jitter (fp32) -> fp64 (+ fp64 ladder), B = I
+    for (int e = tid; e < M * M; e += T) {
+      const int i = e / M, j = e - i * M;
+      double a = 0.0;
+      if (j <= i) {
+        float dot = 0.f;
+        for (int d = 0; d < D; ++d) dot = __builtin_fmaf(zt[i * D + d], zt[j * D + d], dot);
+        float dist = zn[i] + zn[j] - 2.f * dot;
+        dist = dist < 0.f ? 0.f : dist;
+        float kv = s2 * __expf(-0.5f * dist);
+        if (i == j) kv = kv + jitter_var;
+        a = (double)kv;
+        if (i == j) {
+          // GPyTorch adds (jitter_new - jitter_prev) cumulatively to Aprime
+          double acc = a;
+          double prev = 0.0;
+          for (int q = 0; q < attempt; ++q) {
+            double p10 = 1.0;
+            for (int u = 0; u < q; ++u) p10 *= 10.0;
+            const double jn = jitter_chol * p10;
+            acc += jn - prev;
+            prev = jn;
+          }
+          a = acc;
+        }
+      }
+      L[e] = a;
+      Linv[e] = (i == j) ? 1.0 : 0.0;
+    }
+    if (tid == 0) st[0] = 0;
+    barrier_all();
+    int failed = 0;
+    for (int k = 0; k < M; ++k) {
+      if (tid == 0) {
+        const double piv = L[(size_t)k * M + k];
+        if (!(piv > 0.0)) { st[0] = k + 1; bc[0] = 1.0; }
+        else {
+          const double lkk = __builtin_sqrt(piv);
+          L[(size_t)k * M + k] = lkk;
+          bc[0] = 1.0 / lkk;
+        }
+      }
+      barrier_all();
+      if (st[0] != 0) { failed = st[0]; break; }
+      const double inv = bc[0];
+      for (int i = k + 1 + tid; i < M; i += T) L[(size_t)i * M + k] *= inv;
+      for (int j = tid; j <= k; j += T) Linv[(size_t)k * M + j] *= inv;
+      barrier_all();
+      // rank-1 update of the trailing lower triangle and of L^{-1}'s rows below k
+      const int R = M - k - 1;
+      const int nupd = R * (R + 1) / 2;
+      for (int e = tid; e < nupd; e += T) {
+        // e -> (ii, jj), 0 <= jj <= ii < R
+        int ii = (int)((__builtin_sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
+        while ((ii + 1) * (ii + 2) / 2 <= e) ++ii;
+        while (ii * (ii + 1) / 2 > e) --ii;
+        const int jj = e - ii * (ii + 1) / 2;
+        const int i = k + 1 + ii, j = k + 1 + jj;
+        L[(size_t)i * M + j] -= L[(size_t)i * M + k] * L[(size_t)j * M + k];
+      }
+      const int ninv = R * (k + 1);
+      for (int e = tid; e < ninv; e += T) {
+        const int ii = e / (k + 1), j = e - ii * (k + 1);
+        const int i = k + 1 + ii;
+        Linv[(size_t)i * M + j] -= L[(size_t)i * M + k] * Linv[(size_t)k * M + j];
+      }
+      barrier_all();
+    }
+    if (!failed) {
+      status = attempt > 0 ? -attempt : 0;
+      break;
+    }
+    status = failed;
+    barrier_all();
+  }
+  // zero the strictly-upper triangles
+  for (int e = tid; e < M * M; e += T) {
+    const int i = e / M, j = e - i * M;
+    if (j > i) { L[e] = 0.0; Linv[e] = 0.0; }
+  }
+  if (tid == 0) info[0] = status;
+}
+
+// ---------------------------------------------------------------------------
+// Batched predictive mean / variance / expected log-likelihood.
+// MB = number of 16-row blocks of the inducing dimension (M <= 16 MB),
+// DMAX = register capacity for one data point's coordinates (D <= DMAX).
+// ---------------------------------------------------------------------------
+template <int MB, int DMAX>
+__global__ void __launch_bounds__(256)
+gpk_var_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+               const double* __restrict__ Linv, const float* __restrict__ vmean,
+               const float* __restrict__ vstd, const float* __restrict__ hyp,
+               const float* __restrict__ y, int N, int M, int D, float* __restrict__ mean_out,
+               float* __restrict__ var_out, float* __restrict__ ell_out) {
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  float* zt = vsm;               // 16MB x D   centred Z / l (zero-padded rows)
+  float* cm = zt + 16 * MB * D;  // D
+  float* vm = cm + D;            // 16MB  variational mean
+  float* sm1 = vm + 16 * MB;     // 16MB  s^2 - 1
+  float* red = sm1 + 16 * MB;    // 8
+  const int tid = threadIdx.x, T = blockDim.x;
+  const int lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int wave = tid >> 6, NW = T >> 6;
+  const int b = blockIdx.x;
+  // hyp: [s2, noise, jitter, b0, w[D], ls[D]]
+  const float s2 = hyp[0], noise = hyp[1], jit = hyp[2], b0 = hyp[3];
+  const float* w = hyp + 4;
+  const float* ls = hyp + 4 + D;
+
+  for (int e = tid; e < 16 * MB * D; e += T) {
+    const int m = e / D;
+    zt[e] = (m < M) ? Z[e] / ls[e % D] : 0.f;
+  }
+  for (int m = tid; m < 16 * MB; m += T) {
+    vm[m] = (m < M) ? vmean[m] : 0.f;
+    const float sd = (m < M) ? vstd[m] : 1.f;
+    sm1[m] = sd * sd - 1.f;
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += T) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += zt[m * D + d];
+    cm[d] = s / (float)M;  // GPyTorch _sq_dist centres by x1 = Z
+  }
+  __syncthreads();
+  for (int e = tid; e < M * D; e += T) zt[e] -= cm[e % D];
+  __syncthreads();
+
+  const float* Xb = X + (size_t)b * N * D;
+  float ell_acc = 0.f;
+  const float log_noise = __logf(noise);
+  const float nhalf_log2e = -0.72134752044448170f;
+  const int NBLK = (N + 15) / 16;
+  for (int nb = wave; nb < NBLK; nb += NW) {
+    const int i = 16 * nb + c;
+    float xr[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)
+      xr[d] = (d < D && i < N) ? Xb[(size_t)i * D + d] / ls[d] - cm[d] : 0.f;
+    f64x4 acc[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int s = 0; s < 4 * MB; ++s) {
+      const int p = 4 * s + g;  // inducing point of this lane's B-operand row
+      float dist = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        if (d < D) {
+          const float df = zt[p * D + d] - xr[d];
+          dist = __builtin_fmaf(df, df, dist);
+        }
+      }
+      const float kv = (p < M && i < N) ? s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist) : 0.f;
+      const double kd = (double)kv;
+      const int mb0 = (4 * s) >> 4;  // L^{-1}[m][p] = 0 for m < p
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        if (mb >= mb0) {
+          const int m = 16 * mb + c;  // A-operand: lane holds Linv[m][4s + g]
+          const double a = (m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
+          acc[mb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, kd, acc[mb], 0, 0, 0);
+        }
+      }
+    }
+    // acc[mb][r] = A[16 mb + g + 4 r][16 nb + c]  (f64 16x16x4 C/D layout)
+    float mpart = 0.f, vpart = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * mb + g + 4 * r;
+        const float a32 = (float)acc[mb][r];
+        mpart = __builtin_fmaf(a32, vm[m], mpart);
+        vpart = __builtin_fmaf(a32 * a32, sm1[m], vpart);
+      }
+    }
+    mpart += __shfl_xor(mpart, 16, 64);
+    mpart += __shfl_xor(mpart, 32, 64);
+    vpart += __shfl_xor(vpart, 16, 64);
+    vpart += __shfl_xor(vpart, 32, 64);
+    if (g == 0 && i < N) {
+      float mu = b0;
+      float lin = 0.f;
+      for (int d = 0; d < D; ++d) lin = __builtin_fmaf(Xb[(size_t)i * D + d], w[d], lin);
+      const float mean_i = mpart + (lin + mu);
+      float var_i = s2 + jit + vpart;
+      var_i = var_i < 1e-6f ? 1e-6f : var_i;  // MVN.variance clamp (fp32 min_variance)
+      mean_out[(size_t)b * N + i] = mean_i;
+      var_out[(size_t)b * N + i] = var_i;
+      if (y != nullptr) {
+        const float dy = y[(size_t)b * N + i] - mean_i;
+        ell_acc += -0.5f * ((dy * dy + var_i) / noise + log_noise + kLog2PiF);
+      }
+    }
+  }
+  if (ell_out != nullptr) {
+    ell_acc = wave_sum(ell_acc);
+    if (lane == 0) red[wave] = ell_acc;
+    __syncthreads();
+    if (tid == 0) {
+      float s = 0.f;
+      for (int q = 0; q < NW; ++q) s += red[q];
+      ell_out[b] = s;
+    }
+  }
+}
+
+template <int MB, int DMAX>
+int launch_var(const GpkVarArgs& a, hipStream_t stream) {
+  const size_t lds = (size_t)(16 * MB * a.D + a.D + 2 * 16 * MB + 8) * sizeof(float);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)gpk_var_kernel<MB, DMAX>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((gpk_var_kernel<MB, DMAX>), dim3(a.B), dim3(256), lds, stream, a.X, a.Z,
+                     a.Linv, a.vmean, a.vstd, a.hyp, a.y, a.N, a.M, a.D, a.mean, a.var, a.ell);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+template <int DMAX>
+int launch_var_d(const GpkVarArgs& a, hipStream_t stream) {
+  switch ((a.M + 15) / 16) {
+#define GPK_VCASE(mb) case mb: return launch_var<mb, DMAX>(a, stream);
+    GPK_VCASE(1) GPK_VCASE(2) GPK_VCASE(3) GPK_VCASE(4) GPK_VCASE(5) GPK_VCASE(6)
+    GPK_VCASE(7) GPK_VCASE(8) GPK_VCASE(9) GPK_VCASE(10) GPK_VCASE(11) GPK_VCASE(12)
+    GPK_VCASE(13) GPK_VCASE(14) GPK_VCASE(15) GPK_VCASE(16)
+#undef GPK_VCASE
+    default: return -9;
+  }
+}
+
+}  // namespace
+
+int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
+  const size_t lds = (size_t)(a.M * a.D + a.M + a.D + 16) * sizeof(float) + 64;
+  if (lds > 160 * 1024) return -4;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)gpk_kzz_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(gpk_kzz_kernel, dim3(1), dim3(256), lds, stream, a.Z, a.hyp, a.M, a.D,
+                     a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.Linv, a.info);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int gpk_launch_var(const GpkVarArgs& a, hipStream_t stream) {
+  if (a.D <= 16) return launch_var_d<16>(a, stream);
+  if (a.D <= 32) return launch_var_d<32>(a, stream);
+  if (a.D <= 64) return launch_var_d<64>(a, stream);
+  return -8;
+}

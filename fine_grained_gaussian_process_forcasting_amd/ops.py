@@ -112,3 +112,97 @@ def check_cholesky_info(info: torch.Tensor, jitter: float, inputs=(), what: str 
 
 
 LOG_2PI = math.log(2 * math.pi)
+
+
+# ---------------------------------------------------------------------------
+# Variational (DeepGP) path
+# ---------------------------------------------------------------------------
+@dataclass
+class KzzFactor:
+    L: torch.Tensor      # (M, M) float64 lower Cholesky factor of K_ZZ + jitter
+    Linv: torch.Tensor   # (M, M) float64 L^{-1}
+    info: torch.Tensor   # (1,) int32
+
+
+def kzz_cholesky(Z: torch.Tensor, outputscale, lengthscale, jitter: float = 1e-4,
+                 chol_jitter: float = 1e-8, max_tries: int = 3,
+                 hyper: Optional[torch.Tensor] = None) -> KzzFactor:
+    """Shared inducing-point factorisation (include/gpk.h::gpk_kzz_chol_f64)."""
+    if Z.dim() != 2:
+        raise ValueError(f"Z must be (M, D), got {tuple(Z.shape)}")
+    _require_device(Z)
+    Z = Z.detach().contiguous().float()
+    M, D = Z.shape
+    dev = Z.device
+    if hyper is None:
+        hyper = torch.cat([_scalar_tensor(outputscale, dev)[:1],
+                           _scalar_tensor(lengthscale, dev).expand(D) if _scalar_tensor(lengthscale, dev).numel() == 1
+                           else _scalar_tensor(lengthscale, dev)]).contiguous()
+    if hyper.numel() != 1 + D:
+        raise ValueError(f"kzz hyper must hold 1 + D = {1 + D} values, got {hyper.numel()}")
+    L = torch.empty(M, M, device=dev, dtype=torch.float64)
+    Linv = torch.empty(M, M, device=dev, dtype=torch.float64)
+    info = torch.empty(1, device=dev, dtype=torch.int32)
+    rc = _native.lib().gpk_kzz_chol_f64(Z.data_ptr(), hyper.data_ptr(), M, D, float(jitter),
+                                        float(chol_jitter), int(max_tries), L.data_ptr(),
+                                        Linv.data_ptr(), info.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_kzz_chol_f64")
+    return KzzFactor(L, Linv, info)
+
+
+@dataclass
+class VariationalOut:
+    mean: torch.Tensor           # (B, N)
+    var: torch.Tensor            # (B, N)
+    ell: Optional[torch.Tensor]  # (B,) sum over N of the expected log likelihood
+
+
+def pack_variational_hyper(outputscale, noise, jitter, bias, weights, lengthscale, D, device):
+    ls = _scalar_tensor(lengthscale, device)
+    if ls.numel() == 1:
+        ls = ls.expand(D)
+    w = _scalar_tensor(weights, device).reshape(-1)
+    if w.numel() != D:
+        raise ValueError(f"LinearMean weights must have D={D} entries, got {w.numel()}")
+    return torch.cat([_scalar_tensor(outputscale, device)[:1], _scalar_tensor(noise, device)[:1],
+                      _scalar_tensor(jitter, device)[:1], _scalar_tensor(bias, device)[:1],
+                      w, ls]).contiguous()
+
+
+def variational_forward(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vmean: torch.Tensor,
+                        vstd: torch.Tensor, outputscale=None, noise=None, jitter=None, bias=None,
+                        weights=None, lengthscale=None, y: Optional[torch.Tensor] = None,
+                        hyper: Optional[torch.Tensor] = None) -> VariationalOut:
+    """Batched q(f) mean / variance (+ expected log likelihood sum when y is given)
+    for the whitened mean-field VariationalStrategy (include/gpk.h::gpk_variational_f32)."""
+    if X.dim() != 3:
+        raise ValueError(f"X must be (B, N, D), got {tuple(X.shape)}")
+    B, N, D = X.shape
+    M = Z.shape[0]
+    if Z.shape != (M, D):
+        raise ValueError(f"Z must be (M, {D}), got {tuple(Z.shape)}")
+    if Linv.shape != (M, M) or Linv.dtype != torch.float64:
+        raise ValueError("Linv must be (M, M) float64 from kzz_cholesky")
+    _require_device(X, Z, Linv, vmean, vstd)
+    dev = X.device
+    X = X.detach().contiguous().float()
+    Z = Z.detach().contiguous().float()
+    vmean = vmean.detach().contiguous().float().reshape(-1)
+    vstd = vstd.detach().contiguous().float().reshape(-1)
+    if hyper is None:
+        hyper = pack_variational_hyper(outputscale, noise, jitter, bias, weights, lengthscale, D, dev)
+    if y is not None:
+        if y.shape != (B, N):
+            raise ValueError(f"y must be (B, N) = {(B, N)}, got {tuple(y.shape)}")
+        _require_device(y)
+        y = y.detach().contiguous().float()
+    mean = torch.empty(B, N, device=dev, dtype=torch.float32)
+    var = torch.empty(B, N, device=dev, dtype=torch.float32)
+    ell = torch.empty(B, device=dev, dtype=torch.float32) if y is not None else None
+    rc = _native.lib().gpk_variational_f32(
+        X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
+        hyper.data_ptr(), y.data_ptr() if y is not None else None, B, N, M, D,
+        mean.data_ptr(), var.data_ptr(), ell.data_ptr() if ell is not None else None,
+        _stream_ptr(dev))
+    _native.check(rc, "gpk_variational_f32")
+    return VariationalOut(mean, var, ell)

@@ -61,6 +61,48 @@ int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp,
                       int max_tries, float* L, float* z, float* mll, int* info,
                       void* stream);
 
+/*
+ * Shared inducing-point factorisation of the whitened VariationalStrategy:
+ *   A    = K_ZZ + jitter (fp32 add, as K_ZZ.add_jitter), then upcast to fp64
+ *   L    = psd_safe_cholesky(A) with the fp64 ladder chol_jitter * 10^t
+ *   Linv = L^{-1}
+ * K_ZZ = s2 * exp(-0.5 ||(z_i - z_j)/l||^2) with ARD lengthscales.
+ *
+ * Replaces (reference): the per-window (b-fold redundant) fp64 Cholesky that
+ * VariationalStrategy._cholesky_factor runs for ToyDeepGPHiddenLayer
+ * (denoising_model/DeepGP.py:33-38, inducing points expanded to the batch by
+ * upstream _expand_inputs); SURVEY.md §8a rows a7/a9.
+ *
+ * Z   : (M, D) float (M <= 256)     hyp : device float[1 + D] = {s2, lengthscale[D]}
+ * L, Linv : (M, M) double out (lower, zero upper)   info : (1,) int out, codes as above
+ */
+int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitter,
+                     double chol_jitter, int max_tries, double* L, double* Linv, int* info,
+                     void* stream);
+
+/*
+ * Batched variational predictive distribution and expected log likelihood:
+ *   K_ZX = s2 * exp(-0.5 ||(z_m - x_i)/l||^2)       (fp32, per window)
+ *   A    = Linv @ K_ZX                              (fp64, then cast to fp32)
+ *   mean = A^T m + x @ w + b0                       (LinearMean)
+ *   var  = max(s2 + jitter + sum_m A_mi^2 (s_m^2 - 1), 1e-6)
+ *   ell  = sum_i -0.5 [((y_i - mean_i)^2 + var_i)/noise + log noise + log 2pi]
+ *
+ * Replaces (reference): DeepGPp.predict / ToyDeepGPHiddenLayer.__call__
+ * (denoising_model/DeepGP.py:51-99) via upstream VariationalStrategy.forward,
+ * DeepGPLayer.__call__, GaussianLikelihood.expected_log_prob as used by
+ * denoise_model_2.add_gp_noise (denoise_model_2.py:32-40) and the ELBO at
+ * forecast_denoising.py:86-89; SURVEY.md §8a rows a9-a14.
+ *
+ * X : (B, N, D) float (D <= 64)  Z : (M, D)  Linv : (M, M) double (gpk_kzz_chol_f64)
+ * vmean, vstd : (M,) float (MeanFieldVariationalDistribution mean / stddev)
+ * hyp : device float[4 + 2D] = {s2, noise, jitter, bias, weights[D], lengthscale[D]}
+ * y : (B, N) float or NULL;  mean, var : (B, N) float out;  ell : (B,) float out or NULL
+ */
+int gpk_variational_f32(const float* X, const float* Z, const double* Linv, const float* vmean,
+                        const float* vstd, const float* hyp, const float* y, int B, int N, int M,
+                        int D, float* mean, float* var, float* ell, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

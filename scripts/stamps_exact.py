@@ -22,9 +22,25 @@ for it in range(5):
     assert rc == 0
 torch.cuda.synchronize()
 s = st.cpu().numpy().astype(np.float64)
-names = ["prologue", "RBF", "B0 barrier", "trailing upd (wave0, last step)", "steps total (wave0)", "final", "-", "diag_factor total (diag wave)"]
+names = ["prologue", "RBF", "-", "-", "steps total (wave0)", "final", "-", "diag_factor total (diag wave)"]
 tot = s[:, 8]
 print(f"B={B} total cycles: mean {tot.mean():.0f} min {tot.min():.0f} max {tot.max():.0f}")
 print(f"clock GHz (memtime/realtime): {np.mean(s[:, 8] / (s[:, 9] / 100e6)) / 1e9:.3f}")
 for i, n in enumerate(names):
     print(f"  {n:22s} {s[:, i].mean():10.0f}  ({100 * s[:, i].mean() / tot.mean():5.1f}%)")
+
+hw = s[:, 10].astype(np.int64)
+hw0 = s[:, 11].astype(np.int64)
+simd = (hw >> 4) & 3
+cu = (hw >> 8) & 15
+sh = (hw >> 12) & 1
+se = (hw >> 13) & 7
+xcc = s[:, 12].astype(np.int64) & 15
+key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+from collections import defaultdict
+groups = defaultdict(list)
+for bb in range(B):
+    groups[int(key[bb])].append(int(simd[bb]))
+same = sum(1 for v in groups.values() if len(v) == 2 and v[0] == v[1])
+print(f"CUs hosting 2 WGs: {sum(1 for v in groups.values() if len(v) == 2)}; diag waves on the same SIMD: {same}; groups={len(groups)}")
+print("sample hw_id:", [hex(int(x)) for x in hw[:8]])
