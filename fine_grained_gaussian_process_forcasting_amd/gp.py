@@ -1,0 +1,401 @@
+"""gpytorch-free building blocks of the reference GP path, backed by the gfx950 kernels.
+
+Mirrors the GPyTorch 1.9.x objects the reference touches with
+the same module / parameter names, so the reference's call sites
+(denoising_model/DeepGP.py, GPModel.py, denoise_model_2.py, forecast_denoising.py:86-89,
+train.py:20) read the same and its state_dicts keep their keys:
+
+  settings.num_likelihood_samples        gpytorch.settings.num_likelihood_samples
+  Positive / GreaterThan                 gpytorch.constraints (softplus transform)
+  RBFKernel / ScaleKernel                gpytorch.kernels (raw_lengthscale, raw_outputscale)
+  ConstantMean / LinearMean              gpytorch.means
+  GaussianLikelihood                     gpytorch.likelihoods (noise_covar.raw_noise)
+  MultivariateNormal                     gpytorch.distributions (mean, variance clamp)
+  MeanFieldVariationalDistribution       gpytorch.variational
+  VariationalStrategy                    gpytorch.variational (whitened)
+  VariationalELBO / DeepApproximateMLL   gpytorch.mlls
+  ExactMarginalLogLikelihood             gpytorch.mlls
+
+All arithmetic of the hot path runs in libgpk.so (ops.py); torch is used for
+parameters, the tiny constrained-value transforms and elementwise glue on the
+device. Gradients: see ops_autograd.py.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import threading
+import warnings
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .errors import NumericalWarning
+
+LOG_2PI = math.log(2.0 * math.pi)
+
+
+# ---------------------------------------------------------------------------
+# settings (upstream gpytorch/settings.py)
+# ---------------------------------------------------------------------------
+class _Setting:
+    def __init__(self, default):
+        self._default = default
+        self._local = threading.local()
+
+    def value(self, dtype=None):
+        v = getattr(self._local, "stack", None)
+        if v:
+            return v[-1]
+        if isinstance(self._default, dict):
+            return self._default.get(dtype, self._default.get(None))
+        return self._default
+
+    @contextlib.contextmanager
+    def __call__(self, value):
+        stack = getattr(self._local, "stack", None)
+        if stack is None:
+            stack = self._local.stack = []
+        stack.append(value)
+        try:
+            yield
+        finally:
+            stack.pop()
+
+
+class settings:
+    """The gpytorch.settings used on this path (thread-local like GPyTorch's)."""
+    num_likelihood_samples = _Setting(10)          # train.py:20 sets 1
+    cholesky_jitter = _Setting({torch.float32: 1e-6, torch.float64: 1e-8, None: 1e-6})
+    cholesky_max_tries = _Setting(3)
+    variational_cholesky_jitter = _Setting({torch.float32: 1e-4, torch.float64: 1e-6, None: 1e-4})
+    min_variance = _Setting({torch.float32: 1e-6, torch.float64: 1e-10, None: 1e-6})
+    max_cholesky_size = _Setting(800)
+
+
+# ---------------------------------------------------------------------------
+# constraints (upstream constraints/constraints.py)
+# ---------------------------------------------------------------------------
+class Interval(nn.Module):
+    def __init__(self, lower_bound, upper_bound):
+        super().__init__()
+        self.register_buffer("lower_bound", torch.as_tensor(float(lower_bound)))
+        self.register_buffer("upper_bound", torch.as_tensor(float(upper_bound)))
+
+    def transform(self, raw):
+        return F.softplus(raw) + self.lower_bound.to(raw.dtype)
+
+    def inverse_transform(self, value):
+        v = torch.as_tensor(value) - self.lower_bound
+        return torch.where(v > 20, v, torch.log(torch.expm1(v)))
+
+
+class Positive(Interval):
+    def __init__(self):
+        super().__init__(0.0, math.inf)
+
+
+class GreaterThan(Interval):
+    def __init__(self, lower_bound):
+        super().__init__(lower_bound, math.inf)
+
+
+# ---------------------------------------------------------------------------
+# kernels / means (upstream kernels/rbf_kernel.py, scale_kernel.py, means/*)
+# ---------------------------------------------------------------------------
+class RBFKernel(nn.Module):
+    """Lengthscale holder of gpytorch.kernels.RBFKernel; shape (*batch, 1, ard or 1)."""
+
+    def __init__(self, ard_num_dims: Optional[int] = None, batch_shape=torch.Size([])):
+        super().__init__()
+        self.ard_num_dims = ard_num_dims
+        n = 1 if ard_num_dims is None else ard_num_dims
+        self.register_parameter("raw_lengthscale", nn.Parameter(torch.zeros(*batch_shape, 1, n)))
+        self.register_module("raw_lengthscale_constraint", Positive())
+
+    @property
+    def lengthscale(self):
+        return self.raw_lengthscale_constraint.transform(self.raw_lengthscale)
+
+
+class ScaleKernel(nn.Module):
+    def __init__(self, base_kernel: RBFKernel, batch_shape=torch.Size([]), ard_num_dims=None):
+        super().__init__()
+        self.base_kernel = base_kernel
+        self.register_parameter("raw_outputscale", nn.Parameter(torch.zeros(torch.Size(batch_shape))))
+        self.register_module("raw_outputscale_constraint", Positive())
+
+    @property
+    def outputscale(self):
+        return self.raw_outputscale_constraint.transform(self.raw_outputscale)
+
+
+class ConstantMean(nn.Module):
+    def __init__(self, batch_shape=torch.Size([])):
+        super().__init__()
+        self.register_parameter("constant", nn.Parameter(torch.zeros(*batch_shape, 1)))
+
+    def forward(self, x):
+        return self.constant.expand(*x.shape[:-1])
+
+
+class LinearMean(nn.Module):
+    def __init__(self, input_size: int, batch_shape=torch.Size([]), bias: bool = True):
+        super().__init__()
+        self.register_parameter("weights", nn.Parameter(torch.randn(*batch_shape, input_size, 1)))
+        if bias:
+            self.register_parameter("bias", nn.Parameter(torch.randn(*batch_shape, 1)))
+        else:
+            self.bias = None
+
+    def forward(self, x):
+        res = x.matmul(self.weights).squeeze(-1)
+        return res + self.bias if self.bias is not None else res
+
+
+# ---------------------------------------------------------------------------
+# distributions (upstream distributions/multivariate_normal.py)
+# ---------------------------------------------------------------------------
+class MultivariateNormal:
+    """Diagonal-query MVN of the hot path.
+
+    Holds what the reference reads from the GP output: ``mean`` and the marginal
+    ``variance`` (clamped at settings.min_variance with GPyTorch's
+    NumericalWarning), batch_shape / event_shape semantics and ``expand``. Exact-GP
+    priors also carry the window inputs so ``log_prob`` can run the fused kernel.
+    """
+
+    def __init__(self, mean: torch.Tensor, variance: Optional[torch.Tensor] = None,
+                 exact=None, added_noise=None):
+        self._mean = mean
+        self._variance = variance
+        self._exact = exact                # (X, kernel hyper) for exact-GP priors
+        self._added_noise = added_noise    # likelihood noise folded in by GaussianLikelihood
+
+    @property
+    def mean(self):
+        return self._mean
+
+    @property
+    def loc(self):
+        return self._mean
+
+    @property
+    def batch_shape(self):
+        return self._mean.shape[:-1]
+
+    @property
+    def event_shape(self):
+        return self._mean.shape[-1:]
+
+    @property
+    def variance(self):
+        if self._variance is None:
+            raise NotImplementedError("variance of an exact-GP prior is not materialised on this path")
+        var = self._variance
+        if self._added_noise is not None:
+            var = var + self._added_noise
+        min_var = settings.min_variance.value(var.dtype)
+        if bool((var < min_var).any()):
+            warnings.warn(f"Negative variance values detected. This is likely due to numerical "
+                          f"instabilities. Rounding negative variances up to {min_var}.",
+                          NumericalWarning)
+            var = var.clamp_min(min_var)
+        return var
+
+    @property
+    def stddev(self):
+        return self.variance.sqrt()
+
+    def expand(self, batch_size):
+        batch_size = torch.Size(batch_size)
+        mean = self._mean.expand(*batch_size, *self.event_shape)
+        var = self._variance.expand(*batch_size, *self.event_shape) if self._variance is not None else None
+        return MultivariateNormal(mean, var, self._exact, self._added_noise)
+
+    def add_noise(self, noise):
+        total = noise if self._added_noise is None else self._added_noise + noise
+        return MultivariateNormal(self._mean, self._variance, self._exact, total)
+
+    def log_prob(self, value: torch.Tensor) -> torch.Tensor:
+        """Exact-GP marginal log density (fused RBF + Cholesky + solve + logdet kernel)."""
+        if self._exact is None:
+            raise NotImplementedError("log_prob is provided for exact-GP outputs (GPModel.py)")
+        X, lengthscale, outputscale, constant = self._exact
+        noise = self._added_noise if self._added_noise is not None else torch.zeros((), device=X.device)
+        from .ops_autograd import exact_log_prob
+        n = X.shape[-2]
+        return exact_log_prob(X, value, lengthscale, outputscale, constant, noise) * n
+
+
+# ---------------------------------------------------------------------------
+# likelihood (upstream likelihoods/gaussian_likelihood.py, noise_models.py)
+# ---------------------------------------------------------------------------
+class HomoskedasticNoise(nn.Module):
+    def __init__(self, batch_shape=torch.Size([])):
+        super().__init__()
+        self.register_parameter("raw_noise", nn.Parameter(torch.zeros(*batch_shape, 1)))
+        self.register_module("raw_noise_constraint", GreaterThan(1e-4))
+
+    @property
+    def noise(self):
+        return self.raw_noise_constraint.transform(self.raw_noise)
+
+
+class GaussianLikelihood(nn.Module):
+    def __init__(self, batch_shape=torch.Size([])):
+        super().__init__()
+        self.noise_covar = HomoskedasticNoise(batch_shape)
+
+    @property
+    def noise(self):
+        return self.noise_covar.noise
+
+    def forward(self, function_dist: MultivariateNormal) -> MultivariateNormal:
+        """Marginal p(y) = q(f) + noise (only the diagonal is ever read on this path)."""
+        return function_dist.add_noise(self.noise.reshape(()))
+
+    def expected_log_prob(self, target: torch.Tensor, input: MultivariateNormal) -> torch.Tensor:
+        mean, variance = input.mean, input.variance
+        noise = self.noise.reshape(())
+        res = ((target - mean) ** 2 + variance) / noise + noise.log() + LOG_2PI
+        return res.mul(-0.5)
+
+
+# ---------------------------------------------------------------------------
+# variational distribution / strategy (upstream variational/*.py, whitened)
+# ---------------------------------------------------------------------------
+class MeanFieldVariationalDistribution(nn.Module):
+    def __init__(self, num_inducing_points: int, batch_shape=torch.Size([]), mean_init_std=1e-3):
+        super().__init__()
+        self.num_inducing_points = num_inducing_points
+        self.mean_init_std = mean_init_std
+        self.register_parameter("variational_mean", nn.Parameter(torch.zeros(*batch_shape, num_inducing_points)))
+        self.register_parameter("_variational_stddev", nn.Parameter(torch.ones(*batch_shape, num_inducing_points)))
+
+    def initialize_variational_distribution(self):
+        # prior N(0, I) (whitened): m = 0 + mean_init_std * randn, stddev = 1
+        with torch.no_grad():
+            self.variational_mean.data.zero_()
+            self.variational_mean.data.add_(torch.randn_like(self.variational_mean), alpha=self.mean_init_std)
+            self._variational_stddev.data.fill_(1.0)
+
+    def kl_divergence(self) -> torch.Tensor:
+        """KL(N(m, diag s^2) || N(0, I)) = 1/2 (sum s^2 + sum m^2 - M - sum log s^2)."""
+        m = self.variational_mean
+        s2 = self._variational_stddev.pow(2)
+        return 0.5 * (s2.sum(-1) + m.pow(2).sum(-1) - m.shape[-1] - s2.log().sum(-1))
+
+
+class VariationalStrategy(nn.Module):
+    """Whitened VariationalStrategy for one DeepGP layer (output_dims=None).
+
+    __call__(x) with x (..., N, D) returns q(f) as a MultivariateNormal (mean, var)
+    computed by gpk_kzz_chol_f64 (ONE fp64 factorisation of the shared K_ZZ per call)
+    + gpk_variational_f32 (batched fp64-MFMA L^{-1} K_ZX, mean, variance).
+    """
+
+    def __init__(self, model, inducing_points: torch.Tensor, variational_distribution,
+                 learn_inducing_locations: bool = True, jitter_val: Optional[float] = None):
+        super().__init__()
+        object.__setattr__(self, "model", model)
+        ip = inducing_points.clone()
+        if learn_inducing_locations:
+            self.register_parameter("inducing_points", nn.Parameter(ip))
+        else:
+            self.register_buffer("inducing_points", ip)
+        self._variational_distribution = variational_distribution
+        self.register_buffer("variational_params_initialized", torch.tensor(0))
+        self.register_buffer("updated_strategy", torch.tensor(True))
+        self.jitter_val = jitter_val
+
+    @property
+    def variational_distribution(self):
+        return self._variational_distribution
+
+    def _jitter(self, dtype):
+        return self.jitter_val if self.jitter_val is not None else settings.variational_cholesky_jitter.value(dtype)
+
+    def kl_divergence(self) -> torch.Tensor:
+        return self._variational_distribution.kl_divergence()
+
+    def __call__(self, x: torch.Tensor) -> MultivariateNormal:
+        if not int(self.variational_params_initialized.item()):
+            self._variational_distribution.initialize_variational_distribution()
+            self.variational_params_initialized.fill_(1)
+        model = self.model
+        batch = x.shape[:-2]
+        N, D = x.shape[-2:]
+        xf = x.reshape(-1, N, D)
+        from .ops_autograd import variational_predict
+        mean, var = variational_predict(
+            xf, self.inducing_points, self._variational_distribution.variational_mean,
+            self._variational_distribution._variational_stddev,
+            model.covar_module.outputscale, model.covar_module.base_kernel.lengthscale,
+            model.mean_module, self._jitter(x.dtype))
+        return MultivariateNormal(mean.reshape(*batch, N), var.reshape(*batch, N))
+
+
+# ---------------------------------------------------------------------------
+# marginal log likelihoods (upstream mlls/*.py)
+# ---------------------------------------------------------------------------
+class _ApproximateMarginalLogLikelihood(nn.Module):
+    def __init__(self, likelihood, model, num_data: int, beta: float = 1.0, combine_terms: bool = True):
+        super().__init__()
+        self.likelihood = likelihood
+        self.model = model
+        self.num_data = num_data
+        self.beta = beta
+        self.combine_terms = combine_terms
+
+    def _log_likelihood_term(self, approximate_dist_f, target, **kwargs):
+        raise NotImplementedError
+
+    def forward(self, approximate_dist_f: MultivariateNormal, target: torch.Tensor, **kwargs):
+        num_batch = approximate_dist_f.event_shape[0]
+        log_likelihood = self._log_likelihood_term(approximate_dist_f, target, **kwargs).div(num_batch)
+        kl_divergence = self.model.variational_strategy.kl_divergence().div(self.num_data / self.beta)
+        if self.combine_terms:
+            return log_likelihood - kl_divergence
+        return log_likelihood, kl_divergence, torch.zeros_like(log_likelihood)
+
+
+class VariationalELBO(_ApproximateMarginalLogLikelihood):
+    def _log_likelihood_term(self, variational_dist_f, target, **kwargs):
+        return self.likelihood.expected_log_prob(target, variational_dist_f).sum(-1)
+
+
+class DeepApproximateMLL(nn.Module):
+    def __init__(self, base_mll):
+        super().__init__()
+        self.base_mll = base_mll
+
+    def forward(self, approximate_dist_f, target, **kwargs):
+        return self.base_mll(approximate_dist_f, target, **kwargs).mean(0)
+
+
+class ExactMarginalLogLikelihood(nn.Module):
+    def __init__(self, likelihood, model):
+        super().__init__()
+        self.likelihood = likelihood
+        self.model = model
+
+    def forward(self, function_dist: MultivariateNormal, target: torch.Tensor, *params):
+        output = self.likelihood(function_dist)
+        res = output.log_prob(target)
+        num_data = function_dist.event_shape.numel()
+        return res.div(num_data)
+
+
+class _DeepGPVariationalStrategy:
+    """DeepGP.variational_strategy: KL summed over the sub-strategies of the model."""
+
+    def __init__(self, model):
+        self._model = model
+
+    def kl_divergence(self):
+        strategies = [m for m in self._model.modules() if isinstance(m, VariationalStrategy)]
+        return sum(s.kl_divergence().sum() for s in strategies)
