@@ -1,0 +1,69 @@
+"""CPU: libgpk.so loads, exports exactly the C ABI of include/gpk.h, validates arguments
+before touching the device, and the product path refuses CPU tensors (no fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "gpk.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gpk_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from fine_grained_gaussian_process_forcasting_amd import _native
+    lib = _native.lib()
+    names = _header_functions()
+    assert {"gpk_exact_mll_f32", "gpk_kzz_chol_f64", "gpk_variational_f32"} <= set(names)
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _native.SIGNATURES, f"{n} declared in gpk.h but not bound in _native.py"
+    assert lib.gpk_version() >= 100
+    assert lib.gpk_exact_max_n() == 256
+    assert b"success" == lib.gpk_strerror(0)
+
+
+def test_argument_validation_without_device():
+    from fine_grained_gaussian_process_forcasting_amd import _native
+    lib = _native.lib()
+    one = ctypes.c_void_p(16)  # never dereferenced: validation returns first
+    assert lib.gpk_exact_mll_f32(None, one, one, 1, 1, 8, 2, 1e-6, 3, None, None, one, one, None) == -1
+    assert lib.gpk_exact_mll_f32(one, one, one, 5, 1, 8, 2, 1e-6, 3, None, None, one, one, None) == -4
+    assert lib.gpk_exact_mll_f32(one, one, one, 1, 1, 300, 2, 1e-6, 3, None, None, one, one, None) == -6
+    assert lib.gpk_exact_mll_f32(one, one, one, 1, 1, 8, 2, -1.0, 3, None, None, one, one, None) == -8
+    assert lib.gpk_exact_mll_f32(one, one, one, 1, 0, 8, 2, 1e-6, 3, None, None, one, one, None) == 0
+    assert lib.gpk_kzz_chol_f64(one, one, 300, 4, 1e-4, 1e-8, 3, one, one, one, None) == -3
+    assert lib.gpk_variational_f32(one, one, one, one, one, one, None, 1, 8, 8, 65, one, one, None, None) == -11
+    assert b"N exceeds" in lib.gpk_strerror(-6)
+
+
+def test_ops_refuse_cpu_tensors():
+    from fine_grained_gaussian_process_forcasting_amd import ops
+    X = torch.zeros(2, 8, 3)
+    y = torch.zeros(2, 8)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.exact_mll(X, y, 1.0, 1.0, 0.0, 0.1)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.kzz_cholesky(torch.zeros(4, 3), 1.0, 1.0)
+
+
+def test_ops_shape_validation():
+    from fine_grained_gaussian_process_forcasting_amd import ops
+    with pytest.raises(ValueError):
+        ops.exact_mll(torch.zeros(8, 3), torch.zeros(8), 1.0, 1.0, 0.0, 0.1)
+    with pytest.raises(ValueError):
+        ops.exact_mll(torch.zeros(2, 8, 3), torch.zeros(2, 7), 1.0, 1.0, 0.0, 0.1)
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    from fine_grained_gaussian_process_forcasting_amd import _native
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "_LIB_PATH", "/nonexistent/libgpk.so")
+    with pytest.raises(_native.NativeLibraryError):
+        _native.lib()
