@@ -42,13 +42,18 @@ def _digest(paths, extra=""):
     return h.hexdigest()
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(OUT_DIR, exist_ok=True)
-    hdr_digest = _digest(headers(), " ".join(FLAGS))
+def build(force: bool = False, verbose: bool = True, defines=(), out_dir: str = OUT_DIR) -> str:
+    """Compile every csrc/*.hip for gfx950 and link libgpk.so into out_dir.
+    `defines` (e.g. ["GPK_SPLIT_UPDATE=0"]) and a non-default out_dir are for
+    A/B experiments only (load such a build with GPK_LIB=<path>)."""
+    os.makedirs(out_dir, exist_ok=True)
+    lib_path = os.path.join(out_dir, "libgpk.so")
+    flags = FLAGS + [f"-D{d}" for d in defines]
+    hdr_digest = _digest(headers(), " ".join(flags))
     objs = []
     jobs = []
     for src in sources():
-        obj = os.path.join(OUT_DIR, os.path.basename(src) + ".o")
+        obj = os.path.join(out_dir, os.path.basename(src) + ".o")
         stamp = obj + ".sha"
         dig = _digest([src], hdr_digest)
         objs.append(obj)
@@ -58,7 +63,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
     def compile_one(job):
         src, obj, stamp, dig = job
-        cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        cmd = [HIPCC, *flags, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
         if verbose:
             print("[build]", " ".join(os.path.basename(c) if c.startswith(ROOT) else c for c in cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -71,19 +76,21 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         list(ex.map(compile_one, jobs))
-    if jobs or not os.path.exists(LIB):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
+    if jobs or not os.path.exists(lib_path):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib_path + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        os.replace(LIB + ".tmp", LIB)
+        os.replace(lib_path + ".tmp", lib_path)
         if verbose:
-            print("[build] linked", os.path.relpath(LIB, ROOT), flush=True)
-    return LIB
+            print("[build] linked", os.path.relpath(lib_path, ROOT), flush=True)
+    return lib_path
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra -D for A/B builds")
+    ap.add_argument("--out-dir", default=OUT_DIR)
     args = ap.parse_args()
-    build(force=args.force)
+    build(force=args.force, defines=args.defines, out_dir=args.out_dir)

@@ -10,7 +10,9 @@ import ctypes
 import os
 import threading
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libgpk.so")
+# GPK_LIB overrides the in-tree build (A/B experiments with build_native.py --out-dir).
+_LIB_PATH = os.environ.get("GPK_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                       "libgpk.so")
 _lock = threading.Lock()
 _lib = None
 

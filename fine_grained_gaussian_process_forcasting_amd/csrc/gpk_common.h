@@ -29,6 +29,48 @@ GPK_DEVICE f32x4 mma_tn(const f32x4 q, const f32x4 p, f32x4 d) {
   return d;
 }
 
+// Split-f16 tiles. A factor tile R is ROUNDED to R^ = hi + lo (hi = f16(R),
+// lo = f16(R - hi): 22 significant bits, relative rounding <= 2^-22 for
+// |R| >= 2^-2; absolute <= 2^-25 below) and R^ is used everywhere the factor is
+// used -- written to L, and stored as two f16 planes (hi, lo: 64 lanes x half4
+// = 512 B each) for the trailing updates. The products hi.hi, hi.lo, lo.hi,
+// lo.lo are exact in the f16 MFMAs, so the update R^T R^ is accumulated like an
+// fp32 MFMA would with R^ as input: the factorisation stays self-consistent and
+// only the 22-bit storage of the factor costs accuracy (vs 24 bits in fp32).
+GPK_DEVICE f32x4 round_split_f16(const f32x4 v, half4_t& h, half4_t& l) {
+  f32x4 o;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    h[r] = (_Float16)v[r];
+    l[r] = (_Float16)(v[r] - (float)h[r]);
+    o[r] = (float)h[r] + (float)l[r];
+  }
+  return o;
+}
+GPK_DEVICE void store_split_planes(float* tile, int lane, const half4_t h, const half4_t l) {
+  *(half4_t*)&tile[2 * lane] = h;
+  *(half4_t*)&tile[128 + 2 * lane] = l;
+}
+
+// D += Q^T P for tiles stored as split planes (R^ = hi + lo exactly):
+//   K=32 MFMA with A = {Q.hi, Q.lo}, B = {P.hi, P.lo}:  Q.hi P.hi + Q.lo P.lo
+//   K=32 MFMA with A = {Q.hi, Q.lo}, B = {P.lo, P.hi}:  Q.hi P.lo + Q.lo P.hi
+// (k-order {4g+r | first half} ++ {second half}; every product is exact).
+GPK_DEVICE half8_t load_split_hl(const float* tile, int lane) {
+  const half4_t h = *(const half4_t*)&tile[2 * lane];
+  const half4_t l = *(const half4_t*)&tile[128 + 2 * lane];
+  return half8_t{h[0], h[1], h[2], h[3], l[0], l[1], l[2], l[3]};
+}
+GPK_DEVICE f32x4 mma_tn_split(const half8_t q_hl, const float* ptile, int lane, f32x4 d) {
+  const half4_t h = *(const half4_t*)&ptile[2 * lane];
+  const half4_t l = *(const half4_t*)&ptile[128 + 2 * lane];
+  const half8_t p_hl = {h[0], h[1], h[2], h[3], l[0], l[1], l[2], l[3]};
+  const half8_t p_lh = {l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q_hl, p_hl, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q_hl, p_lh, d, 0, 0, 0);
+  return d;
+}
+
 // Make this wave's LDS writes visible to its own other lanes before reading.
 GPK_DEVICE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -48,6 +90,16 @@ GPK_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+// Max over the wave, result uniform. ds_swizzle (immediate xor pattern) needs
+// no lane-address registers, unlike __shfl_xor.
+GPK_DEVICE float wave_max(float v) {
+#define GPK_SWZ_MAX(k) \
+  v = __builtin_fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), ((k) << 10) | 0x1f)));
+  GPK_SWZ_MAX(1) GPK_SWZ_MAX(2) GPK_SWZ_MAX(4) GPK_SWZ_MAX(8) GPK_SWZ_MAX(16)
+#undef GPK_SWZ_MAX
+  return __builtin_fmaxf(readlane_f(v, 0), readlane_f(v, 32));
 }
 
 GPK_DEVICE double wave_sum_d(double v) {

@@ -30,24 +30,31 @@
 #include "gpk_common.h"
 #include "gpk_internal.h"
 
+#ifndef GPK_SPLIT_UPDATE
+#define GPK_SPLIT_UPDATE 1
+#endif
+
 namespace {
 
 constexpr float kLog2Pi = 1.8378770664093453f;
 
 // Static tile -> (wave, slot) plan. Tiles are listed row-descending (i = NB-1
-// .. 0), j = i..NB inside a row (j = NB is the right-hand side), and dealt
-// cyclically: tile t -> wave t % W, slot t / W. Then
-//   tiles with i > k            = { t < P(k) },  P(k) = (NB-k)(NB-k+1)/2 - 1
+// .. 0), j = i..NB-1 inside a row, and dealt cyclically: tile t -> worker
+// wave t % WK, slot t / WK. Then
+//   tiles with i > k            = { t < P(k) },  P(k) = (NB-k)(NB-k-1)/2
 //   diagonal tile (k,k)         = t = P(k)
-//   off-diagonal row-k tiles    = P(k) < t <= P(k) + NB - k
+//   off-diagonal row-k tiles    = P(k) < t <= P(k) + NB - k - 1
+// The right-hand-side block column (y - c) is NOT in the plan: it has one live
+// column, so it is kept in LDS (rw) instead of 16 register tiles; block row i
+// of it belongs to worker i % WK.
 template <int NB>
 struct ExactPlan {
-  static constexpr int NT = NB * (NB + 1) / 2 + NB;
+  static constexpr int NT = NB * (NB + 1) / 2;
   int ij[NT];   // i | j << 8
   constexpr ExactPlan() : ij() {
     int t = 0;
     for (int i = NB - 1; i >= 0; --i)
-      for (int j = i; j <= NB; ++j) ij[t++] = i | (j << 8);
+      for (int j = i; j < NB; ++j) ij[t++] = i | (j << 8);
   }
 };
 
@@ -56,12 +63,12 @@ __constant__ ExactPlan<NB> c_plan = ExactPlan<NB>();
 
 template <int NB>
 GPK_DEVICE constexpr int plan_P(int k) {
-  return (NB - k) * (NB - k + 1) / 2 - 1;
+  return (NB - k) * (NB - k - 1) / 2;
 }
 
 struct ExactLds {
   // offsets in floats
-  int xf, xh, xl, nrm, rv, panel, wbuf, dsc, cpart, red, total;
+  int xf, xh, xl, nrm, rv, rw, panel, wbuf, dsc, cpart, red, total;
 };
 
 __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
@@ -72,7 +79,8 @@ __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
   o.xl = 0;
   o.nrm = o.xf + NB * (2 * DC32) * 256;
   o.rv = o.nrm + NB * 16;
-  o.panel = o.rv + NB * 16;
+  o.rw = o.rv + NB * 16;                 // working copy of -(y - c) (the RHS column)
+  o.panel = o.rw + NB * 16;
   o.wbuf = o.panel + 2 * (NB + 1) * 256;  // double-buffered R panel
   o.dsc = o.wbuf + 256;
   o.cpart = o.dsc + 256;
@@ -210,7 +218,7 @@ GPK_DEVICE void diag_sweep(float (&v)[16]) {
 // turns every later diagonal entry into NaN, so the first failing column is
 // found once from the diagonal of R.
 GPK_DEVICE int diag_factor(const float* tile, float* wbuf, volatile int* done_flag, int epoch,
-                           float* Lb, int N, int row0, float& logdet) {
+                           float* Lb, int N, int row0, float inv_sigma, float& logdet) {
   __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));  // keep per-lane masks local to this call
@@ -255,7 +263,8 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, volatile int* done_fl
     if (Lb != nullptr) {
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        store4(Lb, N, row0 + c, row0 + 4 * g, f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
+        store4(Lb, N, row0 + c, row0 + 4 * g,
+               f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]} * inv_sigma);
     }
   }
   return fail;
@@ -293,6 +302,7 @@ struct WorkerCtx {
   volatile int* vflag;
   float* Lb;
   float* zout;
+  float* rw;
   int N, b, lane, c, grp, wv;
   int epoch0;  // hand-off / factor-done flag value of step 0 in this attempt
   float sumz2;
@@ -317,9 +327,13 @@ GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   };
   auto upd = [&](f32x4& d, int s) {
     const int p = c_plan<NB>.ij[wv + WK * s];
+#if GPK_SPLIT_UPDATE
+    d = mma_tn_split(load_split_hl(pprev + (p & 255) * 256, lane), pprev + (p >> 8) * 256, lane, d);
+#else
     const f32x4 pi = *(const f32x4*)&pprev[(p & 255) * 256 + lane * 4];
     const f32x4 pj = *(const f32x4*)&pprev[(p >> 8) * 256 + lane * 4];
     d = mma_tn(pi, pj, d);
+#endif
   };
   if constexpr (K > 0) {
     // trailing update from panel K-1 over tiles with i >= K (t < P(K-1)),
@@ -358,40 +372,78 @@ GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       }
     }
   }
-  // TRSM of the row-K off-diagonal tiles (P(K) < t <= P(K) + NB - K)
-  constexpr int TLO = Pk + 1, THI = Pk + NB - K;
+  // right-hand side, block rows i >= K owned by this wave: rw_i += R_{K-1,i}^T z_{K-1}
+  // (rw holds -(y - c); only column 0 of the tile is live, so it round-trips
+  // through LDS on the c == 0 lanes)
+  const int rfirst = K + (((wv - K) % WK) + WK) % WK;
+  if constexpr (K > 0) {
+    for (int i = rfirst; i < NB; i += WK) {
+      f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
+      if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+#if GPK_SPLIT_UPDATE
+      d = mma_tn_split(load_split_hl(pprev + i * 256, lane), pprev + NB * 256, lane, d);
+#else
+      d = mma_tn(*(const f32x4*)&pprev[i * 256 + lane * 4], *(const f32x4*)&pprev[NB * 256 + lane * 4], d);
+#endif
+      if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
+    }
+  }
+  // TRSM of the row-K off-diagonal tiles (P(K) < t <= P(K) + NB - K - 1) and,
+  // by the owner of RHS block row K, of the right-hand side: z_K
+  constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
   constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
   constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
   const int tfirst = TLO + (((wv - TLO) % WK) + WK) % WK;
-  if (tfirst <= THI) {
+  const bool own_rhs = (rfirst == K);
+  if (tfirst <= THI || own_rhs) {
     while (x.vflag[2] < x.epoch0 + K) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     f32x4 q;
 #pragma unroll
     for (int r = 0; r < 4; ++r) q[r] = x.wbuf[(4 * grp + r) * 16 + c];
-    static_for_range<SLO, SHI>([&](auto I) {
-      constexpr int s = decltype(I)::value;
-      const int t = wv + WK * s;
-      if (t >= TLO && t <= THI) {
-        const int j = c_plan<NB>.ij[t] >> 8;
-        const f32x4 rkj = mma_tn(q, acc[s], f32x4{0.f, 0.f, 0.f, 0.f});
-        acc[s] = rkj;
-        *(f32x4*)&pcur[j * 256 + lane * 4] = rkj;
-        if (j < NB) {
-          // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c]
-          if (x.Lb != nullptr) store4(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj);
-        } else if (c == 0) {
+    // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
+    const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[30]);
+    if constexpr (THI >= TLO) {
+      static_for_range<SLO, SHI>([&](auto I) {
+        constexpr int s = decltype(I)::value;
+        const int t = wv + WK * s;
+        if (t >= TLO && t <= THI) {
+          const int j = c_plan<NB>.ij[t] >> 8;
+#if GPK_SPLIT_UPDATE
+          half4_t h, l;
+          const f32x4 rkj = round_split_f16(mma_tn(q, acc[s], f32x4{0.f, 0.f, 0.f, 0.f}), h, l);
+          store_split_planes(pcur + j * 256, lane, h, l);
+#else
+          const f32x4 rkj = mma_tn(q, acc[s], f32x4{0.f, 0.f, 0.f, 0.f});
+          *(f32x4*)&pcur[j * 256 + lane * 4] = rkj;
+#endif
+          // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
+          if (x.Lb != nullptr) store4(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
+        }
+      });
+    }
+    if (own_rhs) {
+      f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
+      if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+#if GPK_SPLIT_UPDATE
+      half4_t h, l;
+      const f32x4 zk = round_split_f16(mma_tn(q, d, f32x4{0.f, 0.f, 0.f, 0.f}), h, l);
+      store_split_planes(pcur + NB * 256, lane, h, l);
+#else
+      const f32x4 zk = mma_tn(q, d, f32x4{0.f, 0.f, 0.f, 0.f});
+      *(f32x4*)&pcur[NB * 256 + lane * 4] = zk;
+#endif
+      if (c == 0) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(rkj[r], rkj[r], x.sumz2);
-          if (x.zout != nullptr) {
-            const int row = 16 * K + 4 * grp;
+        for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
+        if (x.zout != nullptr) {
+          const int row = 16 * K + 4 * grp;
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (row + r < x.N) x.zout[(size_t)x.b * x.N + row + r] = rkj[r];
-          }
+          for (int r = 0; r < 4; ++r)
+            if (row + r < x.N) x.zout[(size_t)x.b * x.N + row + r] = zk[r];
         }
       }
-    });
+    }
   }
 }
 
@@ -441,6 +493,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   float* xf = smem + lay.xf;
   float* nrm = smem + lay.nrm;
   float* rv = smem + lay.rv;
+  float* rw = smem + lay.rw;
   float* panel = smem + lay.panel;
   float* wbuf = smem + lay.wbuf;
   float* dsc = smem + lay.dsc;
@@ -455,9 +508,26 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   const int DP = DC * 16;
   const int NP = NB * 16;
 
-  const float s2 = hyp[0];
+  const float s2u = hyp[0];
   const float noise = hyp[1];
   const float cmean = hyp[2];
+  // Factor sigma^2 * K_hat with sigma = 2^sh chosen so the diagonal lands in
+  // [2^13, 2^15): exact in binary (every fp32 result is the unscaled one times a
+  // power of two) and it puts the split-f16 trailing-update operands (|R_ij| <=
+  // sqrt(K_jj) <= 2^7.5) high in the f16 range, so lo parts stay normal down to
+  // entries 2^-9 of the largest. Undone on output: L = R'^T / sigma,
+  // log|K_hat| -= N log sigma^2, and z = L^{-1}(y - c) is unchanged when the
+  // right-hand side is scaled by sigma.
+  int sh = 0;
+  {
+    int e = 0;
+    const float d0 = s2u + noise;
+    if (d0 > 0.f && d0 < __builtin_huge_valf()) (void)__builtin_frexpf(d0, &e);
+    sh = 7 - (e >> 1);  // d0 * 2^(2 sh) in [2^13, 2^15)
+  }
+  const float sigma = __builtin_ldexpf(1.f, sh), sigma2 = sigma * sigma;
+  const float inv_sigma = __builtin_ldexpf(1.f, -sh);
+  const float s2 = s2u * sigma2;
   const float* Xb = X + (size_t)b * N * D;
   float* Lb = Lout ? Lout + (size_t)b * N * N : nullptr;
 
@@ -466,6 +536,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   // issued before any is consumed.
   {
     const int chunks = NP * DC;  // (row, 16-col chunk) pairs
+    float mx = 0.f;              // max |x / l| (bounds the centred values for the f16 split)
     for (int base = 0; base < chunks; base += T) {
       const int q = base + tid;
       float v[16];
@@ -488,12 +559,15 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         for (int e = 0; e < 16; ++e) {
           const int d = d0 + e;
           if (d < D && n < N) v[e] = v[e] / hyp[3 + (n_ls == 1 ? 0 : d)];
+          mx = __builtin_fmaxf(mx, __builtin_fabsf(v[e]));
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           *(f32x4*)&xf[frag_index(n, d0 + 4 * u, NB)] = f32x4{v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]};
       }
     }
+    mx = wave_max(mx);
+    if (lane == 0) red[wave] = mx;
   }
   barrier_lds();
   // flags: [1] tile hand-off epoch, [2] factor-done epoch (epoch = 32*attempt + k,
@@ -503,6 +577,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     flag[1] = -1;
     flag[2] = -1;
     for (int q = 3; q < 16; ++q) flag[q] = 0;
+    flag[30] = __builtin_bit_cast(int, inv_sigma);  // read back per step (SGPR budget)
     if constexpr (STAMPS) ((unsigned long long*)(red + 4 * W + 24))[0] = 0;
   }
   // ---- 2. centre columns by the mean over the N real rows (GPyTorch _sq_dist)
@@ -534,6 +609,20 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   {
     const float* cmean_d = cpart + 64 * W;
     _Float16* xh16 = (_Float16*)(smem + lay.xf);
+    // power-of-two scale 2^a for the f16 images: |x - mean| <= 2 max|x| < 2^(e+1)
+    // -> scaled magnitudes < 2^14 (f16 max 65504), lo parts normal down to 2^-2.
+    // The Gram comes back times 2^(2a) and is rescaled exactly in the RBF.
+    int a_sc = 0;
+    {
+      float m = 0.f;
+      for (int w = 0; w < W; ++w) m = __builtin_fmaxf(m, red[w]);
+      int e = 0;
+      if (m > 0.f && m < __builtin_huge_valf()) (void)__builtin_frexpf(m, &e);
+      a_sc = 13 - e;
+      a_sc = a_sc > 100 ? 100 : (a_sc < -100 ? -100 : a_sc);
+    }
+    const float xsc = __builtin_ldexpf(1.f, a_sc);
+    if (tid == 0) flag[31] = __builtin_bit_cast(int, __builtin_ldexpf(-2.f, -2 * a_sc));
     const int DC32 = (DC + 1) / 2;
     const int n = tid;  // NP <= 256 <= T: one row per thread
     float s = 0.f;
@@ -563,8 +652,9 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
           for (int r = 0; r < 4; ++r) {
             const float t = v[4 * u + r];
             s = __builtin_fmaf(t, t, s);
-            hi[r] = (_Float16)t;
-            lo[r] = (_Float16)(t - (float)hi[r]);
+            const float ts = t * xsc;
+            hi[r] = (_Float16)ts;
+            lo[r] = (_Float16)(ts - (float)hi[r]);
           }
           *(half4_t*)&xh16[hfrag_index(n, 32 * q + 4 * u, NB, 0)] = hi;
           *(half4_t*)&xh16[hfrag_index(n, 32 * q + 4 * u, NB, 1)] = lo;
@@ -574,7 +664,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     }
     if (n < NP) {
       nrm[n] = s;
-      rv[n] = (n < N) ? (y[(size_t)b * N + n] - cmean) : 0.f;
+      rv[n] = (n < N) ? (y[(size_t)b * N + n] - cmean) * sigma : 0.f;
     }
   }
   barrier_lds();
@@ -605,7 +695,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
             flag[17] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
           }
         }
-        const int f = diag_factor(dsc, wbuf, vflag + 2, epoch, Lb, N, 16 * k, logdet);
+        const int f = diag_factor(dsc, wbuf, vflag + 2, epoch, Lb, N, 16 * k, inv_sigma, logdet);
         if constexpr (STAMPS) {
           if (lane == 0) ((unsigned long long*)(red + 4 * W + 24))[0] += __builtin_amdgcn_s_memtime() - dt0;
         }
@@ -618,7 +708,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     }
   } else {
     // ================================================= worker program
-    float diagval = s2 + noise;
+    float diagval = (s2u + noise) * sigma2;
     double jit_prev = 0.0;
     f32x4 acc[SLOTS];
     for (int attempt = 0; attempt <= max_tries; ++attempt) {
@@ -626,22 +716,27 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         double p10 = 1.0;
         for (int q = 1; q < attempt; ++q) p10 *= 10.0;
         const double jn = jitter0 * p10;
-        diagval = diagval + (float)(jn - jit_prev);
+        diagval = diagval + (float)(jn - jit_prev) * sigma2;
         jit_prev = jn;
       }
+    // right-hand side: this wave's block rows of rw <- -(y - c) (fresh per attempt)
+    for (int i = wave; i < NB; i += WK)
+      if (lane < 16) rw[16 * i + lane] = -rv[16 * i + lane];
     // ---- 4. RBF tiles straight into the accumulators (negated), highest slot
     // first; the owner of (0,0) hands it to the diagonal wave as soon as it
     // exists, so factorisation step 0 overlaps the rest of the Gram build.
     {
       const int wv = launder_s(wave);
       constexpr int P0 = plan_P<NB>(0);
+      // -2 / 2^(2a): undoes the f16 image scale on the Gram (uniform -> SGPR)
+      const float gm2 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane((int)vflag[31]));
       static_for_desc<SLOTS>([&](auto I) {
         constexpr int s = decltype(I)::value;
         const int t = wv + WK * s;
         if (t < NT) {
           const int pk = c_plan<NB>.ij[t];
           const int i = pk & 255, j = pk >> 8;
-          if (j < NB) {
+          {
             f32x4 g = {0.f, 0.f, 0.f, 0.f};
             const int DC32 = (DC + 1) / 2;
             const half8_t* x8 = (const half8_t*)(smem + lay.xf);
@@ -661,7 +756,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int row = 16 * i + 4 * grp + r;
-              float dist = nr[r] + nc - 2.f * g[r];
+              float dist = __builtin_fmaf(gm2, g[r], nr[r] + nc);
               dist = dist < 0.f ? 0.f : dist;  // clamp_min(0), NaN-propagating like torch
               float v = s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);
               if (row == col) v = diagval;
@@ -669,9 +764,6 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
               o[r] = -v;
             }
             acc[s] = o;
-          } else {
-            const f32x4 rr = *(const f32x4*)&rv[16 * i + 4 * grp];
-            acc[s] = (c == 0) ? -rr : f32x4{0.f, 0.f, 0.f, 0.f};
           }
         }
         if constexpr (s == P0 / WK) {
@@ -685,7 +777,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     }
       GPK_STAMP(1)
       sumz2 = 0.f;
-      WorkerCtx wx{panel, dsc, wbuf, vflag, Lb, zout, N, b, lane, c, grp, launder_s(wave), 32 * attempt, 0.f};
+      WorkerCtx wx{panel, dsc, wbuf, vflag, Lb, zout, rw, N, b, lane, c, grp, launder_s(wave), 32 * attempt, 0.f};
       failed = worker_steps<NB, WK, SLOTS, 0>(acc, wx);
       sumz2 = wx.sumz2;
       GPK_STAMP(4)
@@ -702,6 +794,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     if (tid == 0) {
       float ld = 0.f, zz = 0.f;
       for (int w = 0; w < W; ++w) { ld += red[w]; zz += red[W + w]; }
+      ld -= (float)(2 * sh) * (float)N * 0.69314718055994531f;  // - N log sigma^2
       mll[b] = -0.5f * (zz + ld + (float)N * kLog2Pi) / (float)N;
       info[b] = info_w;
     }

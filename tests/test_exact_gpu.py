@@ -163,3 +163,29 @@ def test_exact_full_size_bench_config(cuda_device):
     # determinism: a second launch is bitwise identical
     out2 = _run(cuda_device, X, y, LN2, LN2, 0.0, NOISE0)
     assert torch.equal(out.L, out2.L) and torch.equal(out.mll, out2.mll)
+
+
+@pytest.mark.parametrize("N,D,ls,s2,noise,scale,offset", [
+    (256, 32, LN2, LN2, NOISE0, None, 0.0),
+    (256, 2, 1.0, 1.0, 0.05, None, 0.0),        # cond ~ 3e3
+    (256, 1, 1.0, 1.0, 0.01, None, 0.0),        # cond ~ 2e4
+    (256, 32, 2.0, 1e-3, 1e-4, None, 0.0),      # tiny hyper-parameters (scaling path)
+    (256, 32, 0.5, 3e3, 10.0, None, 0.0),       # large hyper-parameters
+    (256, 8, 300.0, 1.0, 0.1, 0.01, 1e3),       # unnormalised inputs (f16 image scaling)
+])
+def test_exact_accuracy_vs_fp32_lapack(cuda_device, N, D, ls, s2, noise, scale, offset):
+    """The kernel stays within a small factor of an fp32 LAPACK Cholesky of the same
+    matrices (the reference's own arithmetic), both measured against fp64."""
+    B = 4
+    g = torch.Generator().manual_seed(N * 7 + D)
+    X = torch.randn(B, N, D, generator=g) / (np.sqrt(D) if scale is None else scale) + offset
+    y = torch.randn(B, N, generator=torch.Generator().manual_seed(N * 7 + D + 1))
+    out = _run(cuda_device, X, y, ls, s2, 0.0, noise)
+    ref = O.exact_mll(X.double().numpy(), y.double().numpy(), ls, s2, 0.0, noise)
+    r32 = O.exact_mll(X.numpy(), y.numpy(), ls, s2, 0.0, noise, dtype=np.float32)
+    for got, want, f32 in ((out.L, ref.L, r32.L), (out.z, ref.z, r32.z)):
+        e = _rel_fro(got.cpu().double().numpy(), want).max()
+        e32 = _rel_fro(f32.astype(np.float64), want).max()
+        assert e <= max(4.0 * e32, 1e-6), (e, e32)
+    em = np.max(np.abs(out.mll.cpu().double().numpy() - ref.mll) / np.abs(ref.mll))
+    assert em <= 1e-4
