@@ -71,6 +71,13 @@ GPK_DEVICE f32x4 mma_tn_split(const half8_t q_hl, const float* ptile, int lane, 
   return d;
 }
 
+// Volatile LDS words used as intra-workgroup flags. Typed in the LDS address
+// space so every access is a ds_read / ds_write (lgkmcnt only): through a generic
+// pointer a volatile access stays a FLAT op, whose s_waitcnt vmcnt(0) would also
+// drain every outstanding global store of the wave.
+typedef __attribute__((address_space(3))) volatile int lds_vint;
+GPK_DEVICE lds_vint* as_lds_flags(int* p) { return (lds_vint*)p; }
+
 // Make this wave's LDS writes visible to its own other lanes before reading.
 GPK_DEVICE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

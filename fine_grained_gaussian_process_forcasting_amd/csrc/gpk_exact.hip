@@ -217,7 +217,7 @@ GPK_DEVICE void diag_sweep(float (&v)[16]) {
 // block, the failure check and log|T| are produced. A non-positive or NaN pivot
 // turns every later diagonal entry into NaN, so the first failing column is
 // found once from the diagonal of R.
-GPK_DEVICE int diag_factor(const float* tile, float* wbuf, volatile int* done_flag, int epoch,
+GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* done_flag, int epoch,
                            float* Lb, int N, int row0, float inv_sigma, float& logdet) {
   __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration
   int lane = threadIdx.x & 63;
@@ -299,7 +299,7 @@ struct WorkerCtx {
   float* panel;
   float* dsc;
   float* wbuf;
-  volatile int* vflag;
+  lds_vint* vflag;
   float* Lb;
   float* zout;
   float* rw;
@@ -673,7 +673,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   const float nhalf_log2e = -0.72134752044448170f;  // -0.5 * log2(e)
   int info_w = 0, failed = 0;
   float logdet = 0.f, sumz2 = 0.f;
-  volatile int* vflag = flag;  // [0] fail column, [1] tile hand-off step, [2] factor-done step
+  lds_vint* vflag = as_lds_flags(flag);  // [0] fail column, [1] tile hand-off step, [2] factor-done step
   // The diagonal wave and the worker waves run separate programs (so the
   // workers' accumulator array is not live across the factorisation code);
   // they meet at the same sequence of barriers: one per factorisation step.
