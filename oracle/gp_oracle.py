@@ -377,3 +377,71 @@ def exact_mll_torch_cpu(X, y, lengthscale, outputscale, mean_constant, noise,
     logdet = L.diagonal(dim1=-2, dim2=-1).pow(2).log().sum(-1)
     n = X.shape[-2]
     return L, -0.5 * (inv_quad + logdet + n * LOG_2PI) / n
+
+
+# ---------------------------------------------------------------------------
+# Gradients of the hot path (what torch autograd produces when train.py:166
+# back-propagates through GPyTorch). Restated in torch fp64 autograd on the CPU
+# with direct-difference distances (mathematically identical to the centred GEMM
+# form away from the clamp); pinned against central finite differences of the
+# NumPy forward above (tests/test_oracle.py). TEST INFRASTRUCTURE ONLY.
+# ---------------------------------------------------------------------------
+def _t64(a, grad=True):
+    import torch
+    return torch.tensor(np.array(a, dtype=np.float64), requires_grad=grad)
+
+
+def _rbf_t(a, b, ls, s2):
+    import torch
+    d = (((a.unsqueeze(-2) - b.unsqueeze(-3)) / ls) ** 2).sum(-1)
+    return s2 * torch.exp(-0.5 * d)
+
+
+def variational_grads(X, Z, lengthscale, outputscale, weights, bias, m, s, gmean, gvar,
+                      jitter=1e-4, min_var=1e-6):
+    """d/dtheta of sum(gmean * mean) + sum(gvar * var) for ``variational_forward``
+    (DeepGP.py:51-99 via VariationalStrategy: K_ZZ + jitter -> fp64 Cholesky,
+    A = L^{-1} K_ZX, mean = A^T m + x w + b0, var = s2 + jitter + sum A^2 (s^2-1)
+    clamped at min_var). Returns a dict of float64 arrays: X, Z, m, s, outputscale,
+    lengthscale (D,), weights (D,), bias."""
+    import torch
+    X = np.asarray(X, np.float64)
+    B, N, D = X.shape
+    M = np.asarray(Z).shape[0]
+    Xt, Zt, mt, st = _t64(X), _t64(Z), _t64(m), _t64(s)
+    wt = _t64(np.reshape(weights, -1))
+    s2t, b0t = _t64(float(outputscale)), _t64(float(bias))
+    lst = _t64(np.broadcast_to(np.asarray(lengthscale, np.float64).reshape(-1), (D,)))
+    Kzz = _rbf_t(Zt, Zt, lst, s2t) + jitter * torch.eye(M, dtype=torch.float64)
+    L = torch.linalg.cholesky(Kzz)
+    Kzx = _rbf_t(Zt.expand(B, M, D), Xt, lst, s2t)
+    A = torch.linalg.solve_triangular(L, Kzx, upper=False)
+    mean = (A * mt[:, None]).sum(-2) + Xt @ wt + b0t
+    var = (s2t + jitter + (A * A * (st * st - 1.0)[:, None]).sum(-2)).clamp_min(min_var)
+    obj = (torch.as_tensor(np.asarray(gmean, np.float64)) * mean).sum() + \
+          (torch.as_tensor(np.asarray(gvar, np.float64)) * var).sum()
+    names = ["X", "Z", "m", "s", "outputscale", "lengthscale", "weights", "bias"]
+    gs = torch.autograd.grad(obj, [Xt, Zt, mt, st, s2t, lst, wt, b0t])
+    return {k: v.detach().numpy() for k, v in zip(names, gs)}
+
+
+def exact_mll_grads(X, y, lengthscale, outputscale, mean_constant, noise, gout=None):
+    """d/dtheta of sum_b gout_b * mll_b for ``exact_mll`` (GPModel.py:5-13 +
+    ExactMarginalLogLikelihood): grads w.r.t. X, y, lengthscale (scalar or (D,)),
+    outputscale, mean_constant, noise. float64 arrays."""
+    import torch
+    X = np.asarray(X, np.float64)
+    B, N, D = X.shape
+    ls_in = np.asarray(lengthscale, np.float64).reshape(-1)
+    Xt, yt, lst = _t64(X), _t64(y), _t64(ls_in)
+    s2t, ct, nzt = _t64(float(outputscale)), _t64(float(mean_constant)), _t64(float(noise))
+    K = _rbf_t(Xt, Xt, lst, s2t) + nzt * torch.eye(N, dtype=torch.float64)
+    L = torch.linalg.cholesky(K)
+    r = (yt - ct).unsqueeze(-1)
+    z = torch.linalg.solve_triangular(L, r, upper=False).squeeze(-1)
+    logdet = 2.0 * torch.log(torch.diagonal(L, dim1=-2, dim2=-1)).sum(-1)
+    mll = -0.5 * ((z * z).sum(-1) + logdet + N * LOG_2PI) / N
+    g = torch.ones(B, dtype=torch.float64) if gout is None else torch.as_tensor(np.asarray(gout, np.float64))
+    gs = torch.autograd.grad((g * mll).sum(), [Xt, yt, lst, s2t, ct, nzt])
+    names = ["X", "y", "lengthscale", "outputscale", "mean_constant", "noise"]
+    return {k: v.detach().numpy() for k, v in zip(names, gs)}

@@ -137,3 +137,65 @@ def test_golden_variational(name):
     elbo = O.deep_elbo(d["y"].astype(np.float64), r.mean, r.var, float(d["noise"]), d["m"], d["s"],
                        num_data=d["X"].shape[-1])
     assert np.allclose(elbo, d["elbo"], atol=1e-12)
+
+
+def _fd(f, x, h=1e-6):
+    return (f(x + h) - f(x - h)) / (2 * h)
+
+
+def test_variational_grads_vs_finite_differences():
+    """Pin the gradient oracle: central differences of the NumPy fp64 forward."""
+    rng = np.random.default_rng(3)
+    B, N, M, D = 2, 7, 5, 3
+    X = rng.standard_normal((B, N, D)) / math.sqrt(D)
+    Z = rng.standard_normal((M, D)) / math.sqrt(D)
+    ls = np.array([0.7, 0.9, 1.1]); s2 = 0.8
+    w = rng.standard_normal(D); b0 = 0.3
+    m = rng.standard_normal(M) * 0.5; s = rng.uniform(0.5, 1.0, M)
+    gm = rng.standard_normal((B, N)); gv = rng.standard_normal((B, N))
+    G = O.variational_grads(X, Z, ls, s2, w, b0, m, s, gm, gv)
+
+    def obj(X=X, Z=Z, ls=ls, s2=s2, w=w, b0=b0, m=m, s=s):
+        r = O.variational_forward(X, Z, ls, s2, w, b0, m, s, jitter=1e-4, dtype=np.float64)
+        return float((gm * r.mean).sum() + (gv * r.var).sum())
+
+    def bump(a, idx, h):
+        a = np.array(a, dtype=np.float64, copy=True); a[idx] += h; return a
+    checks = [
+        (G["outputscale"], _fd(lambda h: obj(s2=s2 + h), 0.0)),
+        (G["bias"], _fd(lambda h: obj(b0=b0 + h), 0.0)),
+        (G["lengthscale"][1], _fd(lambda h: obj(ls=bump(ls, 1, h)), 0.0)),
+        (G["Z"][2, 1], _fd(lambda h: obj(Z=bump(Z, (2, 1), h)), 0.0)),
+        (G["X"][1, 4, 2], _fd(lambda h: obj(X=bump(X, (1, 4, 2), h)), 0.0)),
+        (G["m"][3], _fd(lambda h: obj(m=bump(m, 3, h)), 0.0)),
+        (G["s"][0], _fd(lambda h: obj(s=bump(s, 0, h)), 0.0)),
+        (G["weights"][2], _fd(lambda h: obj(w=bump(w, 2, h)), 0.0)),
+    ]
+    for got, want in checks:
+        assert abs(got - want) <= 1e-6 * max(1.0, abs(want)), (got, want)
+
+
+def test_exact_grads_vs_finite_differences():
+    rng = np.random.default_rng(4)
+    B, N, D = 2, 9, 3
+    X = rng.standard_normal((B, N, D)) / math.sqrt(D)
+    y = rng.standard_normal((B, N))
+    ls, s2, c, nz = 0.8, 1.2, 0.1, 0.3
+    gout = np.array([0.7, -1.3])
+    G = O.exact_mll_grads(X, y, ls, s2, c, nz, gout)
+
+    def obj(X=X, y=y, ls=ls, s2=s2, c=c, nz=nz):
+        return float((gout * O.exact_mll(X, y, ls, s2, c, nz).mll).sum())
+
+    def bump(a, idx, h):
+        a = np.array(a, dtype=np.float64, copy=True); a[idx] += h; return a
+    checks = [
+        (G["outputscale"], _fd(lambda h: obj(s2=s2 + h), 0.0)),
+        (G["noise"], _fd(lambda h: obj(nz=nz + h), 0.0)),
+        (G["mean_constant"], _fd(lambda h: obj(c=c + h), 0.0)),
+        (G["lengthscale"][0], _fd(lambda h: obj(ls=ls + h), 0.0)),
+        (G["X"][1, 3, 2], _fd(lambda h: obj(X=bump(X, (1, 3, 2), h)), 0.0)),
+        (G["y"][0, 5], _fd(lambda h: obj(y=bump(y, (0, 5), h)), 0.0)),
+    ]
+    for got, want in checks:
+        assert abs(got - want) <= 1e-6 * max(1.0, abs(want)), (got, want)
