@@ -77,7 +77,7 @@ int gpk_variational_f32(const float* X, const float* Z, const double* Linv, cons
 }
 
 // Diagnostic (not part of the product ABI): same as gpk_exact_mll_f32 for N in
-// (240, 256], plus per-workgroup phase clocks (16 x u64 per window) in `stamps`.
+// (240, 256], plus per-workgroup phase clocks (32 x u64 per window) in `stamps`.
 int gpk_debug_exact_stamps(const float* X, const float* y, const float* hyp, int n_lengthscale,
                            int B, int N, int D, double jitter, int max_tries, float* L, float* z,
                            float* mll, int* info, unsigned long long* stamps, void* stream) {

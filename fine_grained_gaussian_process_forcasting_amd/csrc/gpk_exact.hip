@@ -9,27 +9,35 @@
 //   mll   = -0.5 * (||L^{-1}(y-c)||^2 + 2 sum log L_ii + N log 2pi) / N
 //           (upstream mlls/exact_marginal_log_likelihood.py, MVN.log_prob)
 //
-// Design: one workgroup of W waves per window, two workgroups per
-// CU. The padded K_hat (NB x NB tiles of 16x16, upper triangle, plus one
-// right-hand-side block column holding y - c) lives in REGISTERS as MFMA
-// accumulators (acc layout, see gpk_common.h). Tiles are dealt to waves in
-// row-descending order (ExactPlan), so at step k the tiles a wave still has to
-// update are a PREFIX of its slots. The blocked right-looking Cholesky works on
-// R = L^T (all accumulators hold -T, so every update is a plain MFMA accumulate):
-//   B(k): owners of (k,j) compute R_kj = R_kk^{-T} T_kj (4 MFMAs) and publish
-//         R_kj through an LDS panel; the RHS block yields z = L^{-1}(y - c).
-//   C(k): every owner of (i,j), i > k, accumulates R_ki^T R_kj (4 MFMAs, two
-//         independent chains per pair of slots). The owner of (k+1,k+1) updates
-//         that tile first and factors it right away (look-ahead), overlapping
-//         the diagonal factorisation with everybody else's trailing update.
+// Design: one workgroup of W waves per window, two workgroups
+// per CU. The padded K_hat (NB x NB tiles of 16x16, upper triangle) lives in
+// REGISTERS as MFMA accumulators (acc layout, see gpk_common.h) of the W-1
+// worker waves; the right-hand side y - c is a block column in LDS. Tiles are
+// dealt to workers in row-descending order (plan_tile), so at step k the tiles
+// a wave still has to update are a PREFIX of its slots. The blocked
+// right-looking Cholesky works on R = L^T (accumulators hold -T, so every
+// update is a plain MFMA accumulate).
+// The last wave is the DIAGONAL wave and owns the critical path alone:
+//   factor (k,k) -> publish R_kk^{-T} -> R_{k,k+1} = R_kk^{-T} T'_{k,k+1} ->
+//   T''_{k+1,k+1} = T'_{k+1,k+1} - R_{k,k+1}^T R_{k,k+1} -> factor (k+1,k+1)
+// (look-ahead), fed by the workers with (k,k+1) and (k+1,k+1) updated through
+// panel k-1. It never joins a barrier: the workers synchronise among
+// themselves (LDS counter) and every hand-off is an LDS flag holding a
+// monotone epoch. The workers per step: trailing update from panel k-1 (the
+// two hand-over tiles first), upper-L zeroing, right-hand side, the deferred
+// RBF of block row k+2 (the Gram is additive, so it may land after earlier
+// updates), then the TRSM of block row k into panel k once R_kk^{-T} is out.
 // Diagonal tiles are factored by one wave in one sweep: lanes 0-15 hold columns
 // of R, lanes 16-31 columns of R^{-T}, and both are produced by the SAME
-// readlane-broadcast instruction stream (DESIGN.md §3.3).
-// Barriers wait on LDS only (s_waitcnt lgkmcnt(0); s_barrier): the L stores
-// stream out behind the factorisation instead of being drained at each step.
+// readlane-broadcast instruction stream.
+// Flag waits read LDS only (ds_read + lgkmcnt): the L stores stream out behind
+// the factorisation instead of being drained at each step.
 #include "gpk_common.h"
 #include "gpk_internal.h"
 
+#ifndef GPK_EXACT_WBIG
+#define GPK_EXACT_WBIG 8
+#endif
 #ifndef GPK_SPLIT_UPDATE
 #define GPK_SPLIT_UPDATE 1
 #endif
@@ -38,7 +46,8 @@ namespace {
 
 constexpr float kLog2Pi = 1.8378770664093453f;
 
-// Static tile -> (wave, slot) plan. Tiles are listed row-descending (i = NB-1
+// Static tile -> (wave, slot) plan (host-evaluable reference; the device uses the
+// closed form plan_tile). Tiles are listed row-descending (i = NB-1
 // .. 0), j = i..NB-1 inside a row, and dealt cyclically: tile t -> worker
 // wave t % WK, slot t / WK. Then
 //   tiles with i > k            = { t < P(k) },  P(k) = (NB-k)(NB-k-1)/2
@@ -59,16 +68,42 @@ struct ExactPlan {
 };
 
 template <int NB>
-__constant__ ExactPlan<NB> c_plan = ExactPlan<NB>();
-
-template <int NB>
 GPK_DEVICE constexpr int plan_P(int k) {
   return (NB - k) * (NB - k - 1) / 2;
 }
 
+// Row-descending plan in closed form: tile t lies in block row i = NB - m where
+// m(m-1)/2 <= t < m(m+1)/2, at column j = i + t - m(m-1)/2.
+constexpr int plan_m(int t) {
+  int m = 1;
+  while ((m + 1) * m / 2 <= t) ++m;
+  return m;
+}
+
+// Tile (i | j << 8) of plan index t, for t known to lie in [LO, HI] at compile
+// time (t = wave + WK * slot): a short chain of scalar compares instead of a
+// constant-memory lookup (which costs two dependent SMEM round trips per tile).
+template <int M0, int HI, int Q>
+GPK_DEVICE int plan_m_tail(int t) {
+  constexpr int bq = (M0 + 1 + Q) * (M0 + Q) / 2;  // first tile of the row with m = M0 + 1 + Q
+  if constexpr (bq > HI) {
+    return M0 + Q;
+  } else {
+    return t >= bq ? plan_m_tail<M0, HI, Q + 1>(t) : M0 + Q;
+  }
+}
+
+template <int NB, int LO, int HI>
+GPK_DEVICE int plan_tile(int t) {
+  const int m = plan_m_tail<plan_m(LO), HI, 0>(t);
+  const int i = NB - m;
+  const int j = i + t - m * (m - 1) / 2;
+  return i | (j << 8);
+}
+
 struct ExactLds {
   // offsets in floats
-  int xf, xh, xl, nrm, rv, rw, panel, wbuf, dsc, cpart, red, total;
+  int xf, xh, xl, nrm, rv, rw, panel, wbuf, dsc, hbuf, cpart, rbfc, red, total;
 };
 
 __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
@@ -81,10 +116,12 @@ __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
   o.rv = o.nrm + NB * 16;
   o.rw = o.rv + NB * 16;                 // working copy of -(y - c) (the RHS column)
   o.panel = o.rw + NB * 16;
-  o.wbuf = o.panel + 2 * (NB + 1) * 256;  // double-buffered R panel
-  o.dsc = o.wbuf + 256;
-  o.cpart = o.dsc + 256;
-  o.red = o.cpart + 64 * W + 256;
+  o.wbuf = o.panel + 2 * (NB + 1) * 256;  // (panel: double-buffered R rows)
+  o.dsc = o.wbuf + 2 * 256;              // (wbuf: R_kk^{-T}, double-buffered by step parity)
+  o.hbuf = o.dsc + 256;                  // (dsc: the diagonal wave's working tile)
+  o.cpart = o.hbuf + 2 * 512;            // (hbuf: look-ahead hand-off {(k,k+1), (k+1,k+1)} x parity)
+  o.rbfc = o.cpart + 64 * W + 256;      // RbfK (16-byte aligned)
+  o.red = o.rbfc + 4;
   o.total = o.red + 4 * W + 40;
   return o;
 }
@@ -117,7 +154,13 @@ GPK_DEVICE void barrier_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// FULL: N == 16 * NB (no padding) -- every row and column of every tile is real.
+template <bool FULL>
 GPK_DEVICE void store4(float* p, int N, int row, int colg, const f32x4 v) {
+  if constexpr (FULL) {
+    *(f32x4*)&p[(size_t)row * N + colg] = v;
+    return;
+  }
   if (row >= N) return;
   if (((N & 3) == 0) && colg + 3 < N) {
     *(f32x4*)&p[(size_t)row * N + colg] = v;
@@ -206,20 +249,89 @@ GPK_DEVICE void diag_sweep(float (&v)[16]) {
   if constexpr (M < 15) diag_sweep<M + 1>(v);
 }
 
+// Flag words (ints in LDS, monotone epochs -- nothing is ever reset within a
+// launch; epoch = 32 * attempt + k):
+enum : int {
+  kFlagT00 = 1,     // tile (0,0) of this attempt is in dsc                (32 * attempt)
+  kFlagFact = 2,    // R_kk^{-T} of step k is in wbuf[k & 1]                (epoch)
+  kFlagFail = 3,    // [3 + attempt]: failing column (provisional 1 first)
+  kFlagHA = 18,     // look-ahead tile (k, k+1)   in hbuf[k & 1]            (epoch)
+  kFlagHB = 19,     // look-ahead tile (k+1, k+1) in hbuf[k & 1] + 256      (epoch)
+  kFlagSync = 20,   // worker-only barrier counter
+  kFlagTmo = 21,    // a spin wait ran out (safety net: the launch still drains)
+  kFlagInvSigma = 30,
+  kFlagGm2 = 31,
+};
+
+// Poll an LDS flag until it reaches `target`. Every wait is bounded: after
+// ~2^18 sleeps (milliseconds) the wave gives up, records it in kFlagTmo and
+// carries on, so a logic error can never leave waves spinning on the GPU
+// (the window then reports info = kInfoTimeout).
+constexpr int kInfoTimeout = 1 << 20;
+GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
+  int n = 0;
+  while (flags[idx] < target) {
+    if (flags[kFlagTmo] != 0) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++n > (1 << 18)) {
+      flags[kFlagTmo] = 1;
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+GPK_DEVICE void publish_tile(float* dst, int lane, const f32x4 v, lds_vint* flags, int idx, int value) {
+  *(f32x4*)&dst[lane * 4] = v;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (lane == 0) flags[idx] = value;
+}
+
+// R_kj = R_kk^{-T} T_kj for one tile: q = -W^T (from wbuf, acc layout), t = -T_kj.
+// Two independent 2-MFMA chains (80 cycles of dependent latency instead of 160).
+// Used by the worker TRSM and by the diagonal wave's look-ahead alike, so both
+// produce bit-identical panels.
+GPK_DEVICE f32x4 trsm_tile(const f32x4 q, const f32x4 t) {
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  f32x4 d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(q[0], t[0], z, 0, 0, 0);
+  f32x4 d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(q[2], t[2], z, 0, 0, 0);
+  d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(q[1], t[1], d0, 0, 0, 0);
+  d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(q[3], t[3], d1, 0, 0, 0);
+  return d0 + d1;
+}
+
+GPK_DEVICE f32x4 load_w(const float* wb, int c, int grp) {
+  f32x4 q;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) q[r] = wb[(4 * grp + r) * 16 + c];
+  return q;
+}
+
+// d += R^T R for a rounded factor tile held as registers (hi, lo).
+GPK_DEVICE f32x4 mma_tn_split_regs(const half4_t h, const half4_t l, f32x4 d) {
+  const half8_t hl = {h[0], h[1], h[2], h[3], l[0], l[1], l[2], l[3]};
+  const half8_t lh = {l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(hl, hl, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(hl, lh, d, 0, 0, 0);
+  return d;
+}
+
 // Factor one 16x16 diagonal tile T in ONE wave (the diagonal wave).
 //   lanes  0-15 (column c): v[m] <- R[m][c]             (R^T R = T, upper)
 //   lanes 16-31 (column c): v[m] <- W[m][c], W = R^{-T}  (lower), started from I
 // from one instruction stream: at step m every lane does
 //   v[m] *= rsqrt(pivot);   v[i] -= R[m][i] * v[m]   (i > m)
 // with R[m][i] broadcast from R-lane i by readlane. `tile` holds -T in acc
-// layout (written by the tile's owner). -W (transposed: wbuf[c*16+m] = -W[m][c])
-// is published FIRST and the factor-done flag raised; only then the L diagonal
-// block, the failure check and log|T| are produced. A non-positive or NaN pivot
-// turns every later diagonal entry into NaN, so the first failing column is
-// found once from the diagonal of R.
-GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* done_flag, int epoch,
-                           float* Lb, int N, int row0, float inv_sigma, float& logdet) {
-  __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration
+// layout. -W (transposed: wbuf[c*16+m] = -W[m][c]) is published FIRST together
+// with the pass/fail verdict (every pivot checked positive-finite on the scalar
+// broadcast: v_cmp_class), then the factor-done flag is raised; only then the L
+// diagonal block, the exact failing column and log|T| are produced.
+template <bool ST, bool FULL>
+GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_vint* fail_flag,
+                           int epoch, float* Lb, int N, int row0, float inv_sigma, float& logdet,
+                           unsigned long long* dst = nullptr) {
+  unsigned long long t0 = 0;
+  if constexpr (ST) t0 = __builtin_amdgcn_s_memtime();
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));  // keep per-lane masks local to this call
   const int c = lane & 15, grp = lane >> 4;
@@ -233,28 +345,47 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* done_flag, 
       v[i] = (grp == 0) ? -t[r] : ((grp == 1 && i == c) ? 1.f : 0.f);
     }
   }
+  if constexpr (ST) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) dst[0] += t1 - t0;
+    t0 = t1;
+    __builtin_amdgcn_sched_barrier(0);
+  }
   diag_sweep<0>(v);
+  if constexpr (ST) {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) dst[1] += t1 - t0;
+    t0 = t1;
+    __builtin_amdgcn_sched_barrier(0);
+  }
   if (grp == 1) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
       *(f32x4*)&wbuf[c * 16 + 4 * g] = f32x4{-v[4 * g], -v[4 * g + 1], -v[4 * g + 2], -v[4 * g + 3]};
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  if (lane == 0) *done_flag = epoch;
-  __builtin_amdgcn_s_setprio(0);
-  // diagonal of R, failure detection, log|T| = sum_c log R[c][c]^2
+  // diagonal of R (lane c < 16 holds R[c][c] in v[c])
   float dg = v[0];
 #pragma unroll
   for (int i = 1; i < 16; ++i) dg = (c == i) ? v[i] : dg;
   const bool okd = (dg > 0.f) && (dg < __builtin_huge_valf());
   const unsigned long long badm = __ballot(lane < 16 && !okd);
-  const int fail = badm ? __builtin_ctzll(badm) + 1 : 0;
-  {
-    float lg = (lane < 16) ? __builtin_amdgcn_logf(dg * dg) : 0.f;
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
-    logdet += readlane_f(lg, 0) * 0.69314718055994531f;  // v_log_f32 is log2
+  if (badm != 0 && lane == 0) *fail_flag = 1;  // provisional: exact column below
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (lane == 0) flags[kFlagFact] = epoch;
+  if constexpr (ST) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) dst[2] += t1 - t0;
+    __builtin_amdgcn_sched_barrier(0);
   }
+  const int fail = badm ? __builtin_ctzll(badm) + 1 : 0;
+  // per-lane partial log2|T| (lanes 0-15); reduced across lanes once, at the end
+  // (a per-step shuffle reduction is 4 LDS round trips on the critical path)
+  logdet += (lane < 16) ? __builtin_amdgcn_logf(dg * dg) : 0.f;
   if (grp == 0) {
     // R lanes: zero below-diagonal garbage, write L[row0 + c][row0 + m] = R[m][c]
 #pragma unroll
@@ -263,11 +394,79 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* done_flag, 
     if (Lb != nullptr) {
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        store4(Lb, N, row0 + c, row0 + 4 * g,
+        store4<FULL>(Lb, N, row0 + c, row0 + 4 * g,
                f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]} * inv_sigma);
     }
   }
   return fail;
+}
+
+// ---------------------------------------------------------------------------
+// RBF tile straight into accumulator form: returns -K_hat(tile i, j) in acc
+// layout (three split-f16 MFMA passes for the Gram).
+// ---------------------------------------------------------------------------
+// Its scalars live in one 16-byte LDS word group (rbfc), read ONCE per batch
+// of tiles (one ds_read_b128) so they do not pin SGPRs across the unrolled
+// factorisation steps: {gm2 = -2 / 2^(2a) (undoes the f16 image scale on the
+// Gram), s2 * sigma^2, (s2 + noise + jitter) * sigma^2, LDS float offset of the
+// squared norms | (D chunks of 32) << 20}.
+struct RbfK {
+  float gm2, s2, diagval;
+  int nrm_dc;
+};
+GPK_DEVICE RbfK read_rbfk(const float* rbfc) {
+  // plain (non-volatile) 16-byte LDS load through a laundered address: one
+  // ds_read_b128, never hoisted or merged across steps
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)rbfc;
+  asm volatile("" : "+v"(addr));
+  const i32x4 v = *(const __attribute__((address_space(3))) i32x4*)(uintptr_t)addr;
+  RbfK k;
+  k.gm2 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(v[0]));
+  k.s2 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(v[1]));
+  k.diagval = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(v[2]));
+  k.nrm_dc = __builtin_amdgcn_readfirstlane(v[3]);
+  return k;
+}
+
+template <int NB, bool FULL>
+GPK_DEVICE f32x4 rbf_tile(const float* smem, const RbfK& k, int i, int j, int lane, int N) {
+  constexpr float nhalf_log2e = -0.72134752044448170f;  // -0.5 * log2(e)
+  const int c = lane & 15, grp = lane >> 4;
+  const int DC32 = k.nrm_dc >> 20;
+  const float* nrm = smem + (k.nrm_dc & 0xfffff);
+  const half8_t* x8 = (const half8_t*)smem;  // f16 hi / lo images (hfrag layout) at offset 0
+  // every LDS operand of the tile is requested before the first MFMA (one
+  // round trip instead of a load -> wait -> MFMA chain)
+  const f32x4 nr = *(const f32x4*)&nrm[16 * i + 4 * grp];
+  const int col = 16 * j + c;
+  const float nc = nrm[col];
+  f32x4 g = {0.f, 0.f, 0.f, 0.f};
+  for (int dd = 0; dd < DC32; ++dd) {
+    const half8_t* xhv = x8 + (2 * dd) * NB * 64;
+    const half8_t* xlv = x8 + (2 * dd + 1) * NB * 64;
+    const half8_t al = xlv[i * 64 + lane], bh = xhv[j * 64 + lane];
+    const half8_t ah = xhv[i * 64 + lane];
+    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, g, 0, 0, 0);
+    const half8_t bl = xlv[j * 64 + lane];
+    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, g, 0, 0, 0);
+  }
+  const float gm2 = k.gm2, s2 = k.s2, diagval = k.diagval;
+  f32x4 o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = 16 * i + 4 * grp + q;
+    float dist = __builtin_fmaf(gm2, g[q], nr[q] + nc);
+    dist = dist < 0.f ? 0.f : dist;  // clamp_min(0), NaN-propagating like torch
+    float v = s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);
+    if (row == col) v = diagval;
+    if constexpr (!FULL) {
+      if (row >= N || col >= N) v = (row == col) ? 1.f : 0.f;
+    }
+    o[q] = -v;
+  }
+  return o;
 }
 
 // ---------------------------------------------------------------------------
@@ -297,68 +496,119 @@ GPK_DEVICE void static_for_range(F&& f) {  // A..B inclusive, ascending
 
 struct WorkerCtx {
   float* panel;
-  float* dsc;
   float* wbuf;
+  float* hbuf;
   lds_vint* vflag;
   float* Lb;
   float* zout;
   float* rw;
+  const float* smem;
+  int rbfc;    // LDS float offset of the RBF constants (RbfK)
   int N, b, lane, c, grp, wv;
-  int epoch0;  // hand-off / factor-done flag value of step 0 in this attempt
+  int epoch0;  // flag value of step 0 in this attempt (32 * attempt)
+  int nsync;   // worker-only barriers passed by this wave
   float sumz2;
+  unsigned long long* st;  // STAMPS builds only: [0..7] phase clocks, [8] last stamp
 };
 
-template <int NB, int WK, int SLOTS, int K>
-GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
+// Diagnostic phase clock inside the worker steps (STAMPS builds only).
+#define GPK_WSTAMP(slot)                                          \
+  if constexpr (ST) {                                             \
+    __builtin_amdgcn_sched_barrier(0);                            \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime();   \
+    x.st[slot] += _n - x.st[8];                                   \
+    x.st[8] = _n;                                                 \
+    __builtin_amdgcn_sched_barrier(0);                            \
+  }
+
+// Barrier among the WK worker waves only (the diagonal wave runs ahead of them
+// and never joins): monotone LDS counter, one ds_add per wave.
+template <int WK>
+GPK_DEVICE void worker_sync(WorkerCtx& x) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  x.nsync += 1;
+  if (x.lane == 0)
+    (void)__atomic_fetch_add((__attribute__((address_space(3))) int*)&x.vflag[kFlagSync], 1,
+                             __ATOMIC_RELAXED);
+  spin_until(x.vflag, kFlagSync, WK * x.nsync);
+}
+
+// One right-looking step K for the worker waves. The diagonal wave owns the
+// diagonal tiles from the moment they are handed over: at step K it factors
+// (K,K), computes R_{K,K+1} itself and applies that last update to (K+1,K+1)
+// (look-ahead), so the workers
+//   1. apply panel K-1 to their tiles with i >= K except (K,K), updating and
+//      handing over (K,K+1) and (K+1,K+1) FIRST (hbuf[K & 1], flags HA / HB);
+//   2. zero L's upper part of block row K, update the right-hand side;
+//   3. build the RBF tiles of block row K+2 (deferred Gram: additive, so it
+//      can land after earlier trailing updates) -- this fills the time the
+//      diagonal wave spends factoring;
+//   4. wait for R_KK^{-T}, TRSM block row K (+ z_K) into panel K;
+//   5. worker-only barrier.
+// Returns nonzero when the diagonal wave reported a failed factorisation.
+template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL>
+GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   constexpr int Pk = plan_P<NB>(K);
-  constexpr int DS = Pk / WK, DW = Pk % WK;  // diagonal tile (K,K): slot / wave
+  constexpr bool LAST = (K == NB - 1);
+  constexpr int TD = Pk;                                  // (K, K): the diagonal wave's
+  constexpr int TA = Pk + 1;                              // (K, K+1)
+  constexpr int TB = LAST ? -1 : plan_P<NB>(K + 1);       // (K+1, K+1)
   // launder per step: keeps the per-slot plan loads / LDS addresses of this
   // step from being hoisted (and pinned in registers) across all NB steps
   const int wv = launder_s(x.wv);
+  const int e0 = launder_s(x.epoch0);
   int lane = x.lane;
   asm volatile("" : "+v"(lane));
   const int c = lane & 15, grp = lane >> 4;
   const float* pprev = x.panel + ((K + 1) & 1) * (NB + 1) * 256;  // panel K-1
   float* pcur = x.panel + (K & 1) * (NB + 1) * 256;                // panel K
-  auto handoff = [&](const f32x4& a) {
-    *(f32x4*)&x.dsc[lane * 4] = a;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) x.vflag[1] = x.epoch0 + K;
-  };
-  auto upd = [&](f32x4& d, int s) {
-    const int p = c_plan<NB>.ij[wv + WK * s];
-#if GPK_SPLIT_UPDATE
-    d = mma_tn_split(load_split_hl(pprev + (p & 255) * 256, lane), pprev + (p >> 8) * 256, lane, d);
-#else
-    const f32x4 pi = *(const f32x4*)&pprev[(p & 255) * 256 + lane * 4];
-    const f32x4 pj = *(const f32x4*)&pprev[(p >> 8) * 256 + lane * 4];
-    d = mma_tn(pi, pj, d);
-#endif
+  float* hA = x.hbuf + (K & 1) * 512;
+  // (the hand-over tiles have compile-time (i, j): no plan lookup, so nothing
+  // wave-specialised gets hoisted out of the attempt loop)
+  auto upd_ij = [&](f32x4& d, auto I, auto J) {
+    constexpr int i = decltype(I)::value, j = decltype(J)::value;
+    d = mma_tn_split(load_split_hl(pprev + i * 256, lane), pprev + j * 256, lane, d);
   };
   if constexpr (K > 0) {
-    // trailing update from panel K-1 over tiles with i >= K (t < P(K-1)),
-    // highest slot first so the row-K tiles -- (K,K) among them -- come first.
-    constexpr int Pkm1 = plan_P<NB>(K - 1);
-    constexpr int NALL = Pkm1 / WK;
-    if constexpr (NALL < SLOTS && (Pkm1 % WK) != 0) {
-      if (wv < Pkm1 % WK) {
-        upd(acc[NALL], NALL);
-        if constexpr (DS == NALL) {
-          if (wv == DW) handoff(acc[NALL]);
-        }
+    if constexpr (!LAST) {
+      if (wv == TA % WK) {
+        upd_ij(acc[TA / WK], IC<K>{}, IC<K + 1>{});
+        publish_tile(hA, lane, acc[TA / WK], x.vflag, kFlagHA, e0 + K);
+      }
+      if (wv == TB % WK) {
+        upd_ij(acc[TB / WK], IC<K + 1>{}, IC<K + 1>{});
+        publish_tile(hA + 256, lane, acc[TB / WK], x.vflag, kFlagHB, e0 + K);
       }
     }
-    static_for_desc<NALL>([&](auto I) {
+    // trailing update from panel K-1 over the other tiles with i >= K
+    // (t < P(K-1)), highest slot first. Re-laundered: the hand-over branches
+    // above pin wv to a constant, and code tail-duplicated into them would
+    // turn plan lookups into constants hoisted out of the attempt loop.
+    const int wv = launder_s(x.wv);
+    auto upd = [&](f32x4& d, auto I) {
       constexpr int s = decltype(I)::value;
-      upd(acc[s], s);
-      if constexpr (s == DS) {
-        if (wv == DW) handoff(acc[s]);
-      }
-    });
+      const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(wv + WK * s);
+      d = mma_tn_split(load_split_hl(pprev + (p & 255) * 256, lane), pprev + (p >> 8) * 256, lane, d);
+    };
+    constexpr int Pkm1 = plan_P<NB>(K - 1);
+    constexpr int NALL = Pkm1 / WK;
+    auto bulk = [&](auto I) {
+      constexpr int s = decltype(I)::value;
+      bool sk = false;
+      if constexpr (s == TD / WK) sk = sk || (wv == TD % WK);
+      if constexpr (!LAST && s == TA / WK) sk = sk || (wv == TA % WK);
+      if constexpr (!LAST && s == TB / WK) sk = sk || (wv == TB % WK);
+      if (!sk) upd(acc[s], I);
+    };
+    if constexpr (NALL < SLOTS && (Pkm1 % WK) != 0) {
+      if (wv < Pkm1 % WK) bulk(IC<NALL>{});
+    }
+    static_for_desc<NALL>(bulk);
   }
+  GPK_WSTAMP(2)  // trailing update (+ hand-over)
   // zero L's strictly-upper part of block-row K (streams out behind the MFMAs)
   if (x.Lb != nullptr) {
-    const int N = x.N;
+    const int N = FULL ? 16 * NB : x.N;
     const int c0 = 16 * (K + 1);
     for (int q = wv; q < 16; q += WK) {
       const int row = 16 * K + q;
@@ -380,59 +630,60 @@ GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     for (int i = rfirst; i < NB; i += WK) {
       f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
-#if GPK_SPLIT_UPDATE
       d = mma_tn_split(load_split_hl(pprev + i * 256, lane), pprev + NB * 256, lane, d);
-#else
-      d = mma_tn(*(const f32x4*)&pprev[i * 256 + lane * 4], *(const f32x4*)&pprev[NB * 256 + lane * 4], d);
-#endif
       if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
     }
   }
+  GPK_WSTAMP(6)  // zero-L, right-hand side
+  // deferred RBF of block row K+2 (its diagonal tile is handed over at step K+1)
+  if constexpr (K + 2 < NB) {
+    constexpr int RLO = plan_P<NB>(K + 2), RHI = plan_P<NB>(K + 1) - 1;
+    constexpr int SLO = RLO / WK;
+    constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
+    const RbfK rk = read_rbfk(x.smem + x.rbfc);
+    static_for_range<SLO, SHI>([&](auto I) {
+      constexpr int s = decltype(I)::value;
+      const int t = wv + WK * s;
+      if (t >= RLO && t <= RHI) {
+        const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(t);
+        acc[s] += rbf_tile<NB, FULL>(x.smem, rk, p & 255, p >> 8, lane, x.N);
+      }
+    });
+  }
   // TRSM of the row-K off-diagonal tiles (P(K) < t <= P(K) + NB - K - 1) and,
   // by the owner of RHS block row K, of the right-hand side: z_K
+  GPK_WSTAMP(3)  // deferred RBF
+  spin_until(x.vflag, kFlagFact, e0 + K);
+  GPK_WSTAMP(7)  // wait for R_KK^{-T}
+  if (x.vflag[kFlagFail + e0 / 32] != 0) return 1;
   constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
   constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
   constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
-  const int tfirst = TLO + (((wv - TLO) % WK) + WK) % WK;
   const bool own_rhs = (rfirst == K);
-  if (tfirst <= THI || own_rhs) {
-    while (x.vflag[2] < x.epoch0 + K) __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    f32x4 q;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) q[r] = x.wbuf[(4 * grp + r) * 16 + c];
+  {
+    const f32x4 q = load_w(x.wbuf + (K & 1) * 256, c, grp);
     // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
-    const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[30]);
+    const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
     if constexpr (THI >= TLO) {
       static_for_range<SLO, SHI>([&](auto I) {
         constexpr int s = decltype(I)::value;
         const int t = wv + WK * s;
         if (t >= TLO && t <= THI) {
-          const int j = c_plan<NB>.ij[t] >> 8;
-#if GPK_SPLIT_UPDATE
+          const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
           half4_t h, l;
-          const f32x4 rkj = round_split_f16(mma_tn(q, acc[s], f32x4{0.f, 0.f, 0.f, 0.f}), h, l);
+          const f32x4 rkj = round_split_f16(trsm_tile(q, acc[s]), h, l);
           store_split_planes(pcur + j * 256, lane, h, l);
-#else
-          const f32x4 rkj = mma_tn(q, acc[s], f32x4{0.f, 0.f, 0.f, 0.f});
-          *(f32x4*)&pcur[j * 256 + lane * 4] = rkj;
-#endif
           // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
-          if (x.Lb != nullptr) store4(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
+          if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
         }
       });
     }
     if (own_rhs) {
       f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
-#if GPK_SPLIT_UPDATE
       half4_t h, l;
-      const f32x4 zk = round_split_f16(mma_tn(q, d, f32x4{0.f, 0.f, 0.f, 0.f}), h, l);
+      const f32x4 zk = round_split_f16(trsm_tile(q, d), h, l);
       store_split_planes(pcur + NB * 256, lane, h, l);
-#else
-      const f32x4 zk = mma_tn(q, d, f32x4{0.f, 0.f, 0.f, 0.f});
-      *(f32x4*)&pcur[NB * 256 + lane * 4] = zk;
-#endif
       if (c == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
@@ -440,36 +691,36 @@ GPK_DEVICE void worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
           const int row = 16 * K + 4 * grp;
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (row + r < x.N) x.zout[(size_t)x.b * x.N + row + r] = zk[r];
+            if (FULL || row + r < x.N) x.zout[(size_t)x.b * x.N + row + r] = zk[r];
         }
       }
     }
   }
+  GPK_WSTAMP(4)  // TRSM
+  worker_sync<WK>(x);
+  GPK_WSTAMP(5)  // worker barrier
+  return 0;
 }
 
-// Steps K..NB-1, one LDS barrier after each; stops after the barrier of a step
-// whose diagonal factorisation failed (the diagonal wave does the same).
-template <int NB, int WK, int SLOTS, int K>
+template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL>
 GPK_DEVICE int worker_steps(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   if constexpr (K < NB) {
-    worker_step<NB, WK, SLOTS, K>(acc, x);
-    barrier_lds();
-    const int failed = x.vflag[3 + x.epoch0 / 32];
-    if (failed) return failed;
-    return worker_steps<NB, WK, SLOTS, K + 1>(acc, x);
+    if (worker_step<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
+    return worker_steps<NB, WK, SLOTS, K + 1, ST, FULL>(acc, x);
   } else {
     return 0;
   }
 }
 
-template <int NB, int W, bool STAMPS = false>
+template <int NB, int W, bool STAMPS, bool FULL>
 __global__ void __launch_bounds__(64 * W, (2 * W) / 4)
 gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
-                 const float* __restrict__ hyp, int n_ls, int N, int D, int DC,
+                 const float* __restrict__ hyp, int n_ls, int N_in, int D, int DC,
                  double jitter0, int max_tries, float* __restrict__ Lout,
                  float* __restrict__ zout, float* __restrict__ mll,
                  int* __restrict__ info, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int NT = ExactPlan<NB>::NT;
+  const int N = FULL ? 16 * NB : N_in;  // FULL: no padded rows anywhere
   constexpr int WK = W - 1;                  // worker waves; wave WK is the diagonal wave
   constexpr int SLOTS = (NT + WK - 1) / WK;
   constexpr int T = 64 * W;
@@ -497,6 +748,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   float* panel = smem + lay.panel;
   float* wbuf = smem + lay.wbuf;
   float* dsc = smem + lay.dsc;
+  float* hbuf = smem + lay.hbuf;
   float* cpart = smem + lay.cpart;
   float* red = smem + lay.red;
   int* flag = (int*)(red + 4 * W);
@@ -570,15 +822,24 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     if (lane == 0) red[wave] = mx;
   }
   barrier_lds();
-  // flags: [1] tile hand-off epoch, [2] factor-done epoch (epoch = 32*attempt + k,
-  // monotone, so nothing is ever reset), [3 + attempt] failing column of attempt
   if (tid == 0) {
     flag[0] = 0;
-    flag[1] = -1;
-    flag[2] = -1;
+    flag[kFlagT00] = -1;
+    flag[kFlagFact] = -1;
     for (int q = 3; q < 16; ++q) flag[q] = 0;
-    flag[30] = __builtin_bit_cast(int, inv_sigma);  // read back per step (SGPR budget)
-    if constexpr (STAMPS) ((unsigned long long*)(red + 4 * W + 24))[0] = 0;
+    flag[kFlagHA] = -1;
+    flag[kFlagHB] = -1;
+    flag[kFlagSync] = 0;
+    flag[kFlagTmo] = 0;
+    flag[kFlagInvSigma] = __builtin_bit_cast(int, inv_sigma);  // read back per step (SGPR budget)
+    smem[lay.rbfc + 1] = s2;
+    ((int*)smem)[lay.rbfc + 3] = lay.nrm | (((DC + 1) / 2) << 20);
+    if constexpr (STAMPS) {
+      ((unsigned long long*)(red + 4 * W + 24))[0] = 0;
+      ((unsigned long long*)(red + 4 * W + 26))[0] = 0;
+      ((unsigned long long*)(red + 4 * W + 28))[0] = 0;
+      for (int q = 0; q < 3; ++q) ((unsigned long long*)(red + 4 * W + 32))[q] = 0;
+    }
   }
   // ---- 2. centre columns by the mean over the N real rows (GPyTorch _sq_dist)
   {
@@ -604,7 +865,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   }
   // ---- 3. subtract the mean, squared norms, residual r = y - c -----------
   // The centred rows are split into f16 hi + lo parts (x = hi + lo + O(2^-22 x))
-  // for the 3-pass f16 MFMA Gram (DESIGN.md §3.2); the images overwrite the
+  // for the 3-pass f16 MFMA Gram (DESIGN.md §4.1); the images overwrite the
   // fp32 staging chunk pair they were read from (read all -> barrier -> write).
   {
     const float* cmean_d = cpart + 64 * W;
@@ -622,7 +883,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       a_sc = a_sc > 100 ? 100 : (a_sc < -100 ? -100 : a_sc);
     }
     const float xsc = __builtin_ldexpf(1.f, a_sc);
-    if (tid == 0) flag[31] = __builtin_bit_cast(int, __builtin_ldexpf(-2.f, -2 * a_sc));
+    if (tid == 0) smem[lay.rbfc] = __builtin_ldexpf(-2.f, -2 * a_sc);
     const int DC32 = (DC + 1) / 2;
     const int n = tid;  // NP <= 256 <= T: one row per thread
     float s = 0.f;
@@ -670,23 +931,26 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   barrier_lds();
   GPK_STAMP(0)
 
-  const float nhalf_log2e = -0.72134752044448170f;  // -0.5 * log2(e)
-  int info_w = 0, failed = 0;
+  int info_w = 0, failed = 0, att_end = 0;
   float logdet = 0.f, sumz2 = 0.f;
-  lds_vint* vflag = as_lds_flags(flag);  // [0] fail column, [1] tile hand-off step, [2] factor-done step
-  // The diagonal wave and the worker waves run separate programs (so the
-  // workers' accumulator array is not live across the factorisation code);
-  // they meet at the same sequence of barriers: one per factorisation step.
-  // Hand-offs inside a step go through LDS flags holding monotone epochs.
+  lds_vint* vflag = as_lds_flags(flag);
+  // The diagonal wave and the worker waves run separate programs and meet at
+  // no barrier until the end: within an attempt every hand-off goes through
+  // LDS flags holding monotone epochs, and the workers synchronise among
+  // themselves (worker_sync). The diagonal wave runs AHEAD of the workers: its
+  // per-step chain is factor (k,k) -> R_{k,k+1} -> last update of (k+1,k+1) ->
+  // factor (k+1,k+1), with the inputs of the look-ahead handed over early.
   if (wave == WK) {
     // ================================================= diagonal wave program
+    __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration
     for (int attempt = 0; attempt <= max_tries; ++attempt) {
+      att_end = attempt;
       logdet = 0.f;
       failed = 0;
-      for (int k = 0; k < NB && !failed; ++k) {
+      spin_until(vflag, kFlagT00, 32 * attempt);
+      for (int k = 0; k < NB; ++k) {
         const int epoch = 32 * attempt + k;
-        while (vflag[1] < epoch) __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        float* wb = wbuf + (k & 1) * 256;
         unsigned long long dt0 = 0;
         if constexpr (STAMPS) {
           dt0 = __builtin_amdgcn_s_memtime();
@@ -695,23 +959,55 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
             flag[17] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
           }
         }
-        const int f = diag_factor(dsc, wbuf, vflag + 2, epoch, Lb, N, 16 * k, inv_sigma, logdet);
+        const int f = diag_factor<STAMPS, FULL>(dsc, wb, vflag, vflag + kFlagFail + attempt, epoch, Lb, N,
+                                          16 * k, inv_sigma, logdet,
+                                          (unsigned long long*)(red + 4 * W + 32));
         if constexpr (STAMPS) {
           if (lane == 0) ((unsigned long long*)(red + 4 * W + 24))[0] += __builtin_amdgcn_s_memtime() - dt0;
         }
-        if (f != 0 && lane == 0) vflag[3 + attempt] = 16 * k + f;
-        barrier_lds();
-        failed = vflag[3 + attempt];
+        if (f != 0) {
+          failed = 16 * k + f;
+          if (lane == 0) vflag[kFlagFail + attempt] = failed;
+          break;
+        }
+        if (k == NB - 1) break;
+        // look-ahead: R_{k,k+1} = R_kk^{-T} T'_{k,k+1}, then the last update of
+        // (k+1,k+1); both tiles arrive (updated through panel k-1) in hbuf[k & 1]
+        const float* hk = hbuf + (k & 1) * 512;
+        unsigned long long hw0 = 0;
+        if constexpr (STAMPS) hw0 = __builtin_amdgcn_s_memtime();
+        spin_until(vflag, kFlagHA, epoch);
+        spin_until(vflag, kFlagHB, epoch);
+        if constexpr (STAMPS) {
+          const unsigned long long hw1 = __builtin_amdgcn_s_memtime();
+          if (lane == 0) ((unsigned long long*)(red + 4 * W + 26))[0] += hw1 - hw0;
+          hw0 = hw1;
+        }
+        const f32x4 q = load_w(wb, c, grp);
+        const f32x4 ta = *(const f32x4*)&hk[lane * 4];
+        f32x4 tb = *(const f32x4*)&hk[256 + lane * 4];
+        half4_t h, l;
+        (void)round_split_f16(trsm_tile(q, ta), h, l);
+        tb = mma_tn_split_regs(h, l, tb);
+        *(f32x4*)&dsc[lane * 4] = tb;
+        if constexpr (STAMPS) {
+          if (lane == 0) ((unsigned long long*)(red + 4 * W + 28))[0] += __builtin_amdgcn_s_memtime() - hw0;
+        }
       }
       if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
       info_w = failed;
     }
+    __builtin_amdgcn_s_setprio(0);
   } else {
     // ================================================= worker program
     float diagval = (s2u + noise) * sigma2;
     double jit_prev = 0.0;
     f32x4 acc[SLOTS];
+    unsigned long long wst[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    WorkerCtx wx{panel, wbuf, hbuf, vflag, Lb, zout, rw, smem, lay.rbfc, N, b, lane, c, grp,
+                 launder_s(wave), 0, 0, 0.f, nullptr};
     for (int attempt = 0; attempt <= max_tries; ++attempt) {
+      att_end = attempt;
       if (attempt > 0) {
         double p10 = 1.0;
         for (int q = 1; q < attempt; ++q) p10 *= 10.0;
@@ -719,133 +1015,149 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         diagval = diagval + (float)(jn - jit_prev) * sigma2;
         jit_prev = jn;
       }
-    // right-hand side: this wave's block rows of rw <- -(y - c) (fresh per attempt)
-    for (int i = wave; i < NB; i += WK)
-      if (lane < 16) rw[16 * i + lane] = -rv[16 * i + lane];
-    // ---- 4. RBF tiles straight into the accumulators (negated), highest slot
-    // first; the owner of (0,0) hands it to the diagonal wave as soon as it
-    // exists, so factorisation step 0 overlaps the rest of the Gram build.
-    {
-      const int wv = launder_s(wave);
-      constexpr int P0 = plan_P<NB>(0);
-      // -2 / 2^(2a): undoes the f16 image scale on the Gram (uniform -> SGPR)
-      const float gm2 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane((int)vflag[31]));
-      static_for_desc<SLOTS>([&](auto I) {
-        constexpr int s = decltype(I)::value;
-        const int t = wv + WK * s;
-        if (t < NT) {
-          const int pk = c_plan<NB>.ij[t];
-          const int i = pk & 255, j = pk >> 8;
-          {
-            f32x4 g = {0.f, 0.f, 0.f, 0.f};
-            const int DC32 = (DC + 1) / 2;
-            const half8_t* x8 = (const half8_t*)(smem + lay.xf);
-            for (int dd = 0; dd < DC32; ++dd) {
-              const half8_t* xhv = x8 + (2 * dd) * NB * 64;
-              const half8_t* xlv = x8 + (2 * dd + 1) * NB * 64;
-              const half8_t ah = xhv[i * 64 + lane], al = xlv[i * 64 + lane];
-              const half8_t bh = xhv[j * 64 + lane], bl = xlv[j * 64 + lane];
-              g = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, g, 0, 0, 0);
-              g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, g, 0, 0, 0);
-              g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, g, 0, 0, 0);
-            }
-            const f32x4 nr = *(const f32x4*)&nrm[16 * i + 4 * grp];
-            const int col = 16 * j + c;
-            const float nc = nrm[col];
-            f32x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = 16 * i + 4 * grp + r;
-              float dist = __builtin_fmaf(gm2, g[r], nr[r] + nc);
-              dist = dist < 0.f ? 0.f : dist;  // clamp_min(0), NaN-propagating like torch
-              float v = s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);
-              if (row == col) v = diagval;
-              if (row >= N || col >= N) v = (row == col) ? 1.f : 0.f;
-              o[r] = -v;
-            }
-            acc[s] = o;
+      // right-hand side: this wave's block rows of rw <- -(y - c) (fresh per attempt)
+      for (int i = wave; i < NB; i += WK)
+        if (lane < 16) rw[16 * i + lane] = -rv[16 * i + lane];
+      // ---- 4. RBF of block rows 0 and 1 (the rest is deferred into the
+      // factorisation steps); the owners of (0,0), (0,1), (1,1) build and hand
+      // those over first, so the diagonal wave starts right away.
+      {
+        const int wv = launder_s(wave);
+        // every worker writes the same value; nobody reads it before this
+        // attempt's first RBF tile (the failed attempt ended at a worker_sync)
+        if (lane == 0) *(__attribute__((address_space(3))) volatile float*)&smem[lay.rbfc + 2] = diagval;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        const RbfK rk = read_rbfk(smem + lay.rbfc);
+        constexpr int P0 = plan_P<NB>(0);
+        constexpr int P1 = NB > 1 ? plan_P<NB>(1) : 0;
+        constexpr int T01 = P0 + 1;
+        const int e0 = 32 * attempt;
+        if (wv == P0 % WK) {
+          acc[P0 / WK] = rbf_tile<NB, FULL>(smem, rk, 0, 0, lane, N);
+          publish_tile(dsc, lane, acc[P0 / WK], vflag, kFlagT00, e0);
+        }
+        if constexpr (NB > 1) {
+          if (wv == T01 % WK) {
+            acc[T01 / WK] = rbf_tile<NB, FULL>(smem, rk, 0, 1, lane, N);
+            publish_tile(hbuf, lane, acc[T01 / WK], vflag, kFlagHA, e0);
+          }
+          if (wv == P1 % WK) {
+            acc[P1 / WK] = rbf_tile<NB, FULL>(smem, rk, 1, 1, lane, N);
+            publish_tile(hbuf + 256, lane, acc[P1 / WK], vflag, kFlagHB, e0);
           }
         }
-        if constexpr (s == P0 / WK) {
-          if (wv == P0 % WK) {
-            *(f32x4*)&dsc[lane * 4] = acc[s];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            if (lane == 0) vflag[1] = 32 * attempt;
+        static_for_desc<SLOTS>([&](auto I) {
+          constexpr int s = decltype(I)::value;
+          const int t = wv + WK * s;
+          if (t < NT) {
+            bool sk = false;
+            if constexpr (s == P0 / WK) sk = sk || (wv == P0 % WK);
+            if constexpr (NB > 1 && s == T01 / WK) sk = sk || (wv == T01 % WK);
+            if constexpr (NB > 1 && s == P1 / WK) sk = sk || (wv == P1 % WK);
+            if (!sk) {
+              if (t >= P1) {
+                const int pk = plan_tile<NB, WK * s, WK * s + WK - 1>(t);
+                acc[s] = rbf_tile<NB, FULL>(smem, rk, pk & 255, pk >> 8, lane, N);
+              } else {
+                acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+              }
+            }
           }
-        }
-      });
-    }
+        });
+      }
       GPK_STAMP(1)
-      sumz2 = 0.f;
-      WorkerCtx wx{panel, dsc, wbuf, vflag, Lb, zout, rw, N, b, lane, c, grp, launder_s(wave), 32 * attempt, 0.f};
-      failed = worker_steps<NB, WK, SLOTS, 0>(acc, wx);
+      wx.epoch0 = 32 * attempt;
+      wx.sumz2 = 0.f;
+      if constexpr (STAMPS) {
+        wx.st = wst;
+        wst[8] = st_last;
+      }
+      failed = worker_steps<NB, WK, SLOTS, 0, STAMPS, FULL>(acc, wx);
+      if constexpr (STAMPS) st_last = wst[8];
       sumz2 = wx.sumz2;
-      GPK_STAMP(4)
       if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
-      info_w = failed;
+      // every worker has left the failed attempt before anyone rebuilds
+      worker_sync<WK>(wx);
+    }
+    if constexpr (STAMPS) {
+      for (int q = 2; q < 8; ++q) st_acc[q] += wst[q];
     }
   }
-  if (!failed) {
-    // ---- 5. reduce logdet / |z|^2 over waves, write the MLL ---------------
-    if (lane == 0) red[wave] = logdet;
-    const float z2 = wave_sum(sumz2);
-    if (lane == 0) red[W + wave] = z2;
-    barrier_lds();
-    if (tid == 0) {
+  // ---- 5. reduce logdet / |z|^2 over waves, write the MLL ---------------
+  const float ld_wave = wave_sum(logdet) * 0.69314718055994531f;  // v_log_f32 is log2
+  if (lane == 0) red[wave] = ld_wave;
+  const float z2 = wave_sum(sumz2);
+  if (lane == 0) red[W + wave] = z2;
+  barrier_lds();
+  if (tid == 0) {
+    const int fcol = vflag[kFlagFail + att_end];
+    if (vflag[kFlagTmo] != 0) {
+      info[b] = kInfoTimeout;
+      mll[b] = __builtin_nanf("");
+    } else if (fcol != 0) {
+      info[b] = fcol;
+      mll[b] = __builtin_nanf("");
+    } else {
       float ld = 0.f, zz = 0.f;
       for (int w = 0; w < W; ++w) { ld += red[w]; zz += red[W + w]; }
       ld -= (float)(2 * sh) * (float)N * 0.69314718055994531f;  // - N log sigma^2
       mll[b] = -0.5f * (zz + ld + (float)N * kLog2Pi) / (float)N;
       info[b] = info_w;
     }
-    if constexpr (STAMPS) {
-      GPK_STAMP(5)
-      if (tid == 0) {
-        unsigned long long* o = stamps + (size_t)b * 16;
-        for (int q = 0; q < 8; ++q) o[q] = st_acc[q];
-        o[7] = ((unsigned long long*)(red + 4 * W + 24))[0];
-        o[10] = (unsigned)flag[16];
-        o[11] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
-        o[12] = (unsigned)flag[17];
-        o[8] = __builtin_amdgcn_s_memtime() - st_t0;
-        o[9] = __builtin_amdgcn_s_memrealtime() - st_rt0;
-      }
+  }
+  if constexpr (STAMPS) {
+    if (tid == 0) {
+      unsigned long long* o = stamps + (size_t)b * 32;
+      for (int q = 0; q < 8; ++q) o[q] = q < 2 ? st_acc[q] : 0;
+      for (int q = 2; q < 8; ++q) o[16 + q] = st_acc[q];
+      o[13] = ((unsigned long long*)(red + 4 * W + 24))[0];
+      o[14] = ((unsigned long long*)(red + 4 * W + 26))[0];
+      o[15] = ((unsigned long long*)(red + 4 * W + 28))[0];
+      for (int q = 0; q < 3; ++q) o[2 + q] = ((unsigned long long*)(red + 4 * W + 32))[q];
+      o[10] = (unsigned)flag[16];
+      o[11] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+      o[12] = (unsigned)flag[17];
+      o[8] = __builtin_amdgcn_s_memtime() - st_t0;
+      o[9] = __builtin_amdgcn_s_memrealtime() - st_rt0;
     }
-  } else if (tid == 0) {
-    info[b] = info_w;
-    mll[b] = __builtin_nanf("");
   }
 }
 
-template <int NB, bool STAMPS>
+template <int NB, bool STAMPS, bool FULL>
 int launch_exact_nb(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
-  constexpr int W = NB >= 6 ? 8 : 4;
+  constexpr int W = NB >= 12 ? GPK_EXACT_WBIG : (NB >= 6 ? 8 : 4);
   const int DC = (a.D + 15) / 16;
   const ExactLds lay = exact_lds_layout(NB, DC, W);
   const size_t lds = (size_t)lay.total * sizeof(float);
   if (DC * 16 > 64 * W || DC * 16 > 256) return -7;
   if (lds > 160 * 1024) return -7;
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)gpk_exact_kernel<NB, W, STAMPS>,
+    (void)hipFuncSetAttribute((const void*)gpk_exact_kernel<NB, W, STAMPS, FULL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((gpk_exact_kernel<NB, W, STAMPS>), dim3(a.B), dim3(64 * W), lds, stream,
+  hipLaunchKernelGGL((gpk_exact_kernel<NB, W, STAMPS, FULL>), dim3(a.B), dim3(64 * W), lds, stream,
                      a.X, a.y, a.hyp, a.n_ls, a.N, a.D, DC, a.jitter, a.max_tries,
                      a.L, a.z, a.mll, a.info, stamps);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
 
+template <int NB>
+int launch_exact_any(const GpkExactArgs& a, hipStream_t stream) {
+  return (a.N == 16 * NB) ? launch_exact_nb<NB, false, true>(a, nullptr, stream)
+                          : launch_exact_nb<NB, false, false>(a, nullptr, stream);
+}
+
 }  // namespace
 
 int gpk_launch_exact_stamps(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
-  if ((a.N + 15) / 16 != 16) return -6;
-  return launch_exact_nb<16, true>(a, stamps, stream);
+  if (a.N != 256) return -6;
+  return launch_exact_nb<16, true, true>(a, stamps, stream);
 }
 
 int gpk_launch_exact(const GpkExactArgs& a, hipStream_t stream) {
   const int NB = (a.N + 15) / 16;
   switch (NB) {
-#define GPK_CASE(nb) case nb: return launch_exact_nb<nb, false>(a, nullptr, stream);
+#define GPK_CASE(nb) case nb: return launch_exact_any<nb>(a, stream);
     GPK_CASE(1) GPK_CASE(2) GPK_CASE(3) GPK_CASE(4) GPK_CASE(5) GPK_CASE(6)
     GPK_CASE(7) GPK_CASE(8) GPK_CASE(9) GPK_CASE(10) GPK_CASE(11) GPK_CASE(12)
     GPK_CASE(13) GPK_CASE(14) GPK_CASE(15) GPK_CASE(16)

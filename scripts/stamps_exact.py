@@ -13,7 +13,7 @@ LN2 = math.log(2)
 hyp = ops.pack_exact_hyper(LN2, LN2 + 1e-4, 0.0, LN2, dev)
 L = torch.empty(B, N, N, device=dev); mll = torch.empty(B, device=dev)
 info = torch.empty(B, dtype=torch.int32, device=dev)
-st = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+st = torch.zeros(B, 32, dtype=torch.int64, device=dev)
 lib = _native.lib()
 for it in range(5):
     rc = lib.gpk_debug_exact_stamps(X.data_ptr(), y.data_ptr(), hyp.data_ptr(), 1, B, N, D, 1e-6, 3,
@@ -22,12 +22,15 @@ for it in range(5):
     assert rc == 0
 torch.cuda.synchronize()
 s = st.cpu().numpy().astype(np.float64)
-names = ["prologue", "RBF", "-", "-", "steps total (wave0)", "final", "-", "diag_factor total (diag wave)"]
+names = ["prologue", "RBF rows 0-1"]
 tot = s[:, 8]
 print(f"B={B} total cycles: mean {tot.mean():.0f} min {tot.min():.0f} max {tot.max():.0f}")
 print(f"clock GHz (memtime/realtime): {np.mean(s[:, 8] / (s[:, 9] / 100e6)) / 1e9:.3f}")
 for i, n in enumerate(names):
     print(f"  {n:22s} {s[:, i].mean():10.0f}  ({100 * s[:, i].mean() / tot.mean():5.1f}%)")
+for i, n in [(18, "w0: trailing upd"), (19, "w0: deferred RBF"), (20, "w0: TRSM"), (21, "w0: worker barrier"),
+             (22, "w0: zero-L + RHS"), (23, "w0: wait R_kk^-T"), (2, "diag: tile load"), (3, "diag: sweep"), (4, "diag: publish"), (13, "diag: factor"), (14, "diag: wait look-ahead tiles"), (15, "diag: look-ahead compute")]:
+    print(f"  {n:28s} {s[:, i].mean():10.0f}  ({100 * s[:, i].mean() / tot.mean():5.1f}%)")
 
 hw = s[:, 10].astype(np.int64)
 hw0 = s[:, 11].astype(np.int64)
