@@ -109,6 +109,20 @@ GPK_DEVICE float wave_max(float v) {
   return __builtin_fmaxf(readlane_f(v, 0), readlane_f(v, 32));
 }
 
+// Max over the wave with DPP row permutes (pure VALU: no LDS-unit round trips,
+// which queue behind other waves' LDS traffic) and four readlanes.
+#define GPK_DPP_MAX(ctrl) \
+  v = __builtin_fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false)));
+GPK_DEVICE float wave_max_dpp(float v) {
+  GPK_DPP_MAX(0xB1)   // quad_perm [1,0,3,2]
+  GPK_DPP_MAX(0x4E)   // quad_perm [2,3,0,1]
+  GPK_DPP_MAX(0x141)  // row_half_mirror
+  GPK_DPP_MAX(0x140)  // row_mirror
+  return __builtin_fmaxf(__builtin_fmaxf(readlane_f(v, 0), readlane_f(v, 16)),
+                         __builtin_fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
+}
+#undef GPK_DPP_MAX
+
 GPK_DEVICE double wave_sum_d(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -659,7 +659,6 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
   constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
   constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
-  const bool own_rhs = (rfirst == K);
   {
     const f32x4 q = load_w(x.wbuf + (K & 1) * 256, c, grp);
     // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
@@ -678,7 +677,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
         }
       });
     }
-    if (own_rhs) {
+    if (rfirst == K) {
       f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
       half4_t h, l;
@@ -725,7 +724,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   constexpr int SLOTS = (NT + WK - 1) / WK;
   constexpr int T = 64 * W;
   // Diagnostic-only phase clocks (STAMPS build): wave 0 lane 0 of each workgroup.
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0, st_t0 = 0, st_rt0 = 0;
+  unsigned long long st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0, st_t0 = 0, st_rt0 = 0;
 #define GPK_STAMP(slot)                                         \
   if constexpr (STAMPS) {                                       \
     __builtin_amdgcn_sched_barrier(0);                          \
@@ -789,6 +788,9 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   {
     const int chunks = NP * DC;  // (row, 16-col chunk) pairs
     float mx = 0.f;              // max |x / l| (bounds the centred values for the f16 split)
+    // x / l as x * (1 / l): one uniform division (GPyTorch divides; the <= 1 ulp
+    // difference is far inside the 1e-4 parity bound)
+    const float inv_l0 = 1.f / hyp[3];
     for (int base = 0; base < chunks; base += T) {
       const int q = base + tid;
       float v[16];
@@ -807,21 +809,26 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
           for (int e = 0; e < 16; ++e)
             v[e] = (n < N && d0 + e < D) ? Xb[(size_t)n * D + d0 + e] : 0.f;
         }
+        if (n_ls == 1) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int d = d0 + e;
-          if (d < D && n < N) v[e] = v[e] / hyp[3 + (n_ls == 1 ? 0 : d)];
-          mx = __builtin_fmaxf(mx, __builtin_fabsf(v[e]));
+          for (int e = 0; e < 16; ++e) v[e] *= inv_l0;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (d0 + e < D) v[e] = v[e] / hyp[3 + d0 + e];
         }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = __builtin_fmaxf(mx, __builtin_fabsf(v[e]));
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           *(f32x4*)&xf[frag_index(n, d0 + 4 * u, NB)] = f32x4{v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]};
       }
     }
-    mx = wave_max(mx);
+    mx = wave_max_dpp(mx);
     if (lane == 0) red[wave] = mx;
   }
   barrier_lds();
+  GPK_STAMP(8)  // X loads + fp32 staging + max
   if (tid == 0) {
     flag[0] = 0;
     flag[kFlagT00] = -1;
@@ -856,12 +863,14 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       cpart[part * DP + d] = (sacc[0] + sacc[1]) + (sacc[2] + sacc[3]);
     }
     barrier_lds();
+    GPK_STAMP(9)  // column partial sums
     if (tid < DP) {
       float s = 0.f;
       for (int p = 0; p < parts; ++p) s += cpart[p * DP + tid];
       cpart[64 * W + tid] = s / (float)N;
     }
     barrier_lds();
+    GPK_STAMP(10)  // mean
   }
   // ---- 3. subtract the mean, squared norms, residual r = y - c -----------
   // The centred rows are split into f16 hi + lo parts (x = hi + lo + O(2^-22 x))
@@ -922,6 +931,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         }
       }
       barrier_lds();
+      GPK_STAMP(11)  // centre + f16 split (per 32-col chunk)
     }
     if (n < NP) {
       nrm[n] = s;
@@ -1110,6 +1120,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       unsigned long long* o = stamps + (size_t)b * 32;
       for (int q = 0; q < 8; ++q) o[q] = q < 2 ? st_acc[q] : 0;
       for (int q = 2; q < 8; ++q) o[16 + q] = st_acc[q];
+      for (int q = 8; q < 12; ++q) o[16 + q] = st_acc[q];
       o[13] = ((unsigned long long*)(red + 4 * W + 24))[0];
       o[14] = ((unsigned long long*)(red + 4 * W + 26))[0];
       o[15] = ((unsigned long long*)(red + 4 * W + 28))[0];

@@ -28,7 +28,8 @@ print(f"B={B} total cycles: mean {tot.mean():.0f} min {tot.min():.0f} max {tot.m
 print(f"clock GHz (memtime/realtime): {np.mean(s[:, 8] / (s[:, 9] / 100e6)) / 1e9:.3f}")
 for i, n in enumerate(names):
     print(f"  {n:22s} {s[:, i].mean():10.0f}  ({100 * s[:, i].mean() / tot.mean():5.1f}%)")
-for i, n in [(18, "w0: trailing upd"), (19, "w0: deferred RBF"), (20, "w0: TRSM"), (21, "w0: worker barrier"),
+for i, n in [(24, "pro: X loads+staging+max"), (25, "pro: column partials"), (26, "pro: mean"),
+             (27, "pro: centre+split"), (18, "w0: trailing upd"), (19, "w0: deferred RBF"), (20, "w0: TRSM"), (21, "w0: worker barrier"),
              (22, "w0: zero-L + RHS"), (23, "w0: wait R_kk^-T"), (2, "diag: tile load"), (3, "diag: sweep"), (4, "diag: publish"), (13, "diag: factor"), (14, "diag: wait look-ahead tiles"), (15, "diag: look-ahead compute")]:
     print(f"  {n:28s} {s[:, i].mean():10.0f}  ({100 * s[:, i].mean() / tot.mean():5.1f}%)")
 
