@@ -30,6 +30,10 @@ SIGNATURES = {
     "gpk_exact_mll_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                   c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
+    "gpk_exact_grad_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "gpk_exact_mll_grad_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                       c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p]),
     "gpk_kzz_chol_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_float, c_double, c_int,
                                  c_void_p, c_void_p, c_void_p, c_void_p]),
     "gpk_variational_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

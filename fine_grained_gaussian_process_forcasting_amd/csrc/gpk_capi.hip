@@ -41,6 +41,30 @@ int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp, int n_le
   return gpk_launch_exact(a, (hipStream_t)stream);
 }
 
+size_t gpk_exact_grad_workspace_bytes(int B, int N) {
+  if (B < 0 || N < 1 || N > gpk_exact_max_n()) return 0;
+  return gpk_exact_grad_ws_floats(B, N) * sizeof(float);
+}
+
+int gpk_exact_mll_grad_f32(const float* X, const float* L, const float* z, const float* hyp,
+                           int n_lengthscale, int B, int N, int D, const float* gout, void* workspace,
+                           float* dX, float* dy, float* dhyp, void* stream) {
+  if (X == nullptr) return -1;
+  if (L == nullptr) return -2;
+  if (z == nullptr) return -3;
+  if (hyp == nullptr) return -4;
+  if (n_lengthscale != 1 && n_lengthscale != D) return -5;
+  if (B < 0) return -6;
+  if (N < 1 || N > gpk_exact_max_n()) return -7;
+  if (D < 1 || D > 64) return -8;
+  if (gout == nullptr) return -9;
+  if (workspace == nullptr && B > 0) return -10;
+  if (dhyp == nullptr) return -13;
+  if (B == 0) return 0;
+  GpkExactGradArgs a{X, L, z, hyp, n_lengthscale, B, N, D, gout, (float*)workspace, dX, dy, dhyp};
+  return gpk_launch_exact_grad(a, (hipStream_t)stream);
+}
+
 int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitter,
                      double chol_jitter, int max_tries, double* L, double* Linv, int* info,
                      void* stream) {

@@ -17,6 +17,23 @@ struct GpkExactArgs {
 };
 
 int gpk_launch_exact(const GpkExactArgs& a, hipStream_t stream);
+
+struct GpkExactGradArgs {
+  const float* X;      // (B, N, D)
+  const float* L;      // (B, N, N) forward factor
+  const float* z;      // (B, N) forward L^{-1}(y - c)
+  const float* hyp;    // as GpkExactArgs
+  int n_ls;
+  int B, N, D;
+  const float* gout;   // (B,) d(objective)/d(mll_b)
+  float* ws;           // gpk_exact_grad_ws_floats(B, N) floats
+  float* dX;           // (B, N, D) or nullptr
+  float* dy;           // (B, N) or nullptr
+  float* dhyp;         // (B, 3 + n_ls): per-window d/d{s2, noise, c, lengthscale...}
+};
+
+size_t gpk_exact_grad_ws_floats(int B, int N);
+int gpk_launch_exact_grad(const GpkExactGradArgs& a, hipStream_t stream);
 int gpk_launch_exact_stamps(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream);
 
 struct GpkKzzArgs {

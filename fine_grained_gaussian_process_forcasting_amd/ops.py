@@ -85,6 +85,40 @@ def exact_mll(X: torch.Tensor, y: torch.Tensor, lengthscale, outputscale, mean_c
     return ExactMLLOut(mll, L, z, info)
 
 
+@dataclass
+class ExactMLLGrad:
+    dX: Optional[torch.Tensor]   # (B, N, D)
+    dy: Optional[torch.Tensor]   # (B, N)
+    dhyp: torch.Tensor           # (B, 3 + n_ls): per-window d/d{s2, noise, c, lengthscale...}
+
+
+def exact_mll_grad(X: torch.Tensor, L: torch.Tensor, z: torch.Tensor, hyper: torch.Tensor,
+                   gout: torch.Tensor, want_dX: bool = True, want_dy: bool = True) -> ExactMLLGrad:
+    """Analytic backward of ``exact_mll`` (one gfx950 kernel launch, see
+    include/gpk.h::gpk_exact_mll_grad_f32). ``L`` and ``z`` are the forward's outputs,
+    ``gout`` (B,) the incoming gradient of each window's MLL."""
+    B, N, D = X.shape
+    _require_device(X, L, z, hyper, gout)
+    X = X.contiguous().float()
+    L = L.contiguous().float()
+    z = z.contiguous().float()
+    gout = gout.reshape(B).contiguous().float()
+    dev = X.device
+    n_ls = hyper.numel() - 3
+    lib = _native.lib()
+    ws = torch.empty(max(1, lib.gpk_exact_grad_workspace_bytes(B, N) // 4), device=dev,
+                     dtype=torch.float32)
+    dX = torch.empty(B, N, D, device=dev, dtype=torch.float32) if want_dX else None
+    dy = torch.empty(B, N, device=dev, dtype=torch.float32) if want_dy else None
+    dhyp = torch.empty(B, 3 + n_ls, device=dev, dtype=torch.float32)
+    rc = lib.gpk_exact_mll_grad_f32(
+        X.data_ptr(), L.data_ptr(), z.data_ptr(), hyper.data_ptr(), n_ls, B, N, D, gout.data_ptr(),
+        ws.data_ptr(), dX.data_ptr() if dX is not None else None,
+        dy.data_ptr() if dy is not None else None, dhyp.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_exact_mll_grad_f32")
+    return ExactMLLGrad(dX, dy, dhyp)
+
+
 def check_cholesky_info(info: torch.Tensor, jitter: float, inputs=(), what: str = "cholesky") -> None:
     """GPyTorch's psd_safe_cholesky bookkeeping, from the per-window info codes.
 

@@ -1,11 +1,11 @@
 """Autograd wrappers of the gfx950 hot-path kernels.
 
-FORWARD values always come from libgpk.so (ops.py). BACKWARD (round 1, interim):
-the gradient is obtained by differentiating a torch restatement of the same
-forward on the SAME device (``_recompute_*`` below, fp32 RBF + fp64 solve exactly
-as the reference) inside ``backward`` only; its forward values are discarded.
-The analytic HIP backward (Cholesky / TRSM / RBF adjoints) is SURVEY.md §8f rank 1
-and replaces this in a later round. Nothing here runs on the CPU.
+FORWARD values always come from libgpk.so (ops.py). BACKWARD: the exact path uses
+the analytic HIP adjoint gpk_exact_mll_grad_f32 (Cholesky / TRSM / RBF adjoints in
+one kernel). The variational path (interim) differentiates a
+torch restatement of the same forward on the SAME device (``_recompute_variational``,
+fp32 RBF + fp64 solve exactly as the reference) inside ``backward`` only; its forward
+values are discarded. Nothing here runs on the CPU.
 """
 from __future__ import annotations
 
@@ -30,41 +30,32 @@ def _sq_dist(x1, x2):
     return res.clamp_min(0)
 
 
-def _recompute_exact(X, y, lengthscale, outputscale, constant, noise):
-    N = X.shape[-2]
-    xs = X / lengthscale
-    d = _sq_dist(xs, xs)
-    eye = torch.eye(N, device=X.device, dtype=X.dtype)
-    d = d * (1 - eye)  # x1 is x2: diagonal distance is exactly 0
-    K = outputscale * torch.exp(-0.5 * d) + noise * eye
-    L, _ = torch.linalg.cholesky_ex(K)
-    r = (y - constant).unsqueeze(-1)
-    z = torch.linalg.solve_triangular(L, r, upper=False)
-    inv_quad = z.pow(2).sum((-1, -2))
-    logdet = 2.0 * torch.log(torch.diagonal(L, dim1=-2, dim2=-1)).sum(-1)
-    return -0.5 * (inv_quad + logdet + N * LOG_2PI) / N
-
-
 class _ExactMLL(torch.autograd.Function):
+    """Forward: gpk_exact_mll_f32 (L and z kept when a gradient is needed).
+    Backward: gpk_exact_mll_grad_f32, the analytic HIP adjoint."""
+
     @staticmethod
     def forward(ctx, X, y, lengthscale, outputscale, constant, noise):
         hyper = ops.pack_exact_hyper(outputscale.detach(), noise.detach(), constant.detach(),
                                      lengthscale.detach(), X.device)
         jitter = 1e-6
+        need = any(ctx.needs_input_grad)
         out = ops.exact_mll(X.detach(), y.detach(), None, None, None, None, hyper=hyper,
-                            jitter=jitter, want_L=False)
+                            jitter=jitter, want_L=need, want_z=need)
         ops.check_cholesky_info(out.info, jitter, inputs=(X, y))
-        ctx.save_for_backward(X, y, lengthscale, outputscale, constant, noise)
+        if need:
+            ctx.save_for_backward(X, out.L, out.z, hyper)
+        ctx.ls_shape = lengthscale.shape
         return out.mll
 
     @staticmethod
     def backward(ctx, grad):
-        X, y, ls, s2, c, noise = ctx.saved_tensors
-        inputs = [t.detach().requires_grad_(True) for t in (X, y, ls, s2, c, noise)]
-        with torch.enable_grad():
-            mll = _recompute_exact(*inputs)
-            grads = torch.autograd.grad(mll, inputs, grad, allow_unused=True)
-        return tuple(grads)
+        X, L, z, hyper = ctx.saved_tensors
+        nx, ny = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        g = ops.exact_mll_grad(X.detach(), L, z, hyper, grad.detach(), want_dX=nx, want_dy=ny)
+        dh = g.dhyp.sum(0)
+        return (g.dX if nx else None, g.dy if ny else None, dh[3:].reshape(ctx.ls_shape),
+                dh[0].reshape(()), dh[2].reshape(()), dh[1].reshape(()))
 
 
 def exact_log_prob(X, y, lengthscale, outputscale, constant, noise) -> torch.Tensor:

@@ -62,6 +62,28 @@ int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp,
                       void* stream);
 
 /*
+ * Analytic backward of gpk_exact_mll_f32 (per window b, objective sum_b gout[b] mll[b]):
+ *   G = gout (alpha alpha^T - K_hat^{-1}) / (2N),  alpha = K_hat^{-1} (y - c) = L^{-T} z
+ *   dhyp[b] = {sum G o E, tr G, gout sum(alpha)/N, dl...}  (E = K / s2, l: 1 or D entries)
+ *   dX = dK/dX contracted with G,  dy = -gout alpha / N
+ * from the forward's L and z (nothing is refactored).
+ *
+ * Replaces (reference): the autograd backward that train.py:166 (loss.backward())
+ * runs through GPyTorch's ExactMarginalLogLikelihood for ExactGPModel
+ * (denoising_model/GPModel.py:5-13; upstream linear_operator inv_quad_logdet /
+ * psd_safe_cholesky backward, kernels/rbf_kernel.py backward); SURVEY.md §8f row 1.
+ *
+ * L : (B, N, N) float, z : (B, N) float (gpk_exact_mll_f32 outputs)   gout : (B,) float
+ * workspace : gpk_exact_grad_workspace_bytes(B, N) bytes of device memory
+ * dX : (B, N, D) float out or NULL (D <= 64)   dy : (B, N) float out or NULL
+ * dhyp : (B, 3 + n_lengthscale) float out (per window; the caller sums over b)
+ */
+size_t gpk_exact_grad_workspace_bytes(int B, int N);
+int gpk_exact_mll_grad_f32(const float* X, const float* L, const float* z, const float* hyp,
+                           int n_lengthscale, int B, int N, int D, const float* gout, void* workspace,
+                           float* dX, float* dy, float* dhyp, void* stream);
+
+/*
  * Shared inducing-point factorisation of the whitened VariationalStrategy:
  *   A    = K_ZZ + jitter (fp32 add, as K_ZZ.add_jitter), then upcast to fp64
  *   L    = psd_safe_cholesky(A) with the fp64 ladder chol_jitter * 10^t
