@@ -15,10 +15,10 @@
 // calls loss.backward(); oracle: oracle/gp_oracle.py::exact_mll_grads.
 //
 // Inputs are the forward's outputs (L, z), so nothing is refactored. One workgroup
-// (4 waves) per window, three phases separated by workgroup barriers:
+// (8 waves) per window, three phases separated by workgroup barriers:
 //   0. inverses of the 16 diagonal blocks of L (forward substitution, one lane
 //      per column, L entries read as uniform scalars);
-//   1. L^-1 by block columns (wave w owns columns J = w mod 4):
+//   1. L^-1 by block columns (wave w owns columns J = w mod 8):
 //      Linv_IJ = -Linv_II sum_{K=J}^{I-1} L_IK Linv_KJ   (fp32 MFMA 16x16x4),
 //      tiles kept in a caller workspace in acc layout (one float4 per lane);
 //   2. alpha = Linv^T z; then for every tile (I <= J): K^-1_IJ = sum_K Linv_KI^T
@@ -31,7 +31,8 @@
 
 namespace {
 
-constexpr int kT = 256;  // 4 waves
+constexpr int kNW = 8;           // waves per workgroup (one window)
+constexpr int kT = 64 * kNW;
 
 // acc-layout tile of L^T for block (I, K): lane (g, c) reg r <- L[16I + c][16K + 4g + r]
 // (padding beyond N is the identity).
@@ -84,9 +85,9 @@ gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
   float* w1 = Wx + NP * DP;            // NP
   float* alpha = w1 + NP;              // NP
   float* nrm = alpha + NP;             // NP
-  float* scr = nrm + NP;               // 4 waves x 256 (transposes)
-  float* part = scr + 4 * 256;         // kT partial sums
-  float* red = part + kT;              // 64
+  float* scr = nrm + NP;               // kNW waves x 256 (transposes)
+  float* part = scr + kNW * 256;       // kT partial sums
+  float* red = part + kT;              // 3 * kNW
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
@@ -98,7 +99,7 @@ gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
   const float gs = gw / (2.f * (float)N);
 
   // ---- 0. diagonal block inverses: lane c < 16 solves column c of L_II X = I
-  for (int I = wave; I < NB; I += 4) {
+  for (int I = wave; I < NB; I += kNW) {
     if (lane < 16) {
       float x[16];
 #pragma unroll
@@ -126,7 +127,7 @@ gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
   __syncthreads();
 
   // ---- 1. block columns of L^-1
-  for (int J = wave; J < NB; J += 4) {
+  for (int J = wave; J < NB; J += kNW) {
     for (int I = J + 1; I < NB; ++I) {
       f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
       int K = J;
@@ -179,7 +180,7 @@ gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
     }
   }
   // alpha = L^-T z (block rows I = wave mod 4); column 0 of each Z tile is live
-  for (int I = wave; I < NB; I += 4) {
+  for (int I = wave; I < NB; I += kNW) {
     f32x4 a = {0.f, 0.f, 0.f, 0.f};
     for (int K = I; K < NB; ++K) {
       f32x4 zt;
@@ -203,7 +204,7 @@ gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
   int t = 0;
   for (int J = 0; J < NB; ++J) {
     for (int I = 0; I <= J; ++I, ++t) {
-      if ((t & 3) != wave) continue;
+      if (t % kNW != wave) continue;
       // K^-1_IJ
       f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = {0.f, 0.f, 0.f, 0.f};
       int K = J;
@@ -287,7 +288,7 @@ gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
   dnz = wave_sum(dnz);
   if (lane == 0) {
     red[wave] = ds2;
-    red[4 + wave] = dnz;
+    red[kNW + wave] = dnz;
   }
   __syncthreads();
 
@@ -313,13 +314,19 @@ gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
     }
   }
   asum = wave_sum(asum);
-  if (lane == 0) red[8 + wave] = asum;
+  if (lane == 0) red[2 * kNW + wave] = asum;
   __syncthreads();
   if (tid == 0) {
     float* o = dhyp + (size_t)b * (3 + n_ls);
-    o[0] = red[0] + red[1] + red[2] + red[3];
-    o[1] = red[4] + red[5] + red[6] + red[7];
-    o[2] = gw * (red[8] + red[9] + red[10] + red[11]) * invN;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int w = 0; w < kNW; ++w) {
+      a0 += red[w];
+      a1 += red[kNW + w];
+      a2 += red[2 * kNW + w];
+    }
+    o[0] = a0;
+    o[1] = a1;
+    o[2] = gw * a2 * invN;
     if (n_ls == 1) {
       float s = 0.f;
       for (int d = 0; d < D; ++d) s += part[d];
@@ -334,7 +341,7 @@ template <int NB>
 int launch_grad_nb(const GpkExactGradArgs& a, hipStream_t stream) {
   const int DP = (a.D + 15) / 16 * 16;
   if (DP > 64) return -7;
-  const size_t lds = sizeof(float) * ((size_t)NB * 256 + 2 * (size_t)NB * 16 * DP + 3 * NB * 16 + 4 * 256 + kT + 64);
+  const size_t lds = sizeof(float) * ((size_t)NB * 256 + 2 * (size_t)NB * 16 * DP + 3 * NB * 16 + kNW * 256 + kT + 3 * kNW);
   if (lds > 160 * 1024) return -7;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)gpk_exact_grad_kernel<NB>,
