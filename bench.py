@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--D", type=int, default=32)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-grad", action="store_true", help="skip the backward side measurement")
     args = ap.parse_args()
 
     rank, local, world = env_rank_world()
@@ -111,7 +112,6 @@ def main():
     B, N, D = args.B, args.N, args.D
     X, y = make_inputs(B, N, D, dev, seed=1000 * rank)
     hyper = ops.pack_exact_hyper(LN2, LN2 + 1e-4, 0.0, LN2, dev)   # GPyTorch init values
-    L = torch.empty(B, N, N, device=dev)
 
     def step():
         out = ops.exact_mll(X, y, None, None, None, None, hyper=hyper)
@@ -162,6 +162,23 @@ def main():
         kern_ms = float(km.item())
     mean_mll = float(totals[-1].item()) / (B * world)
 
+    # Secondary (not the headline): the analytic backward of the same windows
+    # (gpk_exact_mll_grad_f32), outside the timed region above.
+    grad_ms = None
+    if not args.no_grad:
+        fw = ops.exact_mll(X, y, None, None, None, None, hyper=hyper, want_L=True, want_z=True)
+        gout = torch.ones(B, device=dev)
+        ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
+        torch.cuda.synchronize()
+        gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(5)]
+        for a, b in gev:
+            a.record()
+            ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
+            b.record()
+        torch.cuda.synchronize()
+        grad_ms = float(np.mean([a.elapsed_time(b) for a, b in gev]))
+
     if rank == 0:
         value = B * world * args.steps / elapsed
         bpw, fpw = bytes_per_window(N, D), flops_per_window(N, D)
@@ -191,6 +208,10 @@ def main():
                          "fp32_frac": fpw * B / (kern_ms * 1e-3) / FP32_PEAK},
             "mean_mll": mean_mll,
         }
+        if grad_ms is not None:
+            line["backward"] = {"kernel": "gpk_exact_mll_grad_f32", "kernel_ms": grad_ms,
+                                "windows_per_s_per_gpu": B / (grad_ms * 1e-3),
+                                "note": "analytic dX/dy/dhyper of the same windows; not the headline"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(N, D, args.cpu_seconds)
         print(json.dumps(line), flush=True)
