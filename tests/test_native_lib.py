@@ -67,3 +67,24 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(_native, "_LIB_PATH", "/nonexistent/libgpk.so")
     with pytest.raises(_native.NativeLibraryError):
         _native.lib()
+
+
+def test_grad_entry_validation_without_device():
+    from fine_grained_gaussian_process_forcasting_amd import _native
+    lib = _native.lib()
+    one = ctypes.c_void_p(16)  # never dereferenced: validation returns first
+    assert lib.gpk_exact_grad_workspace_bytes(3, 256) == 3 * 16 * 16 * 256 * 4
+    assert lib.gpk_exact_grad_workspace_bytes(3, 257) == 0
+    args = [one, one, one, one, 1, 2, 16, 4, one, one, None, None, one, None]
+    bad = list(args); bad[0] = None
+    assert lib.gpk_exact_mll_grad_f32(*bad) == -1
+    bad = list(args); bad[4] = 3
+    assert lib.gpk_exact_mll_grad_f32(*bad) == -5
+    bad = list(args); bad[6] = 300
+    assert lib.gpk_exact_mll_grad_f32(*bad) == -7
+    bad = list(args); bad[7] = 65
+    assert lib.gpk_exact_mll_grad_f32(*bad) == -8
+    bad = list(args); bad[12] = None
+    assert lib.gpk_exact_mll_grad_f32(*bad) == -13
+    bad = list(args); bad[5] = 0
+    assert lib.gpk_exact_mll_grad_f32(*bad) == 0   # B = 0: nothing to do
