@@ -271,7 +271,7 @@ constexpr int kInfoTimeout = 1 << 20;
 GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
   int n = 0;
   while (flags[idx] < target) {
-    if (flags[kFlagTmo] != 0) break;
+    if ((n & 255) == 255 && flags[kFlagTmo] != 0) break;  // (checked rarely: one LDS read per poll)
     __builtin_amdgcn_s_sleep(1);
     if (++n > (1 << 18)) {
       flags[kFlagTmo] = 1;
