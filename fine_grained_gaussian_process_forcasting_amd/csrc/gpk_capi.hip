@@ -100,6 +100,31 @@ int gpk_variational_f32(const float* X, const float* Z, const double* Linv, cons
   return gpk_launch_var(a, (hipStream_t)stream);
 }
 
+int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Linv,
+                                const float* vmean, const float* vstd, const float* hyp,
+                                const float* gmean, const float* gvar, int B, int N, int M, int D,
+                                double* dA, float* K, float* Q, float* part, void* stream) {
+  if (X == nullptr) return -1;
+  if (Z == nullptr) return -2;
+  if (Linv == nullptr) return -3;
+  if (vmean == nullptr) return -4;
+  if (vstd == nullptr) return -5;
+  if (hyp == nullptr) return -6;
+  if (gmean == nullptr) return -7;
+  if (gvar == nullptr) return -8;
+  if (B < 0) return -9;
+  if (N < 1) return -10;
+  if (M < 1 || M > 256) return -11;
+  if (D < 1 || D > 64) return -12;
+  if (dA == nullptr) return -13;
+  if (K == nullptr) return -14;
+  if (Q == nullptr) return -15;
+  if (part == nullptr) return -16;
+  if (B == 0) return 0;
+  GpkVarAdjArgs a{X, Z, Linv, vmean, vstd, hyp, gmean, gvar, B, N, M, D, dA, K, Q, part};
+  return gpk_launch_var_adjoint(a, (hipStream_t)stream);
+}
+
 // Diagnostic (not part of the product ABI): same as gpk_exact_mll_f32 for N in
 // (240, 256], plus per-workgroup phase clocks (32 x u64 per window) in `stamps`.
 int gpk_debug_exact_stamps(const float* X, const float* y, const float* hyp, int n_lengthscale,

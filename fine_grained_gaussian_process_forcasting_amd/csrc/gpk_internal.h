@@ -62,5 +62,22 @@ struct GpkVarArgs {
   float* ell;          // (B,) or nullptr: sum_i expected log prob
 };
 
+struct GpkVarAdjArgs {
+  const float* X;      // (B, N, D)
+  const float* Z;      // (M, D)
+  const double* Linv;  // (M, M)
+  const float* vmean;  // (M,)
+  const float* vstd;   // (M,)
+  const float* hyp;    // as GpkVarArgs
+  const float* gmean;  // (B, N)
+  const float* gvar;   // (B, N)
+  int B, N, M, D;
+  double* dA;          // (B, M, N) out
+  float* K;            // (B, M, N) out: K_ZX
+  float* Q;            // (B, M, N) out: (L^{-T} dA) o K_ZX
+  float* part;         // (B, 2M + 1) out: sum_i gmean A, sum_i gvar A^2, sum_i gvar
+};
+
 int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream);
+int gpk_launch_var_adjoint(const GpkVarAdjArgs& a, hipStream_t stream);
 int gpk_launch_var(const GpkVarArgs& a, hipStream_t stream);

@@ -271,6 +271,203 @@ gpk_var_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Adjoint of gpk_var_kernel (variational path). Per window and
+// 16-point block it recomputes K_ZX (fp32) and A = L^{-1} K_ZX (fp64 MFMA) exactly
+// as the forward, then with the incoming gmean / gvar (gvar masked where the
+// variance was clamped, MVN.variance):
+//   dA   = gmean_i m_m + 2 gvar_i (s_m^2 - 1) A_mi                 (fp64)
+//   dK   = L^{-T} dA   (fp64 MFMA, triangular k-steps only)
+//   Q    = dK o K_ZX   (the RBF adjoint's only per-entry quantity)
+// and writes dA (fp64), K_ZX and Q (fp32) as (B, M, N) plus per-window partial
+// sums dm = sum_i gmean A, dsm1 = sum_i gvar A^2 and sum_i gvar. The contractions
+// over points / windows (dL^{-1} = sum dA K^T, Q x / Q z) are plain GEMMs done by
+// the caller (rocBLAS through torch), and the M x M K_ZZ adjoint once per call.
+// ---------------------------------------------------------------------------
+template <int MB, int DMAX>
+__global__ void __launch_bounds__(256)
+gpk_var_adjoint_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                       const double* __restrict__ Linv, const float* __restrict__ vmean,
+                       const float* __restrict__ vstd, const float* __restrict__ hyp,
+                       const float* __restrict__ gmean, const float* __restrict__ gvar, int N,
+                       int M, int D, double* __restrict__ dA_out, float* __restrict__ K_out,
+                       float* __restrict__ Q_out, float* __restrict__ part_out) {
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  float* zt = vsm;               // 16MB x D   centred Z / l (zero-padded rows)
+  float* cm = zt + 16 * MB * D;  // D
+  float* vm = cm + D;            // 16MB  variational mean
+  float* sm1 = vm + 16 * MB;     // 16MB  s^2 - 1
+  float* dm = sm1 + 16 * MB;     // 16MB  partial sum_i gmean A
+  float* ds = dm + 16 * MB;      // 16MB  partial sum_i gvar A^2
+  float* ksm = ds + 16 * MB;     // 4 waves x 16MB x 16  K_ZX of the wave's block
+  float* red = ksm + 4 * 16 * MB * 16;  // 8
+  const int tid = threadIdx.x, T = blockDim.x;
+  const int lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int wave = tid >> 6, NW = T >> 6;
+  const int b = blockIdx.x;
+  const float s2 = hyp[0], jit = hyp[2];
+  const float* ls = hyp + 4 + D;
+  const size_t MN = (size_t)M * N;
+
+  for (int e = tid; e < 16 * MB * D; e += T) {
+    const int m = e / D;
+    zt[e] = (m < M) ? Z[e] / ls[e % D] : 0.f;
+  }
+  for (int m = tid; m < 16 * MB; m += T) {
+    vm[m] = (m < M) ? vmean[m] : 0.f;
+    const float sd = (m < M) ? vstd[m] : 1.f;
+    sm1[m] = sd * sd - 1.f;
+    dm[m] = 0.f;
+    ds[m] = 0.f;
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += T) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += zt[m * D + d];
+    cm[d] = s / (float)M;
+  }
+  __syncthreads();
+  for (int e = tid; e < M * D; e += T) zt[e] -= cm[e % D];
+  __syncthreads();
+
+  const float* Xb = X + (size_t)b * N * D;
+  float* kw = ksm + wave * 16 * MB * 16;
+  float gvsum = 0.f;
+  const float nhalf_log2e = -0.72134752044448170f;
+  const int NBLK = (N + 15) / 16;
+  for (int nb = wave; nb < NBLK; nb += NW) {
+    const int i = 16 * nb + c;
+    float xr[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)
+      xr[d] = (d < D && i < N) ? Xb[(size_t)i * D + d] / ls[d] - cm[d] : 0.f;
+    f64x4 acc[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int s = 0; s < 4 * MB; ++s) {
+      const int p = 4 * s + g;
+      float dist = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        if (d < D) {
+          const float df = zt[p * D + d] - xr[d];
+          dist = __builtin_fmaf(df, df, dist);
+        }
+      }
+      const float kv = (p < M && i < N) ? s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist) : 0.f;
+      kw[p * 16 + c] = kv;
+      if (p < M && i < N) K_out[(size_t)b * MN + (size_t)p * N + i] = kv;
+      const double kd = (double)kv;
+      const int mb0 = (4 * s) >> 4;
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        if (mb >= mb0) {
+          const int m = 16 * mb + c;
+          const double a = (m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
+          acc[mb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, kd, acc[mb], 0, 0, 0);
+        }
+      }
+    }
+    // acc[mb][r] = A[16 mb + g + 4 r][16 nb + c]; the variance (for the clamp mask)
+    float vpart = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a32 = (float)acc[mb][r];
+        vpart = __builtin_fmaf(a32 * a32, sm1[16 * mb + g + 4 * r], vpart);
+      }
+    }
+    vpart += __shfl_xor(vpart, 16, 64);
+    vpart += __shfl_xor(vpart, 32, 64);
+    const float var_i = s2 + jit + vpart;
+    const float gm = (i < N) ? gmean[(size_t)b * N + i] : 0.f;
+    float gv = (i < N) ? gvar[(size_t)b * N + i] : 0.f;
+    if (var_i < 1e-6f) gv = 0.f;  // clamp_min(1e-6): no gradient below the clamp
+    if (g == 0) gvsum += gv;
+    // dA (fp64, C layout of A), partial sums for dm / ds, dA out
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * mb + g + 4 * r;
+        const double a = acc[mb][r];
+        const float a32 = (float)a;
+        const double da = (double)gm * (double)vm[m] + 2.0 * (double)gv * (double)sm1[m] * (double)a32;
+        acc[mb][r] = da;
+        float pm = gm * a32, ps = gv * a32 * a32;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {  // sum over the 16 points of the block
+          pm += __shfl_xor(pm, off, 64);
+          ps += __shfl_xor(ps, off, 64);
+        }
+        if (c == 0 && m < M) {
+          (void)__hip_atomic_fetch_add(&dm[m], pm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          (void)__hip_atomic_fetch_add(&ds[m], ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (m < M && i < N) dA_out[(size_t)b * MN + (size_t)m * N + i] = da;
+      }
+    }
+    // dK = L^{-T} dA: output block pb, k-steps s >= 4 pb (L^{-1}[m][p] = 0 for m < p);
+    // the B operand of k-step s is dA[4s + g][c] = acc[s / 4][s % 4]
+#pragma unroll
+    for (int pb = 0; pb < MB; ++pb) {
+      f64x4 dk = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 4 * pb; s < 4 * MB; ++s) {
+        const int m = 4 * s + g, p = 16 * pb + c;
+        const double a = (m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
+        dk = __builtin_amdgcn_mfma_f64_16x16x4f64(a, acc[s >> 2][s & 3], dk, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = 16 * pb + g + 4 * r;
+        if (p < M && i < N) Q_out[(size_t)b * MN + (size_t)p * N + i] = (float)dk[r] * kw[p * 16 + c];
+      }
+    }
+  }
+  gvsum = wave_sum(gvsum);
+  if (lane == 0) red[wave] = gvsum;
+  __syncthreads();
+  // per-window partials: [dm (M), ds (M), sum gvar]
+  float* po = part_out + (size_t)b * (2 * M + 1);
+  for (int m = tid; m < M; m += T) {
+    po[m] = dm[m];
+    po[M + m] = ds[m];
+  }
+  if (tid == 0) {
+    float s = 0.f;
+    for (int q = 0; q < NW; ++q) s += red[q];
+    po[2 * M] = s;
+  }
+}
+
+template <int MB, int DMAX>
+int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
+  const size_t lds = (size_t)(16 * MB * a.D + a.D + 4 * 16 * MB + 4 * 16 * MB * 16 + 8) * sizeof(float);
+  if (lds > 160 * 1024) return -10;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)gpk_var_adjoint_kernel<MB, DMAX>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((gpk_var_adjoint_kernel<MB, DMAX>), dim3(a.B), dim3(256), lds, stream, a.X,
+                     a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.N, a.M, a.D, a.dA,
+                     a.K, a.Q, a.part);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+template <int DMAX>
+int launch_var_adj_d(const GpkVarAdjArgs& a, hipStream_t stream) {
+  switch ((a.M + 15) / 16) {
+#define GPK_VCASE(mb) case mb: return launch_var_adj<mb, DMAX>(a, stream);
+    GPK_VCASE(1) GPK_VCASE(2) GPK_VCASE(3) GPK_VCASE(4) GPK_VCASE(5) GPK_VCASE(6)
+    GPK_VCASE(7) GPK_VCASE(8) GPK_VCASE(9) GPK_VCASE(10) GPK_VCASE(11) GPK_VCASE(12)
+    GPK_VCASE(13) GPK_VCASE(14) GPK_VCASE(15) GPK_VCASE(16)
+#undef GPK_VCASE
+    default: return -10;
+  }
+}
+
 template <int MB, int DMAX>
 int launch_var(const GpkVarArgs& a, hipStream_t stream) {
   const size_t lds = (size_t)(16 * MB * a.D + a.D + 2 * 16 * MB + 8) * sizeof(float);
@@ -307,6 +504,13 @@ int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
                      a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.Linv, a.info);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
+}
+
+int gpk_launch_var_adjoint(const GpkVarAdjArgs& a, hipStream_t stream) {
+  if (a.D <= 16) return launch_var_adj_d<16>(a, stream);
+  if (a.D <= 32) return launch_var_adj_d<32>(a, stream);
+  if (a.D <= 64) return launch_var_adj_d<64>(a, stream);
+  return -11;
 }
 
 int gpk_launch_var(const GpkVarArgs& a, hipStream_t stream) {

@@ -240,3 +240,40 @@ def variational_forward(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
         _stream_ptr(dev))
     _native.check(rc, "gpk_variational_f32")
     return VariationalOut(mean, var, ell)
+
+
+@dataclass
+class VariationalAdjoint:
+    dA: torch.Tensor    # (B, M, N) float64: dObjective / dA
+    K: torch.Tensor     # (B, M, N) K_ZX
+    Q: torch.Tensor     # (B, M, N) (Linv^T dA) o K_ZX
+    part: torch.Tensor  # (B, 2M + 1): sum_i gmean A, sum_i gvar A^2, sum_i gvar
+
+
+def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vmean: torch.Tensor,
+                        vstd: torch.Tensor, hyper: torch.Tensor, gmean: torch.Tensor,
+                        gvar: torch.Tensor) -> VariationalAdjoint:
+    """Per-window adjoint of ``variational_forward`` (one gfx950 launch,
+    include/gpk.h::gpk_variational_adjoint_f32)."""
+    B, N, D = X.shape
+    M = Z.shape[0]
+    _require_device(X, Z, Linv, vmean, vstd, hyper, gmean, gvar)
+    dev = X.device
+    X = X.contiguous().float()
+    Z = Z.contiguous().float()
+    Linv = Linv.contiguous().double()
+    vmean = vmean.reshape(M).contiguous().float()
+    vstd = vstd.reshape(M).contiguous().float()
+    gmean = gmean.reshape(B, N).contiguous().float()
+    gvar = gvar.reshape(B, N).contiguous().float()
+    dA = torch.empty(B, M, N, device=dev, dtype=torch.float64)
+    K = torch.empty(B, M, N, device=dev, dtype=torch.float32)
+    Q = torch.empty(B, M, N, device=dev, dtype=torch.float32)
+    part = torch.empty(B, 2 * M + 1, device=dev, dtype=torch.float32)
+    rc = _native.lib().gpk_variational_adjoint_f32(
+        X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
+        hyper.data_ptr(), gmean.data_ptr(), gvar.data_ptr(), B, N, M, D, dA.data_ptr(), K.data_ptr(),
+        Q.data_ptr(), part.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_variational_adjoint_f32")
+    return VariationalAdjoint(dA, K, Q, part)
+

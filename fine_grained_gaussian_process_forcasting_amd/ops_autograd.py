@@ -1,11 +1,12 @@
 """Autograd wrappers of the gfx950 hot-path kernels.
 
-FORWARD values always come from libgpk.so (ops.py). BACKWARD: the exact path uses
-the analytic HIP adjoint gpk_exact_mll_grad_f32 (Cholesky / TRSM / RBF adjoints in
-one kernel). The variational path (interim) differentiates a
-torch restatement of the same forward on the SAME device (``_recompute_variational``,
-fp32 RBF + fp64 solve exactly as the reference) inside ``backward`` only; its forward
-values are discarded. Nothing here runs on the CPU.
+FORWARD values always come from libgpk.so (ops.py). BACKWARD:
+the exact path uses the analytic HIP adjoint gpk_exact_mll_grad_f32 (Cholesky / TRSM /
+RBF adjoints in one kernel). The variational path uses the per-window HIP adjoint
+gpk_variational_adjoint_f32 (recomputed K_ZX and A = L^-1 K_ZX, dA, L^-T dA, RBF
+adjoint weights); its contractions over points and windows are plain GEMMs (torch ->
+rocBLAS), and the shared M x M K_ZZ factor is differentiated once per call with fp64
+torch ops on the device. Nothing here runs on the CPU.
 """
 from __future__ import annotations
 
@@ -68,21 +69,22 @@ def exact_log_prob(X, y, lengthscale, outputscale, constant, noise) -> torch.Ten
     return _ExactMLL.apply(X, y, ls, s2, c, nz)
 
 
-def _recompute_variational(x, Z, vmean, vstd, s2, ls, w, b0, jitter):
+def _kzz_linv_t(Z, ls, s2, jitter):
+    """Linv(Z, l, s2) in fp64 torch ops (M x M, differentiable): the shared K_ZZ factor
+    of the forward, for its adjoint only (once per call, not per window)."""
     M = Z.shape[0]
     zs = Z / ls
-    xs = x / ls
     Kzz = s2 * torch.exp(-0.5 * _sq_dist(zs, zs))
-    Kzz = Kzz + jitter * torch.eye(M, device=x.device, dtype=x.dtype)
-    L = torch.linalg.cholesky(Kzz.double())
-    Kzx = s2 * torch.exp(-0.5 * _sq_dist(zs.expand(x.shape[0], M, -1), xs))
-    A = torch.linalg.solve_triangular(L, Kzx.double(), upper=False).to(x.dtype)
-    mean = (A * vmean.unsqueeze(-1)).sum(-2) + (x @ w.reshape(-1, 1)).squeeze(-1) + b0
-    var = s2 + jitter + (A * ((vstd.pow(2) - 1).unsqueeze(-1) * A)).sum(-2)
-    return mean, var
+    Kzz = Kzz + jitter * torch.eye(M, device=Z.device, dtype=Z.dtype)
+    L = torch.linalg.cholesky(Kzz)
+    return torch.linalg.solve_triangular(L, torch.eye(M, device=Z.device, dtype=Z.dtype), upper=False)
 
 
 class _VariationalPredict(torch.autograd.Function):
+    """Forward: gpk_kzz_chol_f64 + gpk_variational_f32. Backward: the per-window adjoint
+    gpk_variational_adjoint_f32 (A, dA, L^-T dA, RBF adjoint weights, in HIP), the
+    contractions over points / windows as plain GEMMs, and the M x M K_ZZ adjoint once."""
+
     @staticmethod
     def forward(ctx, x, Z, vmean, vstd, s2, ls, w, b0, jitter):
         dev = x.device
@@ -95,22 +97,55 @@ class _VariationalPredict(torch.autograd.Function):
         out = ops.variational_forward(x.detach(), Z.detach(), kz.Linv, vmean.detach(), vstd.detach(),
                                       hyper=hyper)
         ctx.jitter = jitter
-        ctx.save_for_backward(x, Z, vmean, vstd, s2, ls, w, b0)
+        ctx.save_for_backward(x, Z, vmean, vstd, s2, ls, w, b0, kz.Linv, kz.info, hyper)
         return out.mean, out.var
 
     @staticmethod
     def backward(ctx, gmean, gvar):
-        saved = ctx.saved_tensors
-        inputs = [t.detach().requires_grad_(True) for t in saved]
+        x, Z, vmean, vstd, s2, ls, w, b0, Linv, kinfo, hyper = ctx.saved_tensors
+        B, N, D = x.shape
+        M = Z.shape[0]
+        if gmean is None:
+            gmean = torch.zeros(B, N, device=x.device)
+        if gvar is None:
+            gvar = torch.zeros(B, N, device=x.device)
+        adj = ops.variational_adjoint(x.detach(), Z.detach(), Linv, vmean.detach(), vstd.detach(),
+                                      hyper, gmean, gvar)
+        lsv = ls.detach().reshape(-1).expand(D).float()
+        xs = x.detach().float() / lsv
+        zs = Z.detach().float() / lsv
+        Q = adj.Q
+        r = Q.sum(1)                                      # (B, N)
+        q = Q.sum((0, 2))                                 # (M,)
+        QZ = torch.einsum("bmn,md->bnd", Q, zs)
+        gm = gmean.reshape(B, N).float()
+        dX = (QZ - xs * r.unsqueeze(-1)) / lsv + gm.unsqueeze(-1) * w.detach().reshape(1, 1, D).float()
+        P = torch.einsum("bmn,bnd->md", Q, xs)
+        dZ = (P - zs * q.unsqueeze(-1)) / lsv
+        dls = ((q.unsqueeze(-1) * zs * zs).sum(0) - 2.0 * (zs * P).sum(0)
+               + torch.einsum("bn,bnd->d", r, xs * xs)) / lsv
+        ds2 = Q.sum() / s2.detach().float() + adj.part[:, 2 * M].sum()
+        dvm = adj.part[:, :M].sum(0)
+        dvs = 2.0 * vstd.detach().reshape(M).float() * adj.part[:, M:2 * M].sum(0)
+        dw = torch.einsum("bn,bnd->d", gm, x.detach().float())
+        db0 = gm.sum()
+        # shared K_ZZ factor: dLinv = sum_b dA K^T (lower part: Linv_mp is used for m >= p)
+        dLinv = torch.einsum("bmn,bpn->mp", adj.dA, adj.K.double()).tril()
+        t = int(-kinfo.item()) if int(kinfo.item()) < 0 else 0
+        jit = ctx.jitter + (1e-8 * 10 ** (t - 1) if t > 0 else 0.0)
         with torch.enable_grad():
-            mean, var = _recompute_variational(*inputs, ctx.jitter)
-            outs, gouts = [], []
-            for o, g in ((mean, gmean), (var, gvar)):
-                if g is not None:
-                    outs.append(o)
-                    gouts.append(g)
-            grads = torch.autograd.grad(outs, inputs, gouts, allow_unused=True)
-        return (*grads, None)
+            Z2 = Z.detach().double().requires_grad_(True)
+            l2 = lsv.double().requires_grad_(True)
+            s22 = s2.detach().double().reshape(()).requires_grad_(True)
+            gZ, gl, gs = torch.autograd.grad(_kzz_linv_t(Z2, l2, s22, jit), [Z2, l2, s22], dLinv)
+        dZ = dZ + gZ.float()
+        dls = dls + gl.float()
+        ds2 = ds2 + gs.float()
+        dls_out = dls.sum().reshape(ls.shape) if ls.numel() == 1 else dls.reshape(ls.shape)
+        return (dX.to(x.dtype), dZ.to(Z.dtype), dvm.reshape(vmean.shape).to(vmean.dtype),
+                dvs.reshape(vstd.shape).to(vstd.dtype), ds2.reshape(s2.shape).to(s2.dtype),
+                dls_out.to(ls.dtype), dw.reshape(w.shape).to(w.dtype), db0.reshape(b0.shape).to(b0.dtype),
+                None)
 
 
 def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module, jitter):

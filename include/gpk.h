@@ -125,6 +125,25 @@ int gpk_variational_f32(const float* X, const float* Z, const double* Linv, cons
                         const float* vstd, const float* hyp, const float* y, int B, int N, int M,
                         int D, float* mean, float* var, float* ell, void* stream);
 
+/*
+ * Per-window adjoint of gpk_variational_f32 for the objective
+ * sum(gmean * mean) + sum(gvar * var)  (var's clamp at 1e-6 passes no gradient):
+ *   dA = gmean_i m_m + 2 gvar_i (s_m^2 - 1) A_mi      -> dA   (B, M, N) double out
+ *   K_ZX                                                -> K    (B, M, N) float out
+ *   Q  = (Linv^T dA) o K_ZX                             -> Q    (B, M, N) float out
+ *   part[b] = {sum_i gmean A_mi (M), sum_i gvar A_mi^2 (M), sum_i gvar}  (B, 2M+1) float out
+ * The caller contracts these with plain GEMMs (dLinv = sum_b dA K^T; dX, dZ, dl, ds2
+ * from Q) and back-propagates dLinv through the shared M x M K_ZZ factor once.
+ *
+ * Replaces (reference): the per-window part of the autograd backward that
+ * train.py:166 runs through VariationalStrategy / DeepGPLayer for DeepGPp
+ * (denoising_model/DeepGP.py:51-99, forecast_denoising.py:86-104); SURVEY.md §8f row 1.
+ */
+int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Linv,
+                                const float* vmean, const float* vstd, const float* hyp,
+                                const float* gmean, const float* gvar, int B, int N, int M, int D,
+                                double* dA, float* K, float* Q, float* part, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
