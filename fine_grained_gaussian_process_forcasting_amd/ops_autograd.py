@@ -130,7 +130,9 @@ class _VariationalPredict(torch.autograd.Function):
         dw = torch.einsum("bn,bnd->d", gm, x.detach().float())
         db0 = gm.sum()
         # shared K_ZZ factor: dLinv = sum_b dA K^T (lower part: Linv_mp is used for m >= p)
-        dLinv = torch.einsum("bmn,bpn->mp", adj.dA, adj.K.double()).tril()
+        # (batched per window, then summed: a single M x M GEMM with a B*N-long
+        # contraction leaves the GPU idle -- one output tile)
+        dLinv = torch.bmm(adj.dA, adj.K.double().transpose(1, 2)).sum(0).tril()
         t = int(-kinfo.item()) if int(kinfo.item()) < 0 else 0
         jit = ctx.jitter + (1e-8 * 10 ** (t - 1) if t > 0 else 0.0)
         with torch.enable_grad():
