@@ -30,7 +30,7 @@ GPK_DEVICE void barrier_all() { __syncthreads(); }
 // K_ZZ build + fp64 Cholesky + inverse, one workgroup. L and Linv are the
 // caller's output buffers (M x M fp64) and double as the working matrices.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
                float jitter_var, double jitter_chol, int max_tries, double* __restrict__ L,
                double* __restrict__ Linv, int* __restrict__ info) {
@@ -40,6 +40,7 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
   float* cm = zn + M;              // D       column means
   double* bc = (double*)(((uintptr_t)(cm + D) + 15) & ~(uintptr_t)15);  // broadcast slots
   int* st = (int*)(bc + 4);
+  double* colk = bc + 8;           // 4 x M: columns k, k+1 of L; rows k, k+1 of L^{-1}
   const int tid = threadIdx.x, T = blockDim.x;
   const float s2 = hyp[0];
   const float* ls = hyp + 1;  // D lengthscales (ARD, DeepGP.py:46-49)
@@ -94,42 +95,58 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
     }
     if (tid == 0) st[0] = 0;
     barrier_all();
+    // column k of the trailing matrix and row k of L^{-1} live in LDS (cur / currow):
+    // the threads that update column k+1 / row k+1 also write them there (nxt /
+    // nxtrow), so a step never waits on a global load for its pivot or its scaling.
+    double* cur = colk;
+    double* nxt = colk + M;
+    double* currow = colk + 2 * M;
+    double* nxtrow = colk + 3 * M;
+    for (int i = tid; i < M; i += T) {
+      cur[i] = L[(size_t)i * M];
+      currow[i] = (i == 0) ? 1.0 : 0.0;
+    }
+    barrier_all();
     int failed = 0;
+    const int wv = tid >> 6, ln = tid & 63, NWV = T >> 6;
     for (int k = 0; k < M; ++k) {
-      if (tid == 0) {
-        const double piv = L[(size_t)k * M + k];
-        if (!(piv > 0.0)) { st[0] = k + 1; bc[0] = 1.0; }
-        else {
-          const double lkk = __builtin_sqrt(piv);
-          L[(size_t)k * M + k] = lkk;
-          bc[0] = 1.0 / lkk;
+      const double piv = cur[k];
+      if (!(piv > 0.0)) { failed = k + 1; break; }  // uniform: every thread reads the same LDS word
+      const double lkk = __builtin_sqrt(piv);
+      const double inv = 1.0 / lkk;
+      if (tid == 0) L[(size_t)k * M + k] = lkk;
+      for (int i = k + 1 + tid; i < M; i += T) {
+        const double v = cur[i] * inv;
+        L[(size_t)i * M + k] = v;
+        cur[i] = v;
+      }
+      for (int j = tid; j <= k; j += T) {
+        const double v = currow[j] * inv;
+        Linv[(size_t)k * M + j] = v;
+        currow[j] = v;
+      }
+      barrier_all();
+      // rank-1 update of the trailing lower triangle and of L^{-1}'s rows below k:
+      // one row per wave at a time, lanes along the row (coalesced)
+      for (int i = k + 1 + wv; i < M; i += NWV) {
+        const double lik = cur[i];
+        double* Li = L + (size_t)i * M;
+        for (int j = k + 1 + ln; j <= i; j += 64) {
+          const double v = Li[j] - lik * cur[j];
+          Li[j] = v;
+          if (j == k + 1) nxt[i] = v;
+        }
+        double* Ii = Linv + (size_t)i * M;
+        for (int j = ln; j <= k; j += 64) {
+          const double v = Ii[j] - lik * currow[j];
+          Ii[j] = v;
+          if (i == k + 1) nxtrow[j] = v;
         }
       }
+      if (tid == 0 && k + 1 < M) nxtrow[k + 1] = 1.0;  // B = I: row k+1's diagonal is untouched
       barrier_all();
-      if (st[0] != 0) { failed = st[0]; break; }
-      const double inv = bc[0];
-      for (int i = k + 1 + tid; i < M; i += T) L[(size_t)i * M + k] *= inv;
-      for (int j = tid; j <= k; j += T) Linv[(size_t)k * M + j] *= inv;
-      barrier_all();
-      // rank-1 update of the trailing lower triangle and of L^{-1}'s rows below k
-      const int R = M - k - 1;
-      const int nupd = R * (R + 1) / 2;
-      for (int e = tid; e < nupd; e += T) {
-        // e -> (ii, jj), 0 <= jj <= ii < R
-        int ii = (int)((__builtin_sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
-        while ((ii + 1) * (ii + 2) / 2 <= e) ++ii;
-        while (ii * (ii + 1) / 2 > e) --ii;
-        const int jj = e - ii * (ii + 1) / 2;
-        const int i = k + 1 + ii, j = k + 1 + jj;
-        L[(size_t)i * M + j] -= L[(size_t)i * M + k] * L[(size_t)j * M + k];
-      }
-      const int ninv = R * (k + 1);
-      for (int e = tid; e < ninv; e += T) {
-        const int ii = e / (k + 1), j = e - ii * (k + 1);
-        const int i = k + 1 + ii;
-        Linv[(size_t)i * M + j] -= L[(size_t)i * M + k] * Linv[(size_t)k * M + j];
-      }
-      barrier_all();
+      double* t = cur; cur = nxt; nxt = t;
+      t = currow; currow = nxtrow; nxtrow = t;
     }
     if (!failed) {
       status = attempt > 0 ? -attempt : 0;
@@ -495,12 +512,12 @@ int launch_var_d(const GpkVarArgs& a, hipStream_t stream) {
 }  // namespace
 
 int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
-  const size_t lds = (size_t)(a.M * a.D + a.M + a.D + 16) * sizeof(float) + 64;
+  const size_t lds = (size_t)(a.M * a.D + a.M + a.D + 16) * sizeof(float) + 64 + 4 * a.M * sizeof(double) + 64;
   if (lds > 160 * 1024) return -4;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)gpk_kzz_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(gpk_kzz_kernel, dim3(1), dim3(256), lds, stream, a.Z, a.hyp, a.M, a.D,
+  hipLaunchKernelGGL(gpk_kzz_kernel, dim3(1), dim3(1024), lds, stream, a.Z, a.hyp, a.M, a.D,
                      a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.Linv, a.info);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
