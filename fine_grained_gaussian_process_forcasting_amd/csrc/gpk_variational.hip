@@ -164,6 +164,194 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
 }
 
 // ---------------------------------------------------------------------------
+// Blocked K_ZZ factorisation (one workgroup, 1024 threads, KR = 32-column blocks).
+// Same arithmetic as gpk_kzz_kernel (K_ZZ fp32 -> fp64, GPyTorch's cumulative fp64
+// ladder, L and L^{-1} of [K | I] by forward elimination) but per block of KR columns:
+//   (1) the KR x KR diagonal block and an identity are eliminated in LDS (one
+//       element per thread, one barrier per column) -> L11, L11^{-1};
+//   (2) V = L11^{-1} [Linv rows k.. (cols < k+KR) | A21^T] in LDS, one column per
+//       thread -> the final rows of L^{-1} and the final L21 (written to L2/HBM);
+//   (3) ONE trailing update of every remaining row i: target[i][c] -= sum_p V[p][i]
+//       V[p][c] (c < k+KR: L^{-1}; k+KR <= c <= i: the Schur complement), 4 x 4
+//       register tiles, lanes along c (coalesced), operands from LDS.
+// M/KR block steps instead of M serial column steps through L2.
+// ---------------------------------------------------------------------------
+constexpr int KR = 32;
+
+__global__ void __launch_bounds__(1024)
+gpk_kzz_blocked_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
+                       float jitter_var, double jitter_chol, int max_tries,
+                       double* __restrict__ L, double* __restrict__ Linv, int* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const int Mp = (M + 3) & ~3;
+  double* V = (double*)vsm;                  // KR x Mp
+  double* dg = V + KR * Mp;                  // KR x 2KR  [A11 | I] elimination
+  double* li = dg + KR * 2 * KR;             // KR x KR   L11^{-1}
+  float* zt = (float*)(li + KR * KR);        // M x D     Z / l, centred
+  float* zn = zt + M * D;                    // M
+  float* cm = zn + M;                        // D
+  const int tid = threadIdx.x, T = blockDim.x;
+  const float s2 = hyp[0];
+  const float* ls = hyp + 1;
+
+  for (int e = tid; e < M * D; e += T) zt[e] = Z[e] / ls[e % D];
+  __syncthreads();
+  for (int d = tid; d < D; d += T) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += zt[m * D + d];
+    cm[d] = s / (float)M;
+  }
+  __syncthreads();
+  for (int e = tid; e < M * D; e += T) zt[e] -= cm[e % D];
+  __syncthreads();
+  for (int m = tid; m < M; m += T) {
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s = __builtin_fmaf(zt[m * D + d], zt[m * D + d], s);
+    zn[m] = s;
+  }
+  __syncthreads();
+
+  const int jr = tid >> 5, jc = tid & 31;  // (row, column) of this thread in a KR x KR block
+  int status = 0;
+  for (int attempt = 0; attempt <= max_tries; ++attempt) {
+    double ladder = 0.0;  // GPyTorch adds (jitter_new - jitter_prev) cumulatively
+    {
+      double prev = 0.0, p10 = 1.0;
+      for (int q = 0; q < attempt; ++q) {
+        const double jn = jitter_chol * p10;
+        ladder += jn - prev;
+        prev = jn;
+        p10 *= 10.0;
+      }
+    }
+    for (int e = tid; e < M * M; e += T) {
+      const int i = e / M, j = e - i * M;
+      double a = 0.0;
+      if (j <= i) {
+        float dot = 0.f;
+        for (int d = 0; d < D; ++d) dot = __builtin_fmaf(zt[i * D + d], zt[j * D + d], dot);
+        float dist = zn[i] + zn[j] - 2.f * dot;
+        dist = dist < 0.f ? 0.f : dist;
+        float kv = s2 * __expf(-0.5f * dist);
+        if (i == j) kv = kv + jitter_var;
+        a = (double)kv;
+        if (i == j) a += ladder;
+      }
+      L[e] = a;
+      Linv[e] = (i == j) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+
+    int failed = 0;
+    for (int k = 0; k < M && !failed; k += KR) {
+      const int r = M - k < KR ? M - k : KR;
+      // (1) diagonal block, symmetric fill from the lower storage, identity padding
+      {
+        double a;
+        if (jr < r && jc < r) {
+          const int hi = jr > jc ? jr : jc, lo = jr > jc ? jc : jr;
+          a = L[(size_t)(k + hi) * M + k + lo];
+        } else {
+          a = (jr == jc) ? 1.0 : 0.0;
+        }
+        dg[jr * 2 * KR + jc] = a;
+        dg[jr * 2 * KR + KR + jc] = (jr == jc) ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      for (int j = 0; j < r; ++j) {
+        const double piv = dg[j * 2 * KR + j];
+        if (!(piv > 0.0)) { failed = k + j + 1; break; }  // uniform (same LDS word)
+        if (jr > j) {
+          const double f = dg[jr * 2 * KR + j] / piv;
+          if (jc > j) dg[jr * 2 * KR + jc] -= f * dg[j * 2 * KR + jc];
+          if (jc <= j) dg[jr * 2 * KR + KR + jc] -= f * dg[j * 2 * KR + KR + jc];
+        }
+        __syncthreads();
+      }
+      if (failed) break;
+      {
+        const double s = 1.0 / __builtin_sqrt(dg[jr * 2 * KR + jr]);
+        // L11[jc][jr] = U[jr][jc] for jc >= jr
+        if (jr < r && jc < r && jc >= jr) L[(size_t)(k + jc) * M + k + jr] = dg[jr * 2 * KR + jc] * s;
+        li[jr * KR + jc] = (jr < r && jc <= jr) ? dg[jr * 2 * KR + KR + jc] * s : 0.0;
+      }
+      // (2) stage V = [Linv rows k..k+r (cols < k+r) | A21^T]
+      for (int e = tid; e < KR * M; e += T) {
+        const int p = e / M, c = e - p * M;
+        double v = 0.0;
+        if (p < r) v = c < k + r ? Linv[(size_t)(k + p) * M + c] : L[(size_t)c * M + k + p];
+        V[p * Mp + c] = v;
+      }
+      __syncthreads();
+      for (int c = tid; c < M; c += T) {
+        double vin[KR];
+#pragma unroll
+        for (int p = 0; p < KR; ++p) vin[p] = V[p * Mp + c];
+#pragma unroll
+        for (int j = 0; j < KR; ++j) {
+          double acc = 0.0;
+#pragma unroll
+          for (int p = 0; p <= j; ++p) acc = __builtin_fma(li[j * KR + p], vin[p], acc);
+          V[j * Mp + c] = acc;
+          if (j < r) {
+            if (c < k + r) Linv[(size_t)(k + j) * M + c] = acc;
+            else L[(size_t)c * M + k + j] = acc;
+          }
+        }
+      }
+      __syncthreads();
+      // (3) trailing update of rows k+r .. M-1
+      const int i0 = k + r;
+      const int nrt = (M - i0 + 3) >> 2, nct = Mp >> 2;
+      for (int t = tid; t < nrt * nct; t += T) {
+        const int rt = t / nct, ct = t - rt * nct;
+        const int ib = i0 + 4 * rt, cb = 4 * ct;
+        if (cb > ib + 3) continue;  // tile entirely above the diagonal
+        double acc[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) acc[u][w] = 0.0;
+#pragma unroll 8
+        for (int p = 0; p < KR; ++p) {
+          const double* vr = V + p * Mp;
+          double a[4], b[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) { a[u] = vr[ib + u < Mp ? ib + u : 0]; b[u] = vr[cb + u]; }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) acc[u][w] = __builtin_fma(a[u], b[w], acc[u][w]);
+        }
+        double* tgt = cb < i0 ? Linv : L;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = ib + u;
+          if (i >= M) continue;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const int c = cb + w;
+            if (c <= i && c < M) tgt[(size_t)i * M + c] -= acc[u][w];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (!failed) {
+      status = attempt > 0 ? -attempt : 0;
+      break;
+    }
+    status = failed;
+    __syncthreads();
+  }
+  for (int e = tid; e < M * M; e += T) {
+    const int i = e / M, j = e - i * M;
+    if (j > i) { L[e] = 0.0; Linv[e] = 0.0; }
+  }
+  if (tid == 0) info[0] = status;
+}
+
+// ---------------------------------------------------------------------------
 // Batched predictive mean / variance / expected log-likelihood.
 // MB = number of 16-row blocks of the inducing dimension (M <= 16 MB),
 // DMAX = register capacity for one data point's coordinates (D <= DMAX).
