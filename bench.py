@@ -1,16 +1,27 @@
 """Benchmark of the MI355X GP hot path (BASELINE.json metric: GP windows/sec).
 
-Workload (BASELINE.json configs[3], the north-star shape, which fits one GPU):
-synthetic exact-GP windows B=512 per GPU, N=256, D=32 — per step the fused kernel
-builds the RBF Gram, runs the jittered Cholesky, the forward solve and the MLL for
-every window, writes L (B,N,N) and the MLL, then the ranks SUM-all-reduce the MLL
-partial (one fp64, RCCL over xGMI; overlapped with the next step's kernel).
-Scaling is weak: every rank owns 512 windows; value = total windows / time.
+Headline workload (BASELINE.json configs[3], the north-star shape, which fits one GPU):
+synthetic exact-GP windows, N=256, D=32 -- per step the fused kernel builds the RBF Gram,
+runs the jittered Cholesky, the forward solve and the MLL for every window and writes L
+(B,N,N) and the MLL. Weak scaling (default): every rank owns B=512 windows. Strong
+scaling (--strong): B=512 windows in total, sharded with shard_range. The per-step MLL
+partial sums stay on the device and are SUM-all-reduced across ranks once (RCCL over
+xGMI) at the end of the timed region (distributed.ObjectiveAccumulator), so no
+collective sits on a step's critical path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Side legs in the same JSON line (not the headline):
+  variational  BASELINE configs[4] per GPU: DeepGP variational path B=1024 N=256 M=64
+               D=32 -- shared K_ZZ factor (gpk_kzz_chol_f64) + column-tiled predictive
+               mean / variance / ELL (gpk_variational_f32), and the fused adjoint
+               (gpk_variational_adjoint_f32), with its compute roofline;
+  backward     the exact path's analytic adjoint on the headline windows;
+  cpu_baseline the reference's CPU arithmetic (GPyTorch's torch-CPU calls restated in
+               oracle/) on the GPU box's host cores, all threads and 1 thread, plus the
+               variational path; and the MLL relative error of the GPU kernel vs the
+               fp64 oracle on a window sample (parity unpinned vs GPyTorch: DESIGN §2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-
-Rank 0 prints ONE JSON line (contract in the task statement / DESIGN.md §6).
 """
 from __future__ import annotations
 
@@ -30,10 +41,11 @@ sys.path.insert(0, ROOT)
 
 from fine_grained_gaussian_process_forcasting_amd import ops  # noqa: E402
 from fine_grained_gaussian_process_forcasting_amd.distributed import (  # noqa: E402
-    allreduce_sum_f64, env_rank_world)
+    ObjectiveAccumulator, env_rank_world, shard_range)
 
 HBM_PEAK = 8.0e12          # B/s, MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK = 157.3e12       # FLOP/s, vector == f32 MFMA
+FP64_PEAK = 78.6e12        # FLOP/s, f64 vector == f64 MFMA
 LN2 = math.log(2.0)
 
 
@@ -45,6 +57,14 @@ def flops_per_window(N, D):
     return 3 * D * N * (N + 1) // 2 + N ** 3 // 3 + N * N + 3 * N
 
 
+def var_bytes_per_window(N, D):   # SURVEY.md §8d cfg 5: X + y read, mean + var write, ELL
+    return 4 * (N * D + N + 2 * N + 1)
+
+
+def var_flops_per_window(N, M, D):  # SURVEY.md §8d cfg 5: (fp32, fp64)
+    return 3 * D * M * N + 5 * M * N + 2 * D * N + 8 * N, M * M * N
+
+
 def make_inputs(B, N, D, device, seed):
     g = torch.Generator().manual_seed(seed)
     X = (torch.randn(B, N, D, generator=g) / math.sqrt(D)).to(device)
@@ -52,39 +72,156 @@ def make_inputs(B, N, D, device, seed):
     return X, y
 
 
-def cpu_baseline(N, D, seconds=12.0):
+class EventTimer:
+    """HIP events recorded on the launching (current) stream around each launch."""
+
+    def __init__(self):
+        self.pairs = []
+
+    def __enter__(self):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        self.pairs.append((a, b))
+        return self
+
+    def __exit__(self, *exc):
+        self.pairs[-1][1].record()
+
+    def mean_ms(self):
+        return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else 0.0
+
+
+def cpu_exact_baseline(N, D, seconds, threads):
     """GPyTorch's own CPU arithmetic for this path (oracle.exact_mll_torch_cpu: the
     _sq_dist GEMM, torch.linalg.cholesky_ex + jitter ladder, cholesky_solve, logdet;
     MKL/LAPACK) timed on the host cores, fp32 like the reference."""
     from oracle import gp_oracle as O
-    threads = torch.get_num_threads()
-    Bs = 64
-    g = torch.Generator().manual_seed(0)
-    X = torch.randn(Bs, N, D, generator=g) / math.sqrt(D)
-    y = torch.randn(Bs, N, generator=g)
-    O.exact_mll_torch_cpu(X, y, LN2, LN2, 0.0, LN2 + 1e-4)  # warm-up
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        O.exact_mll_torch_cpu(X, y, LN2, LN2, 0.0, LN2 + 1e-4)
-        n += Bs
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "windows/s", "cores": int(threads), "kind": "port",
-            "sample": f"{n} windows (batches of {Bs}, N={N}, D={D}) through "
-                      f"oracle.exact_mll_torch_cpu (GPyTorch's torch-CPU arithmetic, fp32) over "
-                      f"{dt:.1f}s; torch threads={threads}, os.cpu_count()={os.cpu_count()}"}
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        Bs = 64 if threads > 1 else 8
+        g = torch.Generator().manual_seed(0)
+        X = torch.randn(Bs, N, D, generator=g) / math.sqrt(D)
+        y = torch.randn(Bs, N, generator=g)
+        O.exact_mll_torch_cpu(X, y, LN2, LN2, 0.0, LN2 + 1e-4)  # warm-up
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            O.exact_mll_torch_cpu(X, y, LN2, LN2, 0.0, LN2 + 1e-4)
+            n += Bs
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return n / dt, f"{n} windows (batches of {Bs}, N={N}, D={D}) in {dt:.1f}s"
 
 
-def load_traffic(N, D, B):
+def cpu_var_baseline(N, M, D, seconds, threads):
+    """The reference's variational forward on the CPU (oracle.variational_forward_torch_cpu:
+    GPyTorch's torch calls incl. the per-window fp64 K_ZZ Cholesky of the expanded Z)."""
+    from oracle import gp_oracle as O
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        Bs = 64 if threads > 1 else 8
+        g = torch.Generator().manual_seed(0)
+        X = torch.randn(Bs, N, D, generator=g) / math.sqrt(D)
+        Z = torch.randn(M, D, generator=g) / math.sqrt(D)
+        args = (X, Z, np.full(D, LN2), LN2, torch.randn(D, generator=g), 0.1,
+                1e-3 * torch.randn(M, generator=g), torch.ones(M))
+        O.variational_forward_torch_cpu(*args)
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            O.variational_forward_torch_cpu(*args)
+            n += Bs
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return n / dt, f"{n} windows (batches of {Bs}, N={N}, M={M}, D={D}) in {dt:.1f}s"
+
+
+def mll_rel_err(X, y, mll_gpu, n=32):
+    """Per-window relative error of the GPU MLL vs the fp64 oracle on a window sample."""
+    from oracle import gp_oracle as O
+    idx = np.linspace(0, X.shape[0] - 1, min(n, X.shape[0])).astype(int)
+    ref = O.exact_mll(X[idx].cpu().double().numpy(), y[idx].cpu().double().numpy(), LN2, LN2, 0.0,
+                      LN2 + 1e-4)
+    got = mll_gpu[idx].cpu().double().numpy()
+    return float(np.max(np.abs(got - ref.mll) / np.abs(ref.mll)))
+
+
+def load_traffic(key):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_exact_summary.json")
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        key = f"B{B}_N{N}_D{D}"
         return d.get(key, {}).get("hbm_bytes_per_launch")
     except OSError:
         return None
+
+
+def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
+    """BASELINE configs[4] per GPU: forward (K_ZZ factor + predictive mean / var / ELL)
+    and the fused backward, HIP events per kernel launch."""
+    g = torch.Generator().manual_seed(seed)
+    X = (torch.randn(B, N, D, generator=g) / math.sqrt(D)).to(dev)
+    y = torch.randn(B, N, generator=g).to(dev)
+    Z = (torch.randn(M, D, generator=g) / math.sqrt(D)).to(dev)
+    vm = (1e-3 * torch.randn(M, generator=g)).to(dev)
+    vs = (0.5 + 0.5 * torch.rand(M, generator=g)).to(dev)
+    w = torch.randn(D, generator=g).to(dev)
+    ls = torch.full((D,), LN2, device=dev)
+    kz_h = torch.cat([torch.tensor([LN2], device=dev), ls]).contiguous()
+    hyper = ops.pack_variational_hyper(LN2, LN2 + 1e-4, 1e-4, 0.1, w, ls, D, dev)
+    gm = torch.randn(B, N, device=dev)
+    gv = torch.randn(B, N, device=dev)
+    t_kzz, t_fwd, t_bwd = EventTimer(), EventTimer(), EventTimer()
+
+    def step(timed):
+        if timed:
+            with t_kzz:
+                kz = ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h)
+            with t_fwd:
+                out = ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False)
+            with t_bwd:
+                adj = ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv)
+        else:
+            kz = ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h)
+            out = ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False)
+            adj = ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv)
+        return kz, out, adj
+
+    for _ in range(warmup):
+        step(False)
+    torch.cuda.synchronize()
+    for _ in range(steps):
+        kz, out, adj = step(True)
+    torch.cuda.synchronize()
+    ms = {"kzz": t_kzz.mean_ms(), "fwd": t_fwd.mean_ms(), "bwd": t_bwd.mean_ms()}
+    if world > 1:
+        t = torch.tensor([ms["kzz"], ms["fwd"], ms["bwd"]], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = dict(zip(["kzz", "fwd", "bwd"], t.tolist()))
+    f32, f64 = var_flops_per_window(N, M, D)
+    roof_s = f64 / FP64_PEAK + f32 / FP32_PEAK          # per window, fp64 + fp32 roofs added
+    t_fwd_s = ms["fwd"] * 1e-3
+    achieved = (f32 + f64) * B / t_fwd_s
+    return {
+        "workload": f"DeepGP variational (BASELINE configs[4]): B={B} N={N} M={M} D={D} per GPU",
+        "windows_per_s_fwd": B * world / ((ms["kzz"] + ms["fwd"]) * 1e-3),
+        "windows_per_s_train_step": B * world / ((ms["kzz"] + ms["fwd"] + ms["bwd"]) * 1e-3),
+        "kernel_ms": {"gpk_kzz_chol_f64": ms["kzz"], "gpk_variational_f32": ms["fwd"],
+                      "gpk_variational_adjoint_f32": ms["bwd"]},
+        "roofline": {"kernel": "gpk_var_fwd_kernel", "bound": "mfma",
+                     "achieved": achieved / 1e12, "peak": (f32 + f64) / roof_s / 1e12,
+                     "unit": "TFLOP/s", "frac": roof_s * B / t_fwd_s,
+                     "flops_per_window": {"fp32": f32, "fp64": f64},
+                     "hbm_frac": var_bytes_per_window(N, D) * B / t_fwd_s / HBM_PEAK,
+                     "traffic": load_traffic(f"var_B{B}_N{N}_M{M}_D{D}")},
+        "mean_ell": float(out.ell.double().mean()),
+        "info": int(kz.info.item()),
+    }
 
 
 def main():
@@ -92,95 +229,89 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--B", type=int, default=512, help="windows per GPU")
+    ap.add_argument("--B", type=int, default=512, help="windows per GPU (weak) or in total (--strong)")
     ap.add_argument("--N", type=int, default=256)
     ap.add_argument("--D", type=int, default=32)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--strong", action="store_true", help="B is the global batch, sharded over ranks")
+    ap.add_argument("--var-B", type=int, default=1024)
+    ap.add_argument("--var-N", type=int, default=256)
+    ap.add_argument("--var-M", type=int, default=64)
+    ap.add_argument("--no-var", action="store_true", help="skip the variational side leg")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grad", action="store_true", help="skip the backward side measurement")
     args = ap.parse_args()
 
     rank, local, world = env_rank_world()
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    B, N, D = args.B, args.N, args.D
-    X, y = make_inputs(B, N, D, dev, seed=1000 * rank)
+    N, D = args.N, args.D
+    if args.strong:
+        lo, hi = shard_range(args.B, rank, world)
+        B, B_total = hi - lo, args.B
+        X_all, y_all = make_inputs(args.B, N, D, "cpu", seed=0)
+        X, y = X_all[lo:hi].to(dev), y_all[lo:hi].to(dev)
+    else:
+        B, B_total = args.B, args.B * world
+        X, y = make_inputs(B, N, D, dev, seed=1000 * rank)
     hyper = ops.pack_exact_hyper(LN2, LN2 + 1e-4, 0.0, LN2, dev)   # GPyTorch init values
 
     def step():
-        out = ops.exact_mll(X, y, None, None, None, None, hyper=hyper)
-        return out
+        return ops.exact_mll(X, y, None, None, None, None, hyper=hyper)
 
-    pending = []
     for _ in range(args.warmup):
         out = step()
-        _, w = allreduce_sum_f64(out.mll.sum(dtype=torch.float64), async_op=True)
-        if w is not None:
-            pending.append(w)
-    for w in pending:
-        w.wait()
-    pending.clear()
     torch.cuda.synchronize()
-    # numerical status of the warm-up output (one sync, outside the timed region)
-    ops.check_cholesky_info(out.info, 1e-6, inputs=(X,))
+    ops.check_cholesky_info(out.info, 1e-6, inputs=(X,))   # one sync, outside the timed region
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    totals = []
+    timer = EventTimer()
+    acc = ObjectiveAccumulator(args.steps, dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record()
-        out = step()
-        ev[k][1].record()
-        tot, w = allreduce_sum_f64(out.mll.sum(dtype=torch.float64), async_op=True)
-        totals.append(tot)
-        if w is not None:
-            pending.append(w)
-    for w in pending:
-        w.wait()
+    for _ in range(args.steps):
+        with timer:
+            out = step()
+        acc.add(out.mll.sum(dtype=torch.float64))
+    totals, work = acc.reduce()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = timer.mean_ms()
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        km = torch.tensor([kern_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kern_ms = float(km.item())
-    mean_mll = float(totals[-1].item()) / (B * world)
+        elapsed, kern_ms = (float(v) for v in t.tolist())
+    mean_mll = float(totals[-1].item()) / B_total
 
-    # Secondary (not the headline): the analytic backward of the same windows
-    # (gpk_exact_mll_grad_f32), outside the timed region above.
     grad_ms = None
     if not args.no_grad:
         fw = ops.exact_mll(X, y, None, None, None, None, hyper=hyper, want_L=True, want_z=True)
         gout = torch.ones(B, device=dev)
         ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
         torch.cuda.synchronize()
-        gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(5)]
-        for a, b in gev:
-            a.record()
-            ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
-            b.record()
+        gt = EventTimer()
+        for _ in range(5):
+            with gt:
+                ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
         torch.cuda.synchronize()
-        grad_ms = float(np.mean([a.elapsed_time(b) for a, b in gev]))
+        grad_ms = gt.mean_ms()
+
+    var = None
+    if not args.no_var:
+        var = variational_leg(dev, args.var_B, args.var_N, args.var_M, D, max(5, args.steps // 5),
+                              3, world, seed=7 + rank)
 
     if rank == 0:
-        value = B * world * args.steps / elapsed
+        value = B_total * args.steps / elapsed
         bpw, fpw = bytes_per_window(N, D), flops_per_window(N, D)
         achieved = bpw * B / (kern_ms * 1e-3)
         line = {
@@ -192,19 +323,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": "exact-GP windows (BASELINE configs[3]): RBF Gram + jittered "
-                                   "Cholesky + forward solve + MLL, L written; MLL all-reduced",
-                       "windows_per_gpu": B, "N": N, "D": D, "global_batch": B * world,
+                                   "Cholesky + forward solve + MLL, L written; MLL partials "
+                                   "all-reduced once per timed region",
+                       "windows_per_gpu": B, "N": N, "D": D, "global_batch": B_total,
                        "parallelism": f"window-sharded x{world}", "kernel": "gpk_exact_mll_f32"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "traffic": load_traffic(N, D, B),
-                         "kernel_ms": kern_ms, "bytes_per_window": bpw,
-                         "fp32_flops_per_window": fpw,
+                         "traffic": load_traffic(f"exact_B{B}_N{N}_D{D}"),
+                         "kernel": "gpk_exact_kernel", "kernel_ms": kern_ms,
+                         "bytes_per_window": bpw, "fp32_flops_per_window": fpw,
                          "fp32_frac": fpw * B / (kern_ms * 1e-3) / FP32_PEAK},
             "mean_mll": mean_mll,
         }
@@ -212,8 +344,28 @@ def main():
             line["backward"] = {"kernel": "gpk_exact_mll_grad_f32", "kernel_ms": grad_ms,
                                 "windows_per_s_per_gpu": B / (grad_ms * 1e-3),
                                 "note": "analytic dX/dy/dhyper of the same windows; not the headline"}
+        if var is not None:
+            line["variational"] = var
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(N, D, args.cpu_seconds)
+            # the box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool); os.cpu_count()
+            # reports the whole machine
+            nthr = torch.get_num_threads()
+            v_all, s_all = cpu_exact_baseline(N, D, args.cpu_seconds, nthr)
+            v_one, s_one = cpu_exact_baseline(N, D, args.cpu_seconds / 2, 1)
+            line["cpu_baseline"] = {
+                "value": v_all, "unit": "windows/s", "cores": nthr, "kind": "port",
+                "sample": f"{s_all} through oracle.exact_mll_torch_cpu (GPyTorch's torch-CPU "
+                          f"arithmetic, fp32, MKL) on {nthr} host threads (the job's CPU share; "
+                          f"os.cpu_count()={os.cpu_count()})",
+                "one_thread": {"value": v_one, "cores": 1, "sample": s_one},
+                "mll_rel_err_vs_fp64_oracle": mll_rel_err(X, y, out.mll),
+            }
+            if var is not None:
+                vv, sv = cpu_var_baseline(args.var_N, args.var_M, D, args.cpu_seconds, nthr)
+                line["cpu_baseline"]["variational"] = {
+                    "value": vv, "unit": "windows/s", "cores": nthr, "kind": "port",
+                    "sample": f"{sv} through oracle.variational_forward_torch_cpu (the reference's "
+                              f"per-window fp64 K_ZZ Cholesky + TRSM), forward only"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

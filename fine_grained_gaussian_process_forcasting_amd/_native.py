@@ -38,11 +38,12 @@ SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p, c_void_p]),
     "gpk_variational_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
-                                    c_void_p, c_void_p]),
+                                    c_void_p, c_void_p, c_void_p]),
+    "gpk_variational_adjoint_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "gpk_variational_adjoint_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                             c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                            c_void_p]),
+                                            c_void_p, c_void_p]),
 }
 DEBUG_SIGNATURES = {
     "gpk_debug_exact_stamps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

@@ -71,7 +71,7 @@ int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitte
   if (Z == nullptr) return -1;
   if (hyp == nullptr) return -2;
   if (M < 1 || M > 256) return -3;
-  if (D < 1 || D > 256) return -4;
+  if (D < 1 || D > 64) return -4;
   if (max_tries < 0 || max_tries > 12) return -7;
   if (L == nullptr) return -8;
   if (Linv == nullptr) return -9;
@@ -82,7 +82,7 @@ int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitte
 
 int gpk_variational_f32(const float* X, const float* Z, const double* Linv, const float* vmean,
                         const float* vstd, const float* hyp, const float* y, int B, int N, int M,
-                        int D, float* mean, float* var, float* ell, void* stream) {
+                        int D, float* mean, float* var, float* ell, int* flags, void* stream) {
   if (X == nullptr) return -1;
   if (Z == nullptr) return -2;
   if (Linv == nullptr) return -3;
@@ -95,15 +95,22 @@ int gpk_variational_f32(const float* X, const float* Z, const double* Linv, cons
   if (D < 1 || D > 64) return -11;
   if (mean == nullptr) return -12;
   if (var == nullptr) return -13;
+  if (ell != nullptr && y == nullptr) return -7;
   if (B == 0) return 0;
   GpkVarArgs a{X, Z, Linv, vmean, vstd, hyp, y, B, N, M, D, mean, var, ell};
-  return gpk_launch_var(a, (hipStream_t)stream);
+  return gpk_launch_var(a, flags, (hipStream_t)stream);
+}
+
+size_t gpk_variational_adjoint_workspace_bytes(int B, int N, int M, int D) {
+  if (B < 1 || N < 1 || M < 1 || M > 256 || D < 1 || D > 64) return 0;
+  return gpk_var_adjoint_ws_bytes(B, N, M, D);
 }
 
 int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Linv,
                                 const float* vmean, const float* vstd, const float* hyp,
                                 const float* gmean, const float* gvar, int B, int N, int M, int D,
-                                double* dA, float* K, float* Q, float* part, void* stream) {
+                                void* workspace, float* dX, double* dLinv, float* dZ, float* dpar,
+                                void* stream) {
   if (X == nullptr) return -1;
   if (Z == nullptr) return -2;
   if (Linv == nullptr) return -3;
@@ -112,16 +119,16 @@ int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Li
   if (hyp == nullptr) return -6;
   if (gmean == nullptr) return -7;
   if (gvar == nullptr) return -8;
-  if (B < 0) return -9;
+  if (B < 1) return -9;
   if (N < 1) return -10;
   if (M < 1 || M > 256) return -11;
   if (D < 1 || D > 64) return -12;
-  if (dA == nullptr) return -13;
-  if (K == nullptr) return -14;
-  if (Q == nullptr) return -15;
-  if (part == nullptr) return -16;
-  if (B == 0) return 0;
-  GpkVarAdjArgs a{X, Z, Linv, vmean, vstd, hyp, gmean, gvar, B, N, M, D, dA, K, Q, part};
+  if (workspace == nullptr) return -13;
+  if (dX == nullptr) return -14;
+  if (dLinv == nullptr) return -15;
+  if (dZ == nullptr) return -16;
+  if (dpar == nullptr) return -17;
+  GpkVarAdjArgs a{X, Z, Linv, vmean, vstd, hyp, gmean, gvar, B, N, M, D, workspace, dX, dLinv, dZ, dpar};
   return gpk_launch_var_adjoint(a, (hipStream_t)stream);
 }
 

@@ -72,12 +72,14 @@ struct GpkVarAdjArgs {
   const float* gmean;  // (B, N)
   const float* gvar;   // (B, N)
   int B, N, M, D;
-  double* dA;          // (B, M, N) out
-  float* K;            // (B, M, N) out: K_ZX
-  float* Q;            // (B, M, N) out: (L^{-T} dA) o K_ZX
-  float* part;         // (B, 2M + 1) out: sum_i gmean A, sum_i gvar A^2, sum_i gvar
+  void* ws;            // gpk_var_adjoint_ws_bytes(B, N, M, D) bytes
+  float* dX;           // (B, N, D) out
+  double* dLinv;       // (M, M) out (lower; upper zero)
+  float* dZ;           // (M, D) out: the K_ZX part of dZ
+  float* dpar;         // (2M + 1 + D) out: dvmean, dvstd, ds2, dlengthscale
 };
 
 int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream);
+size_t gpk_var_adjoint_ws_bytes(int B, int N, int M, int D);
 int gpk_launch_var_adjoint(const GpkVarAdjArgs& a, hipStream_t stream);
-int gpk_launch_var(const GpkVarArgs& a, hipStream_t stream);
+int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream);

@@ -9,164 +9,45 @@
 //     var  = s2 + jitter + sum_m A_mi^2 (s_m^2 - 1), clamped >= 1e-6 (MVN.variance)
 //     ELL  = sum_i -0.5 [((y_i - mean_i)^2 + var_i)/noise + log noise + log 2pi]
 //
-// Two launches per call:
-//   gpk_kzz_kernel: ONE workgroup builds K_ZZ for the shared inducing points and
-//     factors it in fp64 together with L^{-1} (forward elimination of [K | I]);
-//     the reference does this b times (Z is expanded over the batch), we do it once.
-//   gpk_var_kernel: one workgroup per window; each wave owns 16-point column
-//     blocks, builds K_ZX columns in fp32 directly in the B-operand layout of
-//     v_mfma_f64_16x16x4_f64 and accumulates A = L^{-1} K_ZX in fp64 tiles
-//     (triangular L^{-1}: only k-steps p <= m), then reduces mean / var / ELL.
+// Kernels:
+//   gpk_kzz_kernel      ONE workgroup: K_ZZ of the shared inducing points, blocked fp64
+//                       Cholesky + L^{-1} (32-column blocks, GPyTorch's fp64 ladder). The
+//                       reference factors the same matrix b times (Z expanded over the batch).
+//   gpk_var_fwd_kernel  the per-point work as ONE column-tiled GEMM A = L^{-1} [K_ZX(b=0) | ...]:
+//                       a workgroup owns a chunk of TW points of one window and all M rows of A;
+//                       K_ZX chunk from an f32-MFMA Gram (GPyTorch's centred _sq_dist form) in
+//                       LDS, A in fp64 MFMA accumulators (v_mfma_f64_16x16x4f64, triangular
+//                       k-range per row tile), mean / variance reduced in the epilogue.
+//   gpk_var_ell_kernel  per-window ELL sum from the written mean / var (fixed order: deterministic).
+//   gpk_var_adj_kernel  adjoint, same tiling: recomputes K_ZX, A; dA; dK = L^{-T} dA (fp64 MFMA);
+//                       Q = dK o K_ZX; dX per point, and per-workgroup partials of
+//                       Q X (M x D), sum_i Q, dvmean, dvstd, ds2, dl (deterministic, no atomics);
+//                       dA and K_ZX (fp32, as the reference's fp32 dA) go to the workspace for
+//   gpk_dlinv_kernel    dL^{-1} = sum_points dA K_ZX^T: split-K fp64-MFMA GEMM, 64 x 64 lower tiles;
+//   gpk_var_red_kernel / gpk_var_fin_kernel  fixed-order sums of the partials -> outputs.
 #include "gpk_common.h"
 #include "gpk_internal.h"
+
+#include <mutex>
 
 namespace {
 
 constexpr float kLog2PiF = 1.8378770664093453f;
+constexpr float kNHalfLog2e = -0.72134752044448170f;  // -0.5 * log2(e)
 
-GPK_DEVICE void barrier_all() { __syncthreads(); }
+#define GPK_HOST_DEVICE_INLINE __host__ __device__ __forceinline__
 
-// ---------------------------------------------------------------------------
-// K_ZZ build + fp64 Cholesky + inverse, one workgroup. L and Linv are the
-// caller's output buffers (M x M fp64) and double as the working matrices.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024)
-gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
-               float jitter_var, double jitter_chol, int max_tries, double* __restrict__ L,
-               double* __restrict__ Linv, int* __restrict__ info) {
-  extern __shared__ __attribute__((aligned(16))) float vsm[];
-  float* zt = vsm;                 // M x D   Z / l, centred
-  float* zn = zt + M * D;          // M       squared norms
-  float* cm = zn + M;              // D       column means
-  double* bc = (double*)(((uintptr_t)(cm + D) + 15) & ~(uintptr_t)15);  // broadcast slots
-  int* st = (int*)(bc + 4);
-  double* colk = bc + 8;           // 4 x M: columns k, k+1 of L; rows k, k+1 of L^{-1}
-  const int tid = threadIdx.x, T = blockDim.x;
-  const float s2 = hyp[0];
-  const float* ls = hyp + 1;  // D lengthscales (ARD, DeepGP.py:46-49)
-
-  for (int e = tid; e < M * D; e += T) zt[e] = Z[e] / ls[e % D];
-  barrier_all();
-  for (int d = tid; d < D; d += T) {
-    float s = 0.f;
-    for (int m = 0; m < M; ++m) s += zt[m * D + d];
-    cm[d] = s / (float)M;
-  }
-  barrier_all();
-  for (int e = tid; e < M * D; e += T) zt[e] -= cm[e % D];
-  barrier_all();
-  for (int m = tid; m < M; m += T) {
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) s = __builtin_fmaf(zt[m * D + d], zt[m * D + d], s);
-    zn[m] = s;
-  }
-  barrier_all();
-
-  int status = 0;
-  for (int attempt = 0; attempt <= max_tries; ++attempt) {
-    // (re)build A = K_ZZ + jitter (fp32) -> fp64 (+ fp64 ladder), B = I
-    for (int e = tid; e < M * M; e += T) {
-      const int i = e / M, j = e - i * M;
-      double a = 0.0;
-      if (j <= i) {
-        float dot = 0.f;
-        for (int d = 0; d < D; ++d) dot = __builtin_fmaf(zt[i * D + d], zt[j * D + d], dot);
-        float dist = zn[i] + zn[j] - 2.f * dot;
-        dist = dist < 0.f ? 0.f : dist;
-        float kv = s2 * __expf(-0.5f * dist);
-        if (i == j) kv = kv + jitter_var;
-        a = (double)kv;
-        if (i == j) {
-          // GPyTorch adds (jitter_new - jitter_prev) cumulatively to Aprime
-          double acc = a;
-          double prev = 0.0;
-          for (int q = 0; q < attempt; ++q) {
-            double p10 = 1.0;
-            for (int u = 0; u < q; ++u) p10 *= 10.0;
-            const double jn = jitter_chol * p10;
-            acc += jn - prev;
-            prev = jn;
-          }
-          a = acc;
-        }
-      }
-      L[e] = a;
-      Linv[e] = (i == j) ? 1.0 : 0.0;
-    }
-    if (tid == 0) st[0] = 0;
-    barrier_all();
-    // column k of the trailing matrix and row k of L^{-1} live in LDS (cur / currow):
-    // the threads that update column k+1 / row k+1 also write them there (nxt /
-    // nxtrow), so a step never waits on a global load for its pivot or its scaling.
-    double* cur = colk;
-    double* nxt = colk + M;
-    double* currow = colk + 2 * M;
-    double* nxtrow = colk + 3 * M;
-    for (int i = tid; i < M; i += T) {
-      cur[i] = L[(size_t)i * M];
-      currow[i] = (i == 0) ? 1.0 : 0.0;
-    }
-    barrier_all();
-    int failed = 0;
-    const int wv = tid >> 6, ln = tid & 63, NWV = T >> 6;
-    for (int k = 0; k < M; ++k) {
-      const double piv = cur[k];
-      if (!(piv > 0.0)) { failed = k + 1; break; }  // uniform: every thread reads the same LDS word
-      const double lkk = __builtin_sqrt(piv);
-      const double inv = 1.0 / lkk;
-      if (tid == 0) L[(size_t)k * M + k] = lkk;
-      for (int i = k + 1 + tid; i < M; i += T) {
-        const double v = cur[i] * inv;
-        L[(size_t)i * M + k] = v;
-        cur[i] = v;
-      }
-      for (int j = tid; j <= k; j += T) {
-        const double v = currow[j] * inv;
-        Linv[(size_t)k * M + j] = v;
-        currow[j] = v;
-      }
-      barrier_all();
-      // rank-1 update of the trailing lower triangle and of L^{-1}'s rows below k:
-      // one row per wave at a time, lanes along the row (coalesced)
-      for (int i = k + 1 + wv; i < M; i += NWV) {
-        const double lik = cur[i];
-        double* Li = L + (size_t)i * M;
-        for (int j = k + 1 + ln; j <= i; j += 64) {
-          const double v = Li[j] - lik * cur[j];
-          Li[j] = v;
-          if (j == k + 1) nxt[i] = v;
-        }
-        double* Ii = Linv + (size_t)i * M;
-        for (int j = ln; j <= k; j += 64) {
-          const double v = Ii[j] - lik * currow[j];
-          Ii[j] = v;
-          if (i == k + 1) nxtrow[j] = v;
-        }
-      }
-      if (tid == 0 && k + 1 < M) nxtrow[k + 1] = 1.0;  // B = I: row k+1's diagonal is untouched
-      barrier_all();
-      double* t = cur; cur = nxt; nxt = t;
-      t = currow; currow = nxtrow; nxtrow = t;
-    }
-    if (!failed) {
-      status = attempt > 0 ? -attempt : 0;
-      break;
-    }
-    status = failed;
-    barrier_all();
-  }
-  // zero the strictly-upper triangles
-  for (int e = tid; e < M * M; e += T) {
-    const int i = e / M, j = e - i * M;
-    if (j > i) { L[e] = 0.0; Linv[e] = 0.0; }
-  }
-  if (tid == 0) info[0] = status;
+GPK_DEVICE f64x4 mfma64(double a, double b, f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+GPK_DEVICE f32x4 mfma32(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
 // Blocked K_ZZ factorisation (one workgroup, 1024 threads, KR = 32-column blocks).
-// Same arithmetic as gpk_kzz_kernel (K_ZZ fp32 -> fp64, GPyTorch's cumulative fp64
-// ladder, L and L^{-1} of [K | I] by forward elimination) but per block of KR columns:
+// K_ZZ (fp32, centred GEMM-form distances as GPyTorch's _sq_dist, + jitter) -> fp64,
+// GPyTorch's cumulative fp64 ladder, L and L^{-1} of [K | I] by blocked elimination:
 //   (1) the KR x KR diagonal block and an identity are eliminated in LDS (one
 //       element per thread, one barrier per column) -> L11, L11^{-1};
 //   (2) V = L11^{-1} [Linv rows k.. (cols < k+KR) | A21^T] in LDS, one column per
@@ -179,9 +60,9 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
 constexpr int KR = 32;
 
 __global__ void __launch_bounds__(1024)
-gpk_kzz_blocked_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
-                       float jitter_var, double jitter_chol, int max_tries,
-                       double* __restrict__ L, double* __restrict__ Linv, int* __restrict__ info) {
+gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
+               float jitter_var, double jitter_chol, int max_tries, double* __restrict__ L,
+               double* __restrict__ Linv, int* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) float vsm[];
   const int Mp = (M + 3) & ~3;
   double* V = (double*)vsm;                  // KR x Mp
@@ -271,7 +152,7 @@ gpk_kzz_blocked_kernel(const float* __restrict__ Z, const float* __restrict__ hy
       if (failed) break;
       {
         const double s = 1.0 / __builtin_sqrt(dg[jr * 2 * KR + jr]);
-        // L11[jc][jr] = U[jr][jc] for jc >= jr
+        // L11[jc][jr] = U[jr][jc] / sqrt(d_jr) for jc >= jr
         if (jr < r && jc < r && jc >= jr) L[(size_t)(k + jc) * M + k + jr] = dg[jr * 2 * KR + jc] * s;
         li[jr * KR + jc] = (jr < r && jc <= jr) ? dg[jr * 2 * KR + KR + jc] * s : 0.0;
       }
@@ -352,375 +233,879 @@ gpk_kzz_blocked_kernel(const float* __restrict__ Z, const float* __restrict__ hy
 }
 
 // ---------------------------------------------------------------------------
-// Batched predictive mean / variance / expected log-likelihood.
-// MB = number of 16-row blocks of the inducing dimension (M <= 16 MB),
-// DMAX = register capacity for one data point's coordinates (D <= DMAX).
+// Column-tile geometry shared by the forward and adjoint kernels.
+//   MB  = 16-row blocks of the inducing dimension (M <= 16 MB <= 256)
+//   4 waves = WR (along rows of A) x WC (along points); a wave owns row tiles
+//   {wr + WR j} (interleaved: balances the triangular k-range) and CT = 2 column tiles.
+//   TW  = points per chunk; a workgroup walks the chunks {part, part + S, ...} of window b.
 // ---------------------------------------------------------------------------
-template <int MB, int DMAX>
-__global__ void __launch_bounds__(256)
-gpk_var_kernel(const float* __restrict__ X, const float* __restrict__ Z,
-               const double* __restrict__ Linv, const float* __restrict__ vmean,
-               const float* __restrict__ vstd, const float* __restrict__ hyp,
-               const float* __restrict__ y, int N, int M, int D, float* __restrict__ mean_out,
-               float* __restrict__ var_out, float* __restrict__ ell_out) {
-  extern __shared__ __attribute__((aligned(16))) float vsm[];
-  float* zt = vsm;               // 16MB x D   centred Z / l (zero-padded rows)
-  float* cm = zt + 16 * MB * D;  // D
-  float* vm = cm + D;            // 16MB  variational mean
-  float* sm1 = vm + 16 * MB;     // 16MB  s^2 - 1
-  float* red = sm1 + 16 * MB;    // 8
+template <int MB>
+struct VarGeo {
+  static constexpr int WR = MB <= 4 ? 1 : (MB <= 8 ? 2 : 4);
+  static constexpr int WC = 4 / WR;
+  static constexpr int RT = (MB + WR - 1) / WR;
+  static constexpr int CT = 2;
+  static constexpr int TW = 16 * CT * WC;
+  static constexpr int MP = 16 * MB;
+  static constexpr int QST = (MP % 32 == 0) ? MP + 16 : MP;  // Q^T row stride (bank spread)
+};
+
+// D padded to a power of two >= 16 (<= 64): MFMA k-steps and d-tiles, and 256 % Dq == 0.
+GPK_HOST_DEVICE_INLINE int dq_of(int D) { return D <= 16 ? 16 : (D <= 32 ? 32 : 64); }
+
+// Stage the centred, scaled inducing points zs = Z/l - mean(Z/l) (rows >= M and
+// columns >= D zero), their squared norms, the q(u) mean and s^2 - 1.
+GPK_DEVICE void stage_inducing(const float* __restrict__ Z, const float* __restrict__ ls,
+                               const float* __restrict__ vmean, const float* __restrict__ vstd,
+                               int M, int D, int MP, int Dq, int ds, float* zs, float* zn, float* cm,
+                               float* vm, float* sm1) {
   const int tid = threadIdx.x, T = blockDim.x;
+  for (int e = tid; e < MP * Dq; e += T) {
+    const int m = e / Dq, d = e - m * Dq;
+    zs[m * ds + d] = (m < M && d < D) ? Z[m * D + d] / ls[d] : 0.f;
+  }
+  for (int m = tid; m < MP; m += T) {
+    vm[m] = (m < M) ? vmean[m] : 0.f;
+    const float sd = (m < M) ? vstd[m] : 1.f;
+    sm1[m] = sd * sd - 1.f;
+  }
+  __syncthreads();
+  for (int d = tid; d < Dq; d += T) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += zs[m * ds + d];
+    cm[d] = d < D ? s / (float)M : 0.f;  // GPyTorch _sq_dist centres by x1 = Z
+  }
+  __syncthreads();
+  for (int e = tid; e < M * Dq; e += T) {
+    const int m = e / Dq, d = e - m * Dq;
+    zs[m * ds + d] -= cm[d];
+  }
+  __syncthreads();
+  for (int m = tid; m < MP; m += T) {
+    float s = 0.f;
+    for (int d = 0; d < Dq; ++d) s = __builtin_fmaf(zs[m * ds + d], zs[m * ds + d], s);
+    zn[m] = s;
+  }
+}
+
+// Stage the chunk's points xs = x/l - cm (invalid columns zero) and their norms.
+GPK_DEVICE void stage_points(const float* __restrict__ Xw, const float* __restrict__ ls, int nvalid,
+                             int D, int TW, int Dq, int ds, const float* cm, float* xs, float* xn) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  for (int e = tid; e < TW * Dq; e += T) {
+    const int j = e / Dq, d = e - j * Dq;
+    xs[j * ds + d] = (j < nvalid && d < D) ? Xw[(size_t)j * D + d] / ls[d] - cm[d] : 0.f;
+  }
+  __syncthreads();
+  for (int j = tid; j < TW; j += T) {
+    float s = 0.f;
+    for (int d = 0; d < Dq; ++d) s = __builtin_fmaf(xs[j * ds + d], xs[j * ds + d], s);
+    xn[j] = s;
+  }
+}
+
+// K_ZX chunk (MP x TW, LDS) = s2 exp(-0.5 clamp(|zs|^2 + |xs|^2 - 2 zs.xs, 0)) on f32 MFMA.
+template <int MB, int TW>
+GPK_DEVICE void build_kzx(const float* zs, const float* xs, const float* zn, const float* xn,
+                          int M, int nvalid, int Dq, int ds, float s2, float* Kl) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = threadIdx.x >> 6;
+  constexpr int NCT = TW / 16;
+  for (int t = wave; t < MB * NCT; t += 4) {
+    const int rt = t / NCT, ct = t - rt * NCT;
+    const float* za = zs + (16 * rt + c) * ds + g;
+    const float* xb = xs + (16 * ct + c) * ds + g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < Dq / 4; ++k) acc = mfma32(za[4 * k], xb[4 * k], acc);
+    const int col = 16 * ct + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = 16 * rt + 4 * g + r;
+      float dist = zn[p] + xn[col] - 2.f * acc[r];
+      dist = dist < 0.f ? 0.f : dist;
+      Kl[p * TW + col] = (p < M && col < nvalid) ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * dist) : 0.f;
+    }
+  }
+}
+
+// A = L^{-1} K_ZX for the wave's row tiles (fp64 MFMA). acc[j][q][r] = A[16 rt_j + g + 4r][16 ct_q + c].
+// Linv loads run one k-step ahead of the MFMAs that use them.
+template <int MB>
+GPK_DEVICE void gemm_linv_k(const double* __restrict__ Linv, const float* Kl, int M,
+                            f64x4 (&acc)[VarGeo<MB>::RT][VarGeo<MB>::CT]) {
+  using G = VarGeo<MB>;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / G::WC, wc = wave - wr * G::WC;
+#pragma unroll
+  for (int j = 0; j < G::RT; ++j)
+#pragma unroll
+    for (int q = 0; q < G::CT; ++q) acc[j][q] = f64x4{0.0, 0.0, 0.0, 0.0};
+  int last = 0;
+#pragma unroll
+  for (int j = 0; j < G::RT; ++j)
+    if (wr + G::WR * j < MB) last = wr + G::WR * j;
+  const int smax = 4 * (last + 1);
+  double an[G::RT];
+  auto load_a = [&](int s, double (&dst)[G::RT]) {
+#pragma unroll
+    for (int j = 0; j < G::RT; ++j) {
+      const int rt = wr + G::WR * j;
+      const int m = 16 * rt + c, p = 4 * s + g;
+      dst[j] = (rt < MB && s < 4 * (rt + 1) && m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
+    }
+  };
+  load_a(0, an);
+  for (int s = 0; s < smax; ++s) {
+    double a[G::RT];
+#pragma unroll
+    for (int j = 0; j < G::RT; ++j) a[j] = an[j];
+    if (s + 1 < smax) load_a(s + 1, an);
+    const int p = 4 * s + g;
+    double b[G::CT];
+#pragma unroll
+    for (int q = 0; q < G::CT; ++q) b[q] = (double)Kl[p * G::TW + 16 * (wc * G::CT + q) + c];
+#pragma unroll
+    for (int j = 0; j < G::RT; ++j) {
+      const int rt = wr + G::WR * j;
+      if (rt < MB && s < 4 * (rt + 1)) {
+#pragma unroll
+        for (int q = 0; q < G::CT; ++q) acc[j][q] = mfma64(a[j], b[q], acc[j][q]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Forward: mean / variance of q(f) for every point (workgroups walk the chunk list).
+// ---------------------------------------------------------------------------
+template <int MB>
+__global__ void __launch_bounds__(256)
+gpk_var_fwd_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                   const double* __restrict__ Linv, const float* __restrict__ vmean,
+                   const float* __restrict__ vstd, const float* __restrict__ hyp, int N, int M,
+                   int D, int nchunks, float* __restrict__ mean_out, float* __restrict__ var_out,
+                   int* __restrict__ flags) {
+  using G = VarGeo<MB>;
+  constexpr int TW = G::TW, MP = G::MP;
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const int Dq = dq_of(D), ds = Dq + 2;
+  float* zs = vsm;                 // MP x ds
+  float* xs = zs + MP * ds;        // TW x ds
+  float* zn = xs + TW * ds;        // MP
+  float* xn = zn + MP;             // TW
+  float* vm = xn + TW;             // MP
+  float* sm1 = vm + MP;            // MP
+  float* cm = sm1 + MP;            // Dq
+  float* Kl = cm + Dq;             // MP x TW
+  float* redm = Kl + MP * TW;      // WR x TW
+  float* redv = redm + G::WR * TW; // WR x TW
+  const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
-  const int wave = tid >> 6, NW = T >> 6;
-  const int b = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / G::WC, wc = wave - wr * G::WC;
   // hyp: [s2, noise, jitter, b0, w[D], ls[D]]
-  const float s2 = hyp[0], noise = hyp[1], jit = hyp[2], b0 = hyp[3];
+  const float s2 = hyp[0], jit = hyp[2], b0 = hyp[3];
   const float* w = hyp + 4;
   const float* ls = hyp + 4 + D;
 
-  for (int e = tid; e < 16 * MB * D; e += T) {
-    const int m = e / D;
-    zt[e] = (m < M) ? Z[e] / ls[e % D] : 0.f;
-  }
-  for (int m = tid; m < 16 * MB; m += T) {
-    vm[m] = (m < M) ? vmean[m] : 0.f;
-    const float sd = (m < M) ? vstd[m] : 1.f;
-    sm1[m] = sd * sd - 1.f;
-  }
-  __syncthreads();
-  for (int d = tid; d < D; d += T) {
-    float s = 0.f;
-    for (int m = 0; m < M; ++m) s += zt[m * D + d];
-    cm[d] = s / (float)M;  // GPyTorch _sq_dist centres by x1 = Z
-  }
-  __syncthreads();
-  for (int e = tid; e < M * D; e += T) zt[e] -= cm[e % D];
-  __syncthreads();
-
-  const float* Xb = X + (size_t)b * N * D;
-  float ell_acc = 0.f;
-  const float log_noise = __logf(noise);
-  const float nhalf_log2e = -0.72134752044448170f;
-  const int NBLK = (N + 15) / 16;
-  for (int nb = wave; nb < NBLK; nb += NW) {
-    const int i = 16 * nb + c;
-    float xr[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d)
-      xr[d] = (d < D && i < N) ? Xb[(size_t)i * D + d] / ls[d] - cm[d] : 0.f;
-    f64x4 acc[MB];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) acc[mb] = f64x4{0.0, 0.0, 0.0, 0.0};
-    for (int s = 0; s < 4 * MB; ++s) {
-      const int p = 4 * s + g;  // inducing point of this lane's B-operand row
-      float dist = 0.f;
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        if (d < D) {
-          const float df = zt[p * D + d] - xr[d];
-          dist = __builtin_fmaf(df, df, dist);
-        }
-      }
-      const float kv = (p < M && i < N) ? s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist) : 0.f;
-      const double kd = (double)kv;
-      const int mb0 = (4 * s) >> 4;  // L^{-1}[m][p] = 0 for m < p
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        if (mb >= mb0) {
-          const int m = 16 * mb + c;  // A-operand: lane holds Linv[m][4s + g]
-          const double a = (m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
-          acc[mb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, kd, acc[mb], 0, 0, 0);
-        }
-      }
-    }
-    // acc[mb][r] = A[16 mb + g + 4 r][16 nb + c]  (f64 16x16x4 C/D layout)
-    float mpart = 0.f, vpart = 0.f;
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * mb + g + 4 * r;
-        const float a32 = (float)acc[mb][r];
-        mpart = __builtin_fmaf(a32, vm[m], mpart);
-        vpart = __builtin_fmaf(a32 * a32, sm1[m], vpart);
-      }
-    }
-    mpart += __shfl_xor(mpart, 16, 64);
-    mpart += __shfl_xor(mpart, 32, 64);
-    vpart += __shfl_xor(vpart, 16, 64);
-    vpart += __shfl_xor(vpart, 32, 64);
-    if (g == 0 && i < N) {
-      float mu = b0;
-      float lin = 0.f;
-      for (int d = 0; d < D; ++d) lin = __builtin_fmaf(Xb[(size_t)i * D + d], w[d], lin);
-      const float mean_i = mpart + (lin + mu);
-      float var_i = s2 + jit + vpart;
-      var_i = var_i < 1e-6f ? 1e-6f : var_i;  // MVN.variance clamp (fp32 min_variance)
-      mean_out[(size_t)b * N + i] = mean_i;
-      var_out[(size_t)b * N + i] = var_i;
-      if (y != nullptr) {
-        const float dy = y[(size_t)b * N + i] - mean_i;
-        ell_acc += -0.5f * ((dy * dy + var_i) / noise + log_noise + kLog2PiF);
-      }
-    }
-  }
-  if (ell_out != nullptr) {
-    ell_acc = wave_sum(ell_acc);
-    if (lane == 0) red[wave] = ell_acc;
+  stage_inducing(Z, ls, vmean, vstd, M, D, MP, Dq, ds, zs, zn, cm, vm, sm1);
+  const int nch = (N + TW - 1) / TW;
+  int clamped = 0;
+  // grid-stride over (window, chunk) pairs: the inducing-point staging is paid once
+  for (int t = blockIdx.x; t < nchunks; t += gridDim.x) {
+    const int b = t / nch, ch = t - b * nch;
+    const int i0 = ch * TW;
+    const int nvalid = N - i0 < TW ? N - i0 : TW;
+    const float* Xw = X + ((size_t)b * N + i0) * D;
+    __syncthreads();  // previous chunk done with xs / Kl / red; zs staged
+    stage_points(Xw, ls, nvalid, D, TW, Dq, ds, cm, xs, xn);
     __syncthreads();
-    if (tid == 0) {
-      float s = 0.f;
-      for (int q = 0; q < NW; ++q) s += red[q];
-      ell_out[b] = s;
+    build_kzx<MB, TW>(zs, xs, zn, xn, M, nvalid, Dq, ds, s2, Kl);
+    __syncthreads();
+    f64x4 acc[G::RT][G::CT];
+    gemm_linv_k<MB>(Linv, Kl, M, acc);
+    // epilogue: partial sum_m A m_m and sum_m A^2 (s_m^2 - 1) over the wave's rows
+#pragma unroll
+    for (int q = 0; q < G::CT; ++q) {
+      float mp = 0.f, vp = 0.f;
+#pragma unroll
+      for (int j = 0; j < G::RT; ++j) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * (wr + G::WR * j) + g + 4 * r;
+          const float a32 = (float)acc[j][q][r];  // A is cast to fp32 (reference)
+          const int rr = row < MP ? row : 0;
+          mp = __builtin_fmaf(a32, row < MP ? vm[rr] : 0.f, mp);
+          vp = __builtin_fmaf(a32 * a32, row < MP ? sm1[rr] : 0.f, vp);
+        }
+      }
+      mp += __shfl_xor(mp, 16, 64);
+      mp += __shfl_xor(mp, 32, 64);
+      vp += __shfl_xor(vp, 16, 64);
+      vp += __shfl_xor(vp, 32, 64);
+      if (g == 0) {
+        redm[wr * TW + 16 * (wc * G::CT + q) + c] = mp;
+        redv[wr * TW + 16 * (wc * G::CT + q) + c] = vp;
+      }
+    }
+    __syncthreads();
+    for (int col = tid; col < nvalid; col += blockDim.x) {
+      float mm = 0.f, vv = 0.f;
+#pragma unroll
+      for (int q = 0; q < G::WR; ++q) {
+        mm += redm[q * TW + col];
+        vv += redv[q * TW + col];
+      }
+      const float* xr = Xw + (size_t)col * D;
+      float lin = 0.f;
+      for (int d = 0; d < D; ++d) lin = __builtin_fmaf(xr[d], w[d], lin);
+      const float mean_i = mm + (lin + b0);
+      float var_i = s2 + jit + vv;
+      if (var_i < 1e-6f) { var_i = 1e-6f; clamped = 1; }  // MVN.variance clamp (fp32)
+      mean_out[(size_t)b * N + i0 + col] = mean_i;
+      var_out[(size_t)b * N + i0 + col] = var_i;
     }
   }
+  if (flags != nullptr && clamped)
+    (void)__hip_atomic_fetch_or(flags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Per-window ELL sum (fixed summation order: run-to-run deterministic).
+__global__ void __launch_bounds__(256)
+gpk_var_ell_kernel(const float* __restrict__ mean, const float* __restrict__ var,
+                   const float* __restrict__ y, const float* __restrict__ hyp, int N,
+                   float* __restrict__ ell) {
+  __shared__ float red[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float noise = hyp[1];
+  const float log_noise = __logf(noise);
+  float acc = 0.f;
+  for (int i = tid; i < N; i += 256) {
+    const size_t o = (size_t)b * N + i;
+    const float dy = y[o] - mean[o];
+    acc += -0.5f * ((dy * dy + var[o]) / noise + log_noise + kLog2PiF);
+  }
+  acc = wave_sum(acc);
+  if ((tid & 63) == 0) red[tid >> 6] = acc;
+  __syncthreads();
+  if (tid == 0) ell[b] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // ---------------------------------------------------------------------------
-// Adjoint of gpk_var_kernel (variational path). Per window and
-// 16-point block it recomputes K_ZX (fp32) and A = L^{-1} K_ZX (fp64 MFMA) exactly
-// as the forward, then with the incoming gmean / gvar (gvar masked where the
-// variance was clamped, MVN.variance):
-//   dA   = gmean_i m_m + 2 gvar_i (s_m^2 - 1) A_mi                 (fp64)
-//   dK   = L^{-T} dA   (fp64 MFMA, triangular k-steps only)
-//   Q    = dK o K_ZX   (the RBF adjoint's only per-entry quantity)
-// and writes dA (fp64), K_ZX and Q (fp32) as (B, M, N) plus per-window partial
-// sums dm = sum_i gmean A, dsm1 = sum_i gvar A^2 and sum_i gvar. The contractions
-// over points / windows (dL^{-1} = sum dA K^T, Q x / Q z) are plain GEMMs done by
-// the caller (rocBLAS through torch), and the M x M K_ZZ adjoint once per call.
+// Adjoint of the forward for the objective sum(gmean * mean) + sum(gvar * var).
+// Per chunk (same tiling as the forward):
+//   K_ZX (LDS), A = L^{-1} K_ZX (fp64 MFMA), var -> clamp mask on gvar,
+//   dA = gmean_i m_m + 2 gvar_i (s_m^2 - 1) A_mi   (fp32: the reference's dA is the
+//        gradient of an fp32 tensor), dA and K_ZX -> workspace for dL^{-1},
+//   dK = L^{-T} dA (fp64 MFMA), Q = dK o K_ZX,
+//   dX_i = (sum_p Q_pi zs_p - xs_i sum_p Q_pi) / l + gmean_i w     (written per point)
+//   partials per workgroup: QX_p = sum_i Q_pi xs_i, q_p = sum_i Q_pi, sum_i gmean A,
+//   sum_i gvar A^2, sum_i r_i xs_i^2, sum Q, sum gvar (reduced by gpk_var_red_kernel).
 // ---------------------------------------------------------------------------
-template <int MB, int DMAX>
-__global__ void __launch_bounds__(256)
-gpk_var_adjoint_kernel(const float* __restrict__ X, const float* __restrict__ Z,
-                       const double* __restrict__ Linv, const float* __restrict__ vmean,
-                       const float* __restrict__ vstd, const float* __restrict__ hyp,
-                       const float* __restrict__ gmean, const float* __restrict__ gvar, int N,
-                       int M, int D, double* __restrict__ dA_out, float* __restrict__ K_out,
-                       float* __restrict__ Q_out, float* __restrict__ part_out) {
+template <int MB, int DQ>
+__global__ void __launch_bounds__(256, 1)
+gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                   const double* __restrict__ Linv, const float* __restrict__ vmean,
+                   const float* __restrict__ vstd, const float* __restrict__ hyp,
+                   const float* __restrict__ gmean, const float* __restrict__ gvar, int N, int M,
+                   int D, int nchunks, long long BN, float* __restrict__ wsdA, float* __restrict__ wsK,
+                   float* __restrict__ wspart, float* __restrict__ dX) {
+  using G = VarGeo<MB>;
+  constexpr int TW = G::TW, MP = G::MP, QST = G::QST;
+  constexpr int Dq = DQ, ds = DQ + 2, NDT = DQ / 16;
   extern __shared__ __attribute__((aligned(16))) float vsm[];
-  float* zt = vsm;               // 16MB x D   centred Z / l (zero-padded rows)
-  float* cm = zt + 16 * MB * D;  // D
-  float* vm = cm + D;            // 16MB  variational mean
-  float* sm1 = vm + 16 * MB;     // 16MB  s^2 - 1
-  float* dm = sm1 + 16 * MB;     // 16MB  partial sum_i gmean A
-  float* ds = dm + 16 * MB;      // 16MB  partial sum_i gvar A^2
-  float* ksm = ds + 16 * MB;     // 4 waves x 16MB x 16  K_ZX of the wave's block
-  float* red = ksm + 4 * 16 * MB * 16;  // 8
-  const int tid = threadIdx.x, T = blockDim.x;
+  float* zs = vsm;                    // MP x ds
+  float* xs = zs + MP * ds;           // TW x ds
+  float* zn = xs + TW * ds;           // MP
+  float* xn = zn + MP;                // TW
+  float* vm = xn + TW;                // MP
+  float* sm1 = vm + MP;               // MP
+  float* cm = sm1 + MP;               // Dq
+  float* gmc = cm + Dq;               // TW
+  float* gvc = gmc + TW;              // TW
+  float* rcol = gvc + TW;             // TW   r_i = sum_p Q_pi
+  float* qacc = rcol + TW;            // MP   sum_i Q_pi (this workgroup)
+  float* dvma = qacc + MP;            // WC x MP
+  float* dsma = dvma + G::WC * MP;    // WC x MP
+  float* rx2 = dsma + G::WC * MP;     // 256  per-thread sum r_i xs_i^2 (thread -> one d)
+  float* redw = rx2 + 256;            // 2 x WR x TW
+  float* Kl = redw + 2 * G::WR * TW;  // MP x TW     (later: Q^T zs partials, WR x TW x Dq)
+  constexpr int KLN = MP * TW > G::WR * TW * DQ ? MP * TW : G::WR * TW * DQ;
+  float* dAl = Kl + KLN;              // MP x TW dA  (later: Q^T, TW x QST)
+  const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
-  const int wave = tid >> 6, NW = T >> 6;
-  const int b = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / G::WC, wc = wave - wr * G::WC;
   const float s2 = hyp[0], jit = hyp[2];
+  const float* w = hyp + 4;
   const float* ls = hyp + 4 + D;
-  const size_t MN = (size_t)M * N;
 
-  for (int e = tid; e < 16 * MB * D; e += T) {
-    const int m = e / D;
-    zt[e] = (m < M) ? Z[e] / ls[e % D] : 0.f;
+  stage_inducing(Z, ls, vmean, vstd, M, D, MP, Dq, ds, zs, zn, cm, vm, sm1);
+  for (int m = tid; m < MP; m += blockDim.x) {
+    qacc[m] = 0.f;
+    for (int q = 0; q < G::WC; ++q) { dvma[q * MP + m] = 0.f; dsma[q * MP + m] = 0.f; }
   }
-  for (int m = tid; m < 16 * MB; m += T) {
-    vm[m] = (m < M) ? vmean[m] : 0.f;
-    const float sd = (m < M) ? vstd[m] : 1.f;
-    sm1[m] = sd * sd - 1.f;
-    dm[m] = 0.f;
-    ds[m] = 0.f;
-  }
-  __syncthreads();
-  for (int d = tid; d < D; d += T) {
-    float s = 0.f;
-    for (int m = 0; m < M; ++m) s += zt[m * D + d];
-    cm[d] = s / (float)M;
-  }
-  __syncthreads();
-  for (int e = tid; e < M * D; e += T) zt[e] -= cm[e % D];
-  __syncthreads();
+  rx2[tid] = 0.f;
+  float sumQ = 0.f, sumgv = 0.f;
+  // persistent f32 accumulators of QX = sum_i Q_pi xs_i: tiles (pt, dt) dealt over the waves
+  constexpr int MAXQT = (MB * NDT + 3) / 4;  // QX tiles (MB x NDT) dealt over 4 waves
+  f32x4 qx[MAXQT];
+#pragma unroll
+  for (int u = 0; u < MAXQT; ++u) qx[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const float* Xb = X + (size_t)b * N * D;
-  float* kw = ksm + wave * 16 * MB * 16;
-  float gvsum = 0.f;
-  const float nhalf_log2e = -0.72134752044448170f;
-  const int NBLK = (N + 15) / 16;
-  for (int nb = wave; nb < NBLK; nb += NW) {
-    const int i = 16 * nb + c;
-    float xr[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d)
-      xr[d] = (d < D && i < N) ? Xb[(size_t)i * D + d] / ls[d] - cm[d] : 0.f;
-    f64x4 acc[MB];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) acc[mb] = f64x4{0.0, 0.0, 0.0, 0.0};
-    for (int s = 0; s < 4 * MB; ++s) {
-      const int p = 4 * s + g;
-      float dist = 0.f;
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        if (d < D) {
-          const float df = zt[p * D + d] - xr[d];
-          dist = __builtin_fmaf(df, df, dist);
-        }
-      }
-      const float kv = (p < M && i < N) ? s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist) : 0.f;
-      kw[p * 16 + c] = kv;
-      if (p < M && i < N) K_out[(size_t)b * MN + (size_t)p * N + i] = kv;
-      const double kd = (double)kv;
-      const int mb0 = (4 * s) >> 4;
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        if (mb >= mb0) {
-          const int m = 16 * mb + c;
-          const double a = (m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
-          acc[mb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, kd, acc[mb], 0, 0, 0);
-        }
-      }
+  const int nch = (N + TW - 1) / TW;
+#pragma unroll 1
+  for (int t = blockIdx.x; t < nchunks; t += gridDim.x) {
+    const int b = t / nch, ch = t - b * nch;
+    const int i0 = ch * TW;
+    const int nvalid = N - i0 < TW ? N - i0 : TW;
+    const size_t col0 = (size_t)b * N + i0;
+    const float* Xw = X + col0 * D;
+    __syncthreads();
+    stage_points(Xw, ls, nvalid, D, TW, Dq, ds, cm, xs, xn);
+    for (int j = tid; j < TW; j += blockDim.x) {
+      gmc[j] = j < nvalid ? gmean[col0 + j] : 0.f;
+      gvc[j] = j < nvalid ? gvar[col0 + j] : 0.f;
     }
-    // acc[mb][r] = A[16 mb + g + 4 r][16 nb + c]; the variance (for the clamp mask)
-    float vpart = 0.f;
+    __syncthreads();
+    build_kzx<MB, TW>(zs, xs, zn, xn, M, nvalid, Dq, ds, s2, Kl);
+    __syncthreads();
+    f64x4 acc[G::RT][G::CT];
+    gemm_linv_k<MB>(Linv, Kl, M, acc);
+    // variance -> clamp mask (no gradient below the clamp)
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
+    for (int q = 0; q < G::CT; ++q) {
+      float vp = 0.f;
+#pragma unroll
+      for (int j = 0; j < G::RT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * (wr + G::WR * j) + g + 4 * r;
+          const float a32 = (float)acc[j][q][r];
+          vp = __builtin_fmaf(a32 * a32, row < MP ? sm1[row] : 0.f, vp);
+        }
+      vp += __shfl_xor(vp, 16, 64);
+      vp += __shfl_xor(vp, 32, 64);
+      if (g == 0) redw[wr * TW + 16 * (wc * G::CT + q) + c] = vp;
+    }
+    __syncthreads();
+    for (int col = tid; col < TW; col += blockDim.x) {
+      float vv = 0.f;
+      for (int q = 0; q < G::WR; ++q) vv += redw[q * TW + col];
+      if (s2 + jit + vv < 1e-6f) gvc[col] = 0.f;  // clamp_min(1e-6): gradient masked
+      sumgv += gvc[col];
+    }
+    __syncthreads();
+    // dA (fp32) -> LDS + workspace; partial sums for dvmean / dvstd
+#pragma unroll
+    for (int j = 0; j < G::RT; ++j) {
+      const int rt = wr + G::WR * j;
+      if (rt >= MB) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float a32 = (float)acc[mb][r];
-        vpart = __builtin_fmaf(a32 * a32, sm1[16 * mb + g + 4 * r], vpart);
-      }
-    }
-    vpart += __shfl_xor(vpart, 16, 64);
-    vpart += __shfl_xor(vpart, 32, 64);
-    const float var_i = s2 + jit + vpart;
-    const float gm = (i < N) ? gmean[(size_t)b * N + i] : 0.f;
-    float gv = (i < N) ? gvar[(size_t)b * N + i] : 0.f;
-    if (var_i < 1e-6f) gv = 0.f;  // clamp_min(1e-6): no gradient below the clamp
-    if (g == 0) gvsum += gv;
-    // dA (fp64, C layout of A), partial sums for dm / ds, dA out
+        const int row = 16 * rt + g + 4 * r;
+        float pm = 0.f, ps = 0.f;
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
+        for (int q = 0; q < G::CT; ++q) {
+          const int col = 16 * (wc * G::CT + q) + c;
+          const float a32 = (float)acc[j][q][r];
+          const float gm = gmc[col], gv = gvc[col];
+          const float da = gm * vm[row] + 2.f * gv * sm1[row] * a32;
+          dAl[row * TW + col] = da;
+          if (row < M && col < nvalid) wsdA[(size_t)row * BN + col0 + col] = da;
+          pm = __builtin_fmaf(gm, a32, pm);
+          ps = __builtin_fmaf(gv, a32 * a32, ps);
+        }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * mb + g + 4 * r;
-        const double a = acc[mb][r];
-        const float a32 = (float)a;
-        const double da = (double)gm * (double)vm[m] + 2.0 * (double)gv * (double)sm1[m] * (double)a32;
-        acc[mb][r] = da;
-        float pm = gm * a32, ps = gv * a32 * a32;
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {  // sum over the 16 points of the block
+        for (int off = 1; off < 16; off <<= 1) {
           pm += __shfl_xor(pm, off, 64);
           ps += __shfl_xor(ps, off, 64);
         }
-        if (c == 0 && m < M) {
-          (void)__hip_atomic_fetch_add(&dm[m], pm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          (void)__hip_atomic_fetch_add(&ds[m], ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (c == 0) {
+          dvma[wc * MP + row] += pm;
+          dsma[wc * MP + row] += ps;
         }
-        if (m < M && i < N) dA_out[(size_t)b * MN + (size_t)m * N + i] = da;
       }
     }
-    // dK = L^{-T} dA: output block pb, k-steps s >= 4 pb (L^{-1}[m][p] = 0 for m < p);
-    // the B operand of k-step s is dA[4s + g][c] = acc[s / 4][s % 4]
+    // K_ZX -> workspace (row-major M x BN, coalesced along points)
+    for (int e = tid; e < M * TW; e += blockDim.x) {
+      const int p = e / TW, col = e - p * TW;
+      if (col < nvalid) wsK[(size_t)p * BN + col0 + col] = Kl[p * TW + col];
+    }
+    __syncthreads();
+    // dK = L^{-T} dA (fp64 MFMA): output rows p = the wave's row tiles, k = m >= p
+    {
+      int first = MB, last = 0;
 #pragma unroll
-    for (int pb = 0; pb < MB; ++pb) {
-      f64x4 dk = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s = 4 * pb; s < 4 * MB; ++s) {
-        const int m = 4 * s + g, p = 16 * pb + c;
-        const double a = (m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
-        dk = __builtin_amdgcn_mfma_f64_16x16x4f64(a, acc[s >> 2][s & 3], dk, 0, 0, 0);
+      for (int j = 0; j < G::RT; ++j) {
+        const int rt = wr + G::WR * j;
+        if (rt < MB) { first = rt < first ? rt : first; last = rt; }
       }
+#pragma unroll
+      for (int j = 0; j < G::RT; ++j)
+#pragma unroll
+        for (int q = 0; q < G::CT; ++q) acc[j][q] = f64x4{0.0, 0.0, 0.0, 0.0};
+      (void)last;
+
+      for (int s = 4 * first; s < 4 * MB; ++s) {
+        const int m = 4 * s + g;
+        double bq[G::CT];
+#pragma unroll
+        for (int q = 0; q < G::CT; ++q) bq[q] = (double)dAl[m * TW + 16 * (wc * G::CT + q) + c];
+#pragma unroll
+        for (int j = 0; j < G::RT; ++j) {
+          const int rt = wr + G::WR * j;
+          if (rt < MB && s >= 4 * rt) {
+            const int p = 16 * rt + c;
+            const double a = (m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
+#pragma unroll
+            for (int q = 0; q < G::CT; ++q) acc[j][q] = mfma64(a, bq[q], acc[j][q]);
+          }
+        }
+      }
+    }
+    __syncthreads();  // every wave is done reading dAl
+    // Q = dK o K_ZX: Q^T -> LDS (over dAl), sum Q, r_i partials, and Q^T zs on f32 MFMA
+    f32x4 xz[G::CT][NDT];
+#pragma unroll
+    for (int q = 0; q < G::CT; ++q)
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) xz[q][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float rp[G::CT] = {};
+#pragma unroll
+    for (int j = 0; j < G::RT; ++j) {
+      const int rt = wr + G::WR * j;
+      if (rt >= MB) continue;
+#pragma unroll
+      for (int q = 0; q < G::CT; ++q) {
+        const int col = 16 * (wc * G::CT + q) + c;
+        float qv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * rt + g + 4 * r;
+          qv[r] = (float)acc[j][q][r] * Kl[row * TW + col];
+          dAl[col * QST + row] = qv[r];
+          sumQ += qv[r];
+          rp[q] += qv[r];
+        }
+        // (Q^T zs)[col][d] += sum over this tile's rows (k-order g + 4r)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            xz[q][dt] = mfma32(qv[r], zs[(16 * rt + g + 4 * r) * ds + 16 * dt + c], xz[q][dt]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < G::CT; ++q) {
+      float v = rp[q];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) redw[wr * TW + 16 * (wc * G::CT + q) + c] = v;
+    }
+    __syncthreads();  // Q^T complete, K_ZX no longer needed, r partials in redw
+    // Q^T zs partials -> LDS (over Kl): [wr][col][d]; xz[q][dt][r] = (Q^T zs)[16ct + 4g + r][16dt + c]
+#pragma unroll
+    for (int q = 0; q < G::CT; ++q)
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int col = 16 * (wc * G::CT + q) + 4 * g + r;
+          Kl[(wr * TW + col) * Dq + 16 * dt + c] = xz[q][dt][r];
+        }
+      }
+    for (int col = tid; col < TW; col += blockDim.x) {
+      float v = 0.f;
+      for (int q = 0; q < G::WR; ++q) v += redw[q * TW + col];
+      rcol[col] = v;
+    }
+    // QX += sum_i Q_pi xs_i (f32 MFMA, A = Q from Q^T, B = xs); tiles dealt over the waves
+#pragma unroll
+    for (int u = 0; u < MAXQT; ++u) {
+      const int tq = wave + 4 * u;
+      if (tq < MB * NDT) {
+        const int pt = tq / NDT, dt = tq - pt * NDT;
+        for (int k = 0; k < TW / 4; ++k)
+          qx[u] = mfma32(dAl[(4 * k + g) * QST + 16 * pt + c], xs[(4 * k + g) * ds + 16 * dt + c], qx[u]);
+      }
+    }
+    for (int p = tid; p < MP; p += blockDim.x) {
+      float v = 0.f;
+      for (int i = 0; i < TW; ++i) v += dAl[i * QST + p];
+      qacc[p] += v;
+    }
+    __syncthreads();  // Q^T zs partials and r complete
+    // dX per point; sum_i r_i xs_i^2 per d (thread tid always sees d = tid % Dq)
+    for (int e = tid; e < TW * Dq; e += blockDim.x) {
+      const int col = e / Dq, d = e - col * Dq;
+      float v = 0.f;
+      for (int q = 0; q < G::WR; ++q) v += Kl[(q * TW + col) * Dq + d];
+      const float xv = xs[col * ds + d];
+      const float r = rcol[col];
+      if (col < nvalid && d < D) {
+        dX[(col0 + col) * D + d] = (v - xv * r) / ls[d] + gmc[col] * w[d];
+        rx2[tid] += r * xv * xv;
+      }
+    }
+  }
+  __syncthreads();
+  // per-workgroup partials: [QX (M x D) | q (M) | dvm (M) | dsm (M) | rx2 (D) | sumQ | sumgv]
+  const int P = M * D + 3 * M + D + 2;
+  float* po = wspart + (size_t)blockIdx.x * P;
+#pragma unroll
+  for (int u = 0; u < MAXQT; ++u) {
+    const int tq = wave + 4 * u;
+    if (tq < MB * NDT) {
+      const int pt = tq / NDT, dt = tq - pt * NDT;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int p = 16 * pb + g + 4 * r;
-        if (p < M && i < N) Q_out[(size_t)b * MN + (size_t)p * N + i] = (float)dk[r] * kw[p * 16 + c];
+        const int p = 16 * pt + 4 * g + r, d = 16 * dt + c;
+        if (p < M && d < D) po[p * D + d] = qx[u][r];
       }
     }
   }
-  gvsum = wave_sum(gvsum);
-  if (lane == 0) red[wave] = gvsum;
+  for (int m = tid; m < M; m += blockDim.x) {
+    float a = 0.f, s = 0.f;
+    for (int q = 0; q < G::WC; ++q) { a += dvma[q * MP + m]; s += dsma[q * MP + m]; }
+    po[M * D + m] = qacc[m];
+    po[M * D + M + m] = a;
+    po[M * D + 2 * M + m] = s;
+  }
+  // sum r xs^2 over the threads that accumulated the same d (d = tid % Dq)
+  for (int d = tid; d < D; d += blockDim.x) {
+    float v = 0.f;
+    for (int t = d; t < 256; t += Dq) v += rx2[t];
+    po[M * D + 3 * M + d] = v;
+  }
+  sumQ = wave_sum(sumQ);
+  if (lane == 0) redw[wave] = sumQ;
+  __syncthreads();  // rx2 read, sumQ partials out
+  rx2[tid] = sumgv;  // accumulated by the column threads
   __syncthreads();
-  // per-window partials: [dm (M), ds (M), sum gvar]
-  float* po = part_out + (size_t)b * (2 * M + 1);
-  for (int m = tid; m < M; m += T) {
-    po[m] = dm[m];
-    po[M + m] = ds[m];
-  }
   if (tid == 0) {
-    float s = 0.f;
-    for (int q = 0; q < NW; ++q) s += red[q];
-    po[2 * M] = s;
+    float v = 0.f;
+    for (int t = 0; t < 256; ++t) v += rx2[t];
+    po[M * D + 3 * M + D] = (redw[0] + redw[1]) + (redw[2] + redw[3]);
+    po[M * D + 3 * M + D + 1] = v;
   }
 }
 
-template <int MB, int DMAX>
+// ---------------------------------------------------------------------------
+// dL^{-1} = sum_cols dA[:, col] K[:, col]^T (lower part): split-K fp64-MFMA GEMM.
+// Workgroup = one 64 x 64 lower output tile (ti >= tj) x one split of the columns;
+// 4 waves, each a 32 x 32 quadrant (2 x 2 MFMA tiles). fp32 operands are exact in fp64.
+// Partials -> ws (split, tile, 64 x 64) doubles.
+// ---------------------------------------------------------------------------
+constexpr int DLKC = 32;   // columns staged per step
+constexpr int DLST = 34;   // LDS row stride (floats): 2c + g spreads the MFMA operand reads
+
+__global__ void __launch_bounds__(256)
+gpk_dlinv_kernel(const float* __restrict__ dA, const float* __restrict__ Kz, int M, long long BN,
+                 int ntiles, long long cols_per_split, double* __restrict__ part) {
+  __shared__ float sa[64 * DLST];
+  __shared__ float sb[64 * DLST];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int wave = tid >> 6, qr = wave >> 1, qc = wave & 1;
+  const int tile = blockIdx.x % ntiles, split = blockIdx.x / ntiles;
+  int ti = 0;
+  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
+  const int tj = tile - ti * (ti + 1) / 2;
+  const int m0 = 64 * ti, p0 = 64 * tj;
+  const long long c0 = (long long)split * cols_per_split;
+  long long c1 = c0 + cols_per_split;
+  c1 = c1 < BN ? c1 : BN;
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[u][v] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (long long cb = c0; cb < c1; cb += DLKC) {
+    __syncthreads();
+    for (int e = tid; e < 64 * DLKC; e += 256) {
+      const int rr = e / DLKC, kk = e - rr * DLKC;
+      const long long col = cb + kk;
+      const bool okc = col < c1;
+      sa[rr * DLST + kk] = (m0 + rr < M && okc) ? dA[(size_t)(m0 + rr) * BN + col] : 0.f;
+      sb[rr * DLST + kk] = (p0 + rr < M && okc) ? Kz[(size_t)(p0 + rr) * BN + col] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < DLKC / 4; ++k) {
+      double a[2], bb[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        a[u] = (double)sa[(32 * qr + 16 * u + c) * DLST + 4 * k + g];
+        bb[u] = (double)sb[(32 * qc + 16 * u + c) * DLST + 4 * k + g];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) acc[u][v] = mfma64(a[u], bb[v], acc[u][v]);
+    }
+  }
+  double* po = part + ((size_t)split * ntiles + tile) * 4096;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 32 * qr + 16 * u + g + 4 * r, col = 32 * qc + 16 * v + c;
+        po[row * 64 + col] = acc[u][v][r];
+      }
+}
+
+// Fixed-order reductions: (a) the per-workgroup adjoint partials (fp64 sums),
+// (b) the split-K dL^{-1} partials -> dLinv (M x M, upper zero).
+__global__ void __launch_bounds__(256)
+gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __restrict__ tot,
+                   const double* __restrict__ dlpart, int nsplit, int ntiles, int M,
+                   double* __restrict__ dLinv) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e < P) {
+    double s = 0.0;
+    for (int q = 0; q < nwg; ++q) s += (double)wspart[(size_t)q * P + e];
+    tot[e] = s;
+    return;
+  }
+  const long long f = e - P;
+  if (f >= (long long)M * M) return;
+  const int m = (int)(f / M), p = (int)(f - (long long)m * M);
+  double s = 0.0;
+  if (p <= m) {
+    const int ti = m >> 6, tj = p >> 6;
+    const int tile = ti * (ti + 1) / 2 + tj;
+    const int o = (m & 63) * 64 + (p & 63);
+    for (int q = 0; q < nsplit; ++q) s += dlpart[((size_t)q * ntiles + tile) * 4096 + o];
+  }
+  dLinv[f] = s;
+}
+
+// Outputs from the reduced totals (one workgroup):
+//   dZ_p = (QX_p - zs_p q_p) / l;   dl_d = (sum_p q_p zs_pd^2 - 2 sum_p zs_pd QX_pd + sum_i r_i xs_id^2) / l_d
+//   ds2 = sum Q / s2 + sum gvar;    dvmean = sum gmean A;   dvstd = 2 s sum gvar A^2
+// dpar = [dvmean (M) | dvstd (M) | ds2 | dl (D)]
+__global__ void __launch_bounds__(256)
+gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
+                   const float* __restrict__ hyp, const double* __restrict__ tot, int M, int D,
+                   float* __restrict__ dZ, float* __restrict__ dpar) {
+  __shared__ double cmd[64];
+  __shared__ double dld[64];
+  const int tid = threadIdx.x;
+  const float s2 = hyp[0];
+  const float* ls = hyp + 4 + D;
+  for (int d = tid; d < D; d += 256) {
+    float s = 0.f;  // the same fp32 sum as stage_inducing: the identical centre
+    for (int m = 0; m < M; ++m) s += Z[m * D + d] / ls[d];
+    cmd[d] = (double)(s / (float)M);
+  }
+  __syncthreads();
+  const double* QX = tot;
+  const double* q = tot + (size_t)M * D;
+  const double* dvm = q + M;
+  const double* dsm = dvm + M;
+  const double* rx2 = dsm + M;
+  const double sumQ = rx2[D], sumgv = rx2[D + 1];
+  for (int e = tid; e < M * D; e += 256) {
+    const int p = e / D, d = e - p * D;
+    const double zsv = (double)(Z[p * D + d] / ls[d] - (float)cmd[d]);
+    dZ[e] = (float)((QX[e] - zsv * q[p]) / (double)ls[d]);
+  }
+  for (int d = tid; d < D; d += 256) {
+    double acc = rx2[d];
+    for (int p = 0; p < M; ++p) {
+      const double zsv = (double)(Z[p * D + d] / ls[d] - (float)cmd[d]);
+      acc += q[p] * zsv * zsv - 2.0 * zsv * QX[(size_t)p * D + d];
+    }
+    dld[d] = acc / (double)ls[d];
+  }
+  __syncthreads();
+  for (int m = tid; m < M; m += 256) {
+    dpar[m] = (float)dvm[m];
+    dpar[M + m] = (float)(2.0 * (double)vstd[m] * dsm[m]);
+  }
+  if (tid == 0) dpar[2 * M] = (float)(sumQ / (double)s2 + sumgv);
+  for (int d = tid; d < D; d += 256) dpar[2 * M + 1 + d] = (float)dld[d];
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <int MB>
+size_t var_fwd_lds(int D) {
+  using G = VarGeo<MB>;
+  const int Dq = dq_of(D), ds = Dq + 2;
+  return (size_t)(G::MP * ds + G::TW * ds + G::MP + G::TW + 2 * G::MP + Dq + G::MP * G::TW +
+                  2 * G::WR * G::TW) * sizeof(float);
+}
+
+template <int MB, int DQ>
+size_t var_adj_lds() {
+  using G = VarGeo<MB>;
+  const int Dq = DQ, ds = Dq + 2;
+  const size_t kl = (size_t)G::MP * G::TW > (size_t)G::WR * G::TW * Dq ? (size_t)G::MP * G::TW
+                                                                       : (size_t)G::WR * G::TW * Dq;
+  const size_t da = (size_t)G::MP * G::TW > (size_t)G::TW * G::QST ? (size_t)G::MP * G::TW
+                                                                   : (size_t)G::TW * G::QST;
+  return ((size_t)G::MP * ds + G::TW * ds + G::MP + G::TW + 2 * G::MP + Dq + 3 * G::TW + G::MP +
+          2 * G::WC * G::MP + 256 + 2 * G::WR * G::TW + kl + da) * sizeof(float);
+}
+
+// hipFuncSetAttribute once per kernel instantiation (thread-safe; the C ABI has no
+// mutable global state beyond this idempotent one-time setup).
+template <auto Kernel>
+void set_lds_once() {
+  static std::once_flag once;  // one flag per kernel instantiation
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute((const void*)Kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  });
+}
+
+// Workgroups for a chunk list: every chunk once, at most ~4 per CU so the inducing-point
+// staging of a workgroup is amortised over several chunks.
+int chunk_grid(long long nchunks, int per_cu) {
+  const long long cap = 256LL * per_cu;
+  return (int)(nchunks < cap ? nchunks : cap);
+}
+
+template <int MB>
+int launch_var_fwd(const GpkVarArgs& a, int* flags, hipStream_t stream) {
+  using G = VarGeo<MB>;
+  const size_t lds = var_fwd_lds<MB>(a.D);
+  if (lds > 160 * 1024) return -11;
+  set_lds_once<gpk_var_fwd_kernel<MB>>();
+  const long long nch = (long long)a.B * ((a.N + G::TW - 1) / G::TW);
+  if (nch > 0x7fffffffLL) return -8;
+  hipLaunchKernelGGL((gpk_var_fwd_kernel<MB>), dim3(chunk_grid(nch, 4)), dim3(256), lds, stream,
+                     a.X, a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.N, a.M, a.D, (int)nch, a.mean,
+                     a.var, flags);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  if (a.ell != nullptr) {
+    hipLaunchKernelGGL(gpk_var_ell_kernel, dim3(a.B), dim3(256), 0, stream, a.mean, a.var, a.y,
+                       a.hyp, a.N, a.ell);
+    e = hipGetLastError();
+  }
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+struct AdjPlan {
+  int nchunks, nwg, P, ntiles, nsplit;
+  long long BN, cols_per_split;
+  size_t off_dA, off_K, off_part, off_tot, off_dl, total;  // byte offsets
+};
+
+template <int MB>
+AdjPlan adj_plan(int B, int N, int M, int D) {
+  using G = VarGeo<MB>;
+  AdjPlan p{};
+  p.nchunks = B * ((N + G::TW - 1) / G::TW);
+  p.nwg = chunk_grid(p.nchunks, 2);
+  p.P = M * D + 3 * M + D + 2;
+  p.BN = (long long)B * N;
+  const int MT = (M + 63) / 64;
+  p.ntiles = MT * (MT + 1) / 2;
+  long long want = 512 / p.ntiles;
+  if (want < 1) want = 1;
+  long long cps = (p.BN + want - 1) / want;
+  cps = ((cps + DLKC - 1) / DLKC) * DLKC;
+  if (cps < DLKC) cps = DLKC;
+  p.cols_per_split = cps;
+  p.nsplit = (int)((p.BN + cps - 1) / cps);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t o = 0;
+  p.off_dA = o; o = al(o + (size_t)M * p.BN * sizeof(float));
+  p.off_K = o; o = al(o + (size_t)M * p.BN * sizeof(float));
+  p.off_part = o; o = al(o + (size_t)p.nwg * p.P * sizeof(float));
+  p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
+  p.off_dl = o; o = al(o + (size_t)p.nsplit * p.ntiles * 4096 * sizeof(double));
+  p.total = o;
+  return p;
+}
+
+template <int MB, int DQ>
 int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
-  const size_t lds = (size_t)(16 * MB * a.D + a.D + 4 * 16 * MB + 4 * 16 * MB * 16 + 8) * sizeof(float);
-  if (lds > 160 * 1024) return -10;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)gpk_var_adjoint_kernel<MB, DMAX>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((gpk_var_adjoint_kernel<MB, DMAX>), dim3(a.B), dim3(256), lds, stream, a.X,
-                     a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.N, a.M, a.D, a.dA,
-                     a.K, a.Q, a.part);
-  const hipError_t e = hipGetLastError();
+  const size_t lds = var_adj_lds<MB, DQ>();
+  if (lds > 160 * 1024) return -12;
+  set_lds_once<gpk_var_adj_kernel<MB, DQ>>();
+  const AdjPlan p = adj_plan<MB>(a.B, a.N, a.M, a.D);
+  char* ws = (char*)a.ws;
+  float* wsdA = (float*)(ws + p.off_dA);
+  float* wsK = (float*)(ws + p.off_K);
+  float* wspart = (float*)(ws + p.off_part);
+  double* tot = (double*)(ws + p.off_tot);
+  double* dl = (double*)(ws + p.off_dl);
+  hipLaunchKernelGGL((gpk_var_adj_kernel<MB, DQ>), dim3(p.nwg), dim3(256), lds, stream, a.X, a.Z,
+                     a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.N, a.M, a.D, p.nchunks,
+                     p.BN, wsdA, wsK, wspart, a.dX);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gpk_dlinv_kernel, dim3(p.ntiles * p.nsplit), dim3(256), 0, stream, wsdA, wsK,
+                     a.M, p.BN, p.ntiles, p.cols_per_split, dl);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const long long nred = (long long)p.P + (long long)a.M * a.M;
+  hipLaunchKernelGGL(gpk_var_red_kernel, dim3((unsigned)((nred + 255) / 256)), dim3(256), 0, stream,
+                     wspart, p.nwg, p.P, tot, dl, p.nsplit, p.ntiles, a.M, a.dLinv);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(1), dim3(256), 0, stream, a.Z, a.vstd, a.hyp, tot,
+                     a.M, a.D, a.dZ, a.dpar);
+  e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
 
-template <int DMAX>
-int launch_var_adj_d(const GpkVarAdjArgs& a, hipStream_t stream) {
-  switch ((a.M + 15) / 16) {
-#define GPK_VCASE(mb) case mb: return launch_var_adj<mb, DMAX>(a, stream);
-    GPK_VCASE(1) GPK_VCASE(2) GPK_VCASE(3) GPK_VCASE(4) GPK_VCASE(5) GPK_VCASE(6)
-    GPK_VCASE(7) GPK_VCASE(8) GPK_VCASE(9) GPK_VCASE(10) GPK_VCASE(11) GPK_VCASE(12)
-    GPK_VCASE(13) GPK_VCASE(14) GPK_VCASE(15) GPK_VCASE(16)
-#undef GPK_VCASE
-    default: return -10;
+// Instantiated row-block counts; M is padded up to the next one (zero rows).
+#define GPK_MB_SWITCH(MBV, CALL)                                                   \
+  {                                                                                \
+    const int mbv_ = (MBV);                                                        \
+    if (mbv_ <= 1) { CALL(1) } else if (mbv_ <= 2) { CALL(2) }                     \
+    else if (mbv_ <= 3) { CALL(3) } else if (mbv_ <= 4) { CALL(4) }                \
+    else if (mbv_ <= 6) { CALL(6) } else if (mbv_ <= 8) { CALL(8) }                \
+    else if (mbv_ <= 12) { CALL(12) } else if (mbv_ <= 16) { CALL(16) }            \
   }
-}
-
-template <int MB, int DMAX>
-int launch_var(const GpkVarArgs& a, hipStream_t stream) {
-  const size_t lds = (size_t)(16 * MB * a.D + a.D + 2 * 16 * MB + 8) * sizeof(float);
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)gpk_var_kernel<MB, DMAX>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((gpk_var_kernel<MB, DMAX>), dim3(a.B), dim3(256), lds, stream, a.X, a.Z,
-                     a.Linv, a.vmean, a.vstd, a.hyp, a.y, a.N, a.M, a.D, a.mean, a.var, a.ell);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : (int)e;
-}
-
-template <int DMAX>
-int launch_var_d(const GpkVarArgs& a, hipStream_t stream) {
-  switch ((a.M + 15) / 16) {
-#define GPK_VCASE(mb) case mb: return launch_var<mb, DMAX>(a, stream);
-    GPK_VCASE(1) GPK_VCASE(2) GPK_VCASE(3) GPK_VCASE(4) GPK_VCASE(5) GPK_VCASE(6)
-    GPK_VCASE(7) GPK_VCASE(8) GPK_VCASE(9) GPK_VCASE(10) GPK_VCASE(11) GPK_VCASE(12)
-    GPK_VCASE(13) GPK_VCASE(14) GPK_VCASE(15) GPK_VCASE(16)
-#undef GPK_VCASE
-    default: return -9;
-  }
-}
 
 }  // namespace
 
 int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
-  const size_t lds = (size_t)(a.M * a.D + a.M + a.D + 16) * sizeof(float) + 64 + 4 * a.M * sizeof(double) + 64;
+  const int Mp = (a.M + 3) & ~3;
+  const size_t lds = (size_t)(KR * Mp + KR * 2 * KR + KR * KR) * sizeof(double) +
+                     (size_t)(a.M * a.D + a.M + a.D) * sizeof(float);
   if (lds > 160 * 1024) return -4;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)gpk_kzz_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_lds_once<gpk_kzz_kernel>();
   hipLaunchKernelGGL(gpk_kzz_kernel, dim3(1), dim3(1024), lds, stream, a.Z, a.hyp, a.M, a.D,
                      a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.Linv, a.info);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
 
-int gpk_launch_var_adjoint(const GpkVarAdjArgs& a, hipStream_t stream) {
-  if (a.D <= 16) return launch_var_adj_d<16>(a, stream);
-  if (a.D <= 32) return launch_var_adj_d<32>(a, stream);
-  if (a.D <= 64) return launch_var_adj_d<64>(a, stream);
-  return -11;
+int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream) {
+  if (flags != nullptr) {
+    const hipError_t e = hipMemsetAsync(flags, 0, sizeof(int), stream);
+    if (e != hipSuccess) return (int)e;
+  }
+#define GPK_CALL_FWD(mb) return launch_var_fwd<mb>(a, flags, stream);
+  GPK_MB_SWITCH((a.M + 15) / 16, GPK_CALL_FWD)
+#undef GPK_CALL_FWD
+  return -10;
 }
 
-int gpk_launch_var(const GpkVarArgs& a, hipStream_t stream) {
-  if (a.D <= 16) return launch_var_d<16>(a, stream);
-  if (a.D <= 32) return launch_var_d<32>(a, stream);
-  if (a.D <= 64) return launch_var_d<64>(a, stream);
-  return -8;
+size_t gpk_var_adjoint_ws_bytes(int B, int N, int M, int D) {
+#define GPK_CALL_WS(mb) return adj_plan<mb>(B, N, M, D).total;
+  GPK_MB_SWITCH((M + 15) / 16, GPK_CALL_WS)
+#undef GPK_CALL_WS
+  return 0;
+}
+
+int gpk_launch_var_adjoint(const GpkVarAdjArgs& a, hipStream_t stream) {
+#define GPK_CALL_ADJ(mb)                                         \
+  if (a.D <= 32) return launch_var_adj<mb, 32>(a, stream);       \
+  return launch_var_adj<mb, 64>(a, stream);
+  GPK_MB_SWITCH((a.M + 15) / 16, GPK_CALL_ADJ)
+#undef GPK_CALL_ADJ
+  return -11;
 }

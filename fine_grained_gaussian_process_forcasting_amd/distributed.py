@@ -49,3 +49,53 @@ def global_mean_objective(per_window: torch.Tensor, total_windows: int, group=No
     if work is not None:
         work.wait()
     return t / float(total_windows)
+
+
+def allreduce_shared_grads(params, group=None, scale: float = 1.0) -> Optional[torch.Tensor]:
+    """Sum the gradients of the SHARED GP parameters over ranks with ONE collective
+    (SURVEY.md §8e): every rank back-propagated its own shard of windows, so the shared
+    hyper-parameters / inducing points / q(u) hold partial gradients. They are packed
+    into one flat fp32 buffer (variational: M*D + 2M + D + 4 floats, ~9 KB at M=64,
+    D=32 -- latency-bound, one xGMI hop), SUM-all-reduced, scaled and written back.
+    Parameters without a gradient contribute zeros. Returns the flat buffer."""
+    params = [p for p in params if p is not None]
+    if not params:
+        return None
+    dev = params[0].device
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1).float().to(dev)
+                      for p in params])
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    if scale != 1.0:
+        flat.mul_(scale)
+    o = 0
+    for p in params:
+        n = p.numel()
+        g = flat[o:o + n].view_as(p).to(p.dtype)
+        if p.grad is None:
+            p.grad = g.clone()
+        else:
+            p.grad.copy_(g)
+        o += n
+    return flat
+
+
+class ObjectiveAccumulator:
+    """Per-step objective partials kept on the device and reduced across ranks with ONE
+    all-reduce for many steps (the per-step value is only logged): no collective sits
+    on the critical path of a step, which matters at 64 windows per GPU."""
+
+    def __init__(self, steps: int, device, group=None):
+        self.buf = torch.zeros(max(1, steps), dtype=torch.float64, device=device)
+        self.n = 0
+        self.group = group
+
+    def add(self, partial: torch.Tensor) -> None:
+        self.buf[self.n].copy_(partial.detach().reshape(()).to(torch.float64))
+        self.n += 1
+
+    def reduce(self, async_op: bool = False):
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            work = dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            return self.buf[:self.n], work
+        return self.buf[:self.n], None

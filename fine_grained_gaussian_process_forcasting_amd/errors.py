@@ -9,6 +9,12 @@ class NanError(RuntimeError):
     pass
 
 
+class GpkInternalError(RuntimeError):
+    """A kernel reported an internal failure (e.g. a bounded LDS spin-wait timed out,
+    info = 1 << 20): a bug or a hardware fault, never a property of the inputs."""
+    pass
+
+
 class NumericalWarning(RuntimeWarning):
     """Mirror of gpytorch.utils.warnings.NumericalWarning."""
     pass

@@ -42,32 +42,41 @@ LOG_2PI = math.log(2.0 * math.pi)
 # settings (upstream gpytorch/settings.py)
 # ---------------------------------------------------------------------------
 class _Setting:
+    """One process-wide value, like GPyTorch's ``_value_context``: entering the context
+    stores the value once for the whole process (``_global_value`` is a class
+    attribute there), so a value set on the main thread (train.py:20) is what the
+    Optuna worker threads (train.py:86, n_jobs=4) read. Exit restores the value that
+    was current on entry."""
+
+    _lock = threading.Lock()
+    _UNSET = object()
+
     def __init__(self, default):
         self._default = default
-        self._local = threading.local()
+        self._value = self._UNSET
 
     def value(self, dtype=None):
-        v = getattr(self._local, "stack", None)
-        if v:
-            return v[-1]
+        v = self._value
+        if v is not self._UNSET:
+            return v
         if isinstance(self._default, dict):
             return self._default.get(dtype, self._default.get(None))
         return self._default
 
     @contextlib.contextmanager
     def __call__(self, value):
-        stack = getattr(self._local, "stack", None)
-        if stack is None:
-            stack = self._local.stack = []
-        stack.append(value)
+        with self._lock:
+            prev = self._value
+            self._value = value
         try:
             yield
         finally:
-            stack.pop()
+            with self._lock:
+                self._value = prev
 
 
 class settings:
-    """The gpytorch.settings used on this path (thread-local like GPyTorch's)."""
+    """The gpytorch.settings used on this path (process-global like GPyTorch's)."""
     num_likelihood_samples = _Setting(10)          # train.py:20 sets 1
     cholesky_jitter = _Setting({torch.float32: 1e-6, torch.float64: 1e-8, None: 1e-6})
     cholesky_max_tries = _Setting(3)
@@ -169,11 +178,12 @@ class MultivariateNormal:
     """
 
     def __init__(self, mean: torch.Tensor, variance: Optional[torch.Tensor] = None,
-                 exact=None, added_noise=None):
+                 exact=None, added_noise=None, clamp_flag: Optional[torch.Tensor] = None):
         self._mean = mean
         self._variance = variance
         self._exact = exact                # (X, kernel hyper) for exact-GP priors
         self._added_noise = added_noise    # likelihood noise folded in by GaussianLikelihood
+        self._clamp_flag = clamp_flag      # (1,) int32 from gpk_variational_f32: clamp fired
 
     @property
     def mean(self):
@@ -199,6 +209,14 @@ class MultivariateNormal:
         if self._added_noise is not None:
             var = var + self._added_noise
         min_var = settings.min_variance.value(var.dtype)
+        if self._clamp_flag is not None and self._added_noise is None:
+            # the kernel already clamped (fp32 min_variance); it tells us whether it did:
+            # one host read of the flag, as GPyTorch's own .lt(min_var).any() sync
+            if int(self._clamp_flag.item()) & 1:
+                warnings.warn(f"Negative variance values detected. This is likely due to numerical "
+                              f"instabilities. Rounding negative variances up to {min_var}.",
+                              NumericalWarning)
+            return var
         if bool((var < min_var).any()):
             warnings.warn(f"Negative variance values detected. This is likely due to numerical "
                           f"instabilities. Rounding negative variances up to {min_var}.",
@@ -214,11 +232,11 @@ class MultivariateNormal:
         batch_size = torch.Size(batch_size)
         mean = self._mean.expand(*batch_size, *self.event_shape)
         var = self._variance.expand(*batch_size, *self.event_shape) if self._variance is not None else None
-        return MultivariateNormal(mean, var, self._exact, self._added_noise)
+        return MultivariateNormal(mean, var, self._exact, self._added_noise, self._clamp_flag)
 
     def add_noise(self, noise):
         total = noise if self._added_noise is None else self._added_noise + noise
-        return MultivariateNormal(self._mean, self._variance, self._exact, total)
+        return MultivariateNormal(self._mean, self._variance, self._exact, total, self._clamp_flag)
 
     def log_prob(self, value: torch.Tensor) -> torch.Tensor:
         """Exact-GP marginal log density (fused RBF + Cholesky + solve + logdet kernel)."""
@@ -294,8 +312,9 @@ class VariationalStrategy(nn.Module):
     """Whitened VariationalStrategy for one DeepGP layer (output_dims=None).
 
     __call__(x) with x (..., N, D) returns q(f) as a MultivariateNormal (mean, var)
-    computed by gpk_kzz_chol_f64 (ONE fp64 factorisation of the shared K_ZZ per call)
-    + gpk_variational_f32 (batched fp64-MFMA L^{-1} K_ZX, mean, variance).
+    computed by gpk_kzz_chol_f64 (ONE fp64 factorisation of the shared K_ZZ, cached across
+    the calls of a step / eval batches, ops_autograd.KzzCache) + gpk_variational_f32
+    (column-tiled fp64-MFMA L^{-1} K_ZX, mean, variance).
     """
 
     def __init__(self, model, inducing_points: torch.Tensor, variational_distribution,
@@ -311,6 +330,18 @@ class VariationalStrategy(nn.Module):
         self.register_buffer("variational_params_initialized", torch.tensor(0))
         self.register_buffer("updated_strategy", torch.tensor(True))
         self.jitter_val = jitter_val
+        self._initialized = False     # host mirror of the buffer: no device sync per call
+        from .ops_autograd import KzzCache
+        self._kzz_cache = KzzCache()
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        self._initialized = bool(int(self.variational_params_initialized))
+        self._kzz_cache.clear()
+
+    def train(self, mode: bool = True):
+        self._kzz_cache.clear()      # GPyTorch clears its cholesky cache on mode switches
+        return super().train(mode)
 
     @property
     def variational_distribution(self):
@@ -323,20 +354,23 @@ class VariationalStrategy(nn.Module):
         return self._variational_distribution.kl_divergence()
 
     def __call__(self, x: torch.Tensor) -> MultivariateNormal:
-        if not int(self.variational_params_initialized.item()):
+        if not self._initialized:
             self._variational_distribution.initialize_variational_distribution()
             self.variational_params_initialized.fill_(1)
+            self._initialized = True
         model = self.model
         batch = x.shape[:-2]
         N, D = x.shape[-2:]
         xf = x.reshape(-1, N, D)
         from .ops_autograd import variational_predict
-        mean, var = variational_predict(
+        kern = model.covar_module
+        key = (self.inducing_points, kern.raw_outputscale, kern.base_kernel.raw_lengthscale)
+        mean, var, flag = variational_predict(
             xf, self.inducing_points, self._variational_distribution.variational_mean,
             self._variational_distribution._variational_stddev,
-            model.covar_module.outputscale, model.covar_module.base_kernel.lengthscale,
-            model.mean_module, self._jitter(x.dtype))
-        return MultivariateNormal(mean.reshape(*batch, N), var.reshape(*batch, N))
+            kern.outputscale, kern.base_kernel.lengthscale,
+            model.mean_module, self._jitter(x.dtype), cache=self._kzz_cache, key_tensors=key)
+        return MultivariateNormal(mean.reshape(*batch, N), var.reshape(*batch, N), clamp_flag=flag)
 
 
 # ---------------------------------------------------------------------------

@@ -15,7 +15,7 @@ from typing import Optional
 import torch
 
 from . import _native
-from .errors import NanError, NotPSDError, NumericalWarning
+from .errors import GpkInternalError, NanError, NotPSDError, NumericalWarning
 
 
 def _require_device(*ts: torch.Tensor) -> None:
@@ -119,30 +119,41 @@ def exact_mll_grad(X: torch.Tensor, L: torch.Tensor, z: torch.Tensor, hyper: tor
     return ExactMLLGrad(dX, dy, dhyp)
 
 
-def check_cholesky_info(info: torch.Tensor, jitter: float, inputs=(), what: str = "cholesky") -> None:
+INFO_TIMEOUT = 1 << 20   # gpk_exact.hip kInfoTimeout: a bounded LDS spin-wait expired
+
+
+def check_cholesky_info(info: torch.Tensor, jitter: float, inputs=(), what: str = "cholesky",
+                        max_tries: int = 3) -> None:
     """GPyTorch's psd_safe_cholesky bookkeeping, from the per-window info codes.
 
     One device->host sync (GPyTorch pays the same: ``torch.any(info)``). Emits the
     same NumericalWarning text per ladder step and raises NanError / NotPSDError.
+    When any window is still not PD, psd_safe_cholesky has walked the whole ladder
+    (``max_tries`` warnings) before raising, whatever the other windows needed.
     """
     info_h = info.detach().to("cpu")
     if not bool((info_h != 0).any()):
         return
-    if bool((info_h > 0).any()):
+    if bool((info_h >= INFO_TIMEOUT).any()):
+        raise GpkInternalError(f"{what}: kernel spin-wait timed out (info = 1<<20) in windows "
+                               f"{torch.nonzero(info_h >= INFO_TIMEOUT).flatten().tolist()[:16]}")
+    failed = bool((info_h > 0).any())
+    if failed:
         for t in inputs:
             if t is not None and bool(torch.isnan(t).any()):
                 raise NanError(f"{what}: {int(torch.isnan(t).sum())} of {t.numel()} elements of the "
                                f"{tuple(t.shape)} tensor are NaN.")
     steps = int((-info_h[info_h < 0]).max()) if bool((info_h < 0).any()) else 0
-    if bool((info_h > 0).any()):
-        steps = max(steps, 0)
+    if failed:
+        steps = max_tries
     for i in range(steps):
         warnings.warn(f"A not p.d., added jitter of {jitter * (10 ** i):.1e} to the diagonal",
                       NumericalWarning)
-    if bool((info_h > 0).any()):
+    if failed:
         raise NotPSDError(
             f"Matrix not positive definite after repeatedly adding jitter up to "
-            f"{jitter * 10 ** 2:.1e}. Failing windows: {torch.nonzero(info_h > 0).flatten().tolist()[:16]}")
+            f"{jitter * 10 ** (max_tries - 1):.1e}. Failing windows: "
+            f"{torch.nonzero(info_h > 0).flatten().tolist()[:16]}")
 
 
 LOG_2PI = math.log(2 * math.pi)
@@ -187,8 +198,9 @@ def kzz_cholesky(Z: torch.Tensor, outputscale, lengthscale, jitter: float = 1e-4
 @dataclass
 class VariationalOut:
     mean: torch.Tensor           # (B, N)
-    var: torch.Tensor            # (B, N)
+    var: torch.Tensor            # (B, N) clamped at 1e-6
     ell: Optional[torch.Tensor]  # (B,) sum over N of the expected log likelihood
+    flags: Optional[torch.Tensor]  # (1,) int32: bit 0 = the variance clamp fired
 
 
 def pack_variational_hyper(outputscale, noise, jitter, bias, weights, lengthscale, D, device):
@@ -206,7 +218,7 @@ def pack_variational_hyper(outputscale, noise, jitter, bias, weights, lengthscal
 def variational_forward(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vmean: torch.Tensor,
                         vstd: torch.Tensor, outputscale=None, noise=None, jitter=None, bias=None,
                         weights=None, lengthscale=None, y: Optional[torch.Tensor] = None,
-                        hyper: Optional[torch.Tensor] = None) -> VariationalOut:
+                        hyper: Optional[torch.Tensor] = None, want_flags: bool = True) -> VariationalOut:
     """Batched q(f) mean / variance (+ expected log likelihood sum when y is given)
     for the whitened mean-field VariationalStrategy (include/gpk.h::gpk_variational_f32)."""
     if X.dim() != 3:
@@ -221,6 +233,7 @@ def variational_forward(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
     dev = X.device
     X = X.detach().contiguous().float()
     Z = Z.detach().contiguous().float()
+    Linv = Linv.detach().contiguous()
     vmean = vmean.detach().contiguous().float().reshape(-1)
     vstd = vstd.detach().contiguous().float().reshape(-1)
     if hyper is None:
@@ -233,47 +246,84 @@ def variational_forward(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
     mean = torch.empty(B, N, device=dev, dtype=torch.float32)
     var = torch.empty(B, N, device=dev, dtype=torch.float32)
     ell = torch.empty(B, device=dev, dtype=torch.float32) if y is not None else None
+    flags = torch.empty(1, device=dev, dtype=torch.int32) if want_flags else None
     rc = _native.lib().gpk_variational_f32(
         X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
         hyper.data_ptr(), y.data_ptr() if y is not None else None, B, N, M, D,
         mean.data_ptr(), var.data_ptr(), ell.data_ptr() if ell is not None else None,
-        _stream_ptr(dev))
+        flags.data_ptr() if flags is not None else None, _stream_ptr(dev))
     _native.check(rc, "gpk_variational_f32")
-    return VariationalOut(mean, var, ell)
+    return VariationalOut(mean, var, ell, flags)
 
 
 @dataclass
 class VariationalAdjoint:
-    dA: torch.Tensor    # (B, M, N) float64: dObjective / dA
-    K: torch.Tensor     # (B, M, N) K_ZX
-    Q: torch.Tensor     # (B, M, N) (Linv^T dA) o K_ZX
-    part: torch.Tensor  # (B, 2M + 1): sum_i gmean A, sum_i gvar A^2, sum_i gvar
+    dX: torch.Tensor      # (B, N, D)
+    dLinv: torch.Tensor   # (M, M) float64, lower: sum over points of dA K_ZX^T
+    dZ: torch.Tensor      # (M, D) the K_ZX part of dZ
+    dvmean: torch.Tensor  # (M,)
+    dvstd: torch.Tensor   # (M,)
+    ds2: torch.Tensor     # () K_ZX + variance parts
+    dls: torch.Tensor     # (D,) the K_ZX part
 
 
 def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vmean: torch.Tensor,
                         vstd: torch.Tensor, hyper: torch.Tensor, gmean: torch.Tensor,
                         gvar: torch.Tensor) -> VariationalAdjoint:
-    """Per-window adjoint of ``variational_forward`` (one gfx950 launch,
-    include/gpk.h::gpk_variational_adjoint_f32)."""
+    """Adjoint of ``variational_forward`` except the shared K_ZZ factor (fused gfx950
+    kernels behind include/gpk.h::gpk_variational_adjoint_f32)."""
     B, N, D = X.shape
     M = Z.shape[0]
     _require_device(X, Z, Linv, vmean, vstd, hyper, gmean, gvar)
     dev = X.device
-    X = X.contiguous().float()
-    Z = Z.contiguous().float()
-    Linv = Linv.contiguous().double()
-    vmean = vmean.reshape(M).contiguous().float()
-    vstd = vstd.reshape(M).contiguous().float()
-    gmean = gmean.reshape(B, N).contiguous().float()
-    gvar = gvar.reshape(B, N).contiguous().float()
-    dA = torch.empty(B, M, N, device=dev, dtype=torch.float64)
-    K = torch.empty(B, M, N, device=dev, dtype=torch.float32)
-    Q = torch.empty(B, M, N, device=dev, dtype=torch.float32)
-    part = torch.empty(B, 2 * M + 1, device=dev, dtype=torch.float32)
-    rc = _native.lib().gpk_variational_adjoint_f32(
+    X = X.detach().contiguous().float()
+    Z = Z.detach().contiguous().float()
+    Linv = Linv.detach().contiguous().double()
+    vmean = vmean.detach().reshape(M).contiguous().float()
+    vstd = vstd.detach().reshape(M).contiguous().float()
+    gmean = gmean.detach().reshape(B, N).contiguous().float()
+    gvar = gvar.detach().reshape(B, N).contiguous().float()
+    lib = _native.lib()
+    nbytes = lib.gpk_variational_adjoint_workspace_bytes(B, N, M, D)
+    if nbytes == 0:
+        raise ValueError(f"unsupported variational shape B={B} N={N} M={M} D={D}")
+    ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+    dX = torch.empty(B, N, D, device=dev, dtype=torch.float32)
+    dLinv = torch.empty(M, M, device=dev, dtype=torch.float64)
+    dZ = torch.empty(M, D, device=dev, dtype=torch.float32)
+    dpar = torch.empty(2 * M + 1 + D, device=dev, dtype=torch.float32)
+    rc = lib.gpk_variational_adjoint_f32(
         X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
-        hyper.data_ptr(), gmean.data_ptr(), gvar.data_ptr(), B, N, M, D, dA.data_ptr(), K.data_ptr(),
-        Q.data_ptr(), part.data_ptr(), _stream_ptr(dev))
+        hyper.data_ptr(), gmean.data_ptr(), gvar.data_ptr(), B, N, M, D, ws.data_ptr(),
+        dX.data_ptr(), dLinv.data_ptr(), dZ.data_ptr(), dpar.data_ptr(), _stream_ptr(dev))
     _native.check(rc, "gpk_variational_adjoint_f32")
-    return VariationalAdjoint(dA, K, Q, part)
+    return VariationalAdjoint(dX, dLinv, dZ, dpar[:M], dpar[M:2 * M], dpar[2 * M], dpar[2 * M + 1:])
 
+
+def kzz_backward(dLinv: torch.Tensor, L: torch.Tensor, Linv: torch.Tensor, Z: torch.Tensor,
+                 outputscale: torch.Tensor, lengthscale: torch.Tensor):
+    """Back-propagate dObjective/dLinv (lower, fp64) through Linv = chol(K_ZZ + jitter)^{-1}
+    to (dZ, d outputscale, d lengthscale): once per optimizer step for all GP calls that
+    shared the factor. M x M fp64 GEMMs with the factor the forward produced (no
+    refactorisation): Lbar = -tril(Linv^T G Linv^T); Cholesky adjoint
+    S = Linv^T Phi(L^T Lbar) Linv, Kbar = (S + S^T)/2; RBF adjoint over K_ZZ.
+    Pure torch on the tensors' device (M x M only; the per-point work is in HIP)."""
+    G = dLinv.tril()
+    LinvT = Linv.transpose(0, 1)
+    Lbar = -(LinvT @ G @ LinvT).tril()
+    P = (L.transpose(0, 1) @ Lbar).tril()
+    P.diagonal().mul_(0.5)
+    S = LinvT @ P @ Linv
+    Kbar = 0.5 * (S + S.transpose(0, 1))
+    D = Z.shape[1]
+    ls = lengthscale.detach().double().reshape(-1).expand(D)
+    s2 = outputscale.detach().double().reshape(())
+    zs = Z.detach().double() / ls
+    d2 = (zs.unsqueeze(1) - zs.unsqueeze(0)).pow(2).sum(-1)
+    W = Kbar * (s2 * torch.exp(-0.5 * d2))
+    w1 = W.sum(1)
+    Wz = W @ zs
+    dZ = 2.0 * (Wz - zs * w1.unsqueeze(1)) / ls
+    dls = 2.0 * ((w1.unsqueeze(1) * zs * zs).sum(0) - (Wz * zs).sum(0)) / ls
+    ds2 = W.sum() / s2
+    return dZ, ds2, dls

@@ -2,11 +2,11 @@
 
 FORWARD values always come from libgpk.so (ops.py). BACKWARD:
 the exact path uses the analytic HIP adjoint gpk_exact_mll_grad_f32 (Cholesky / TRSM /
-RBF adjoints in one kernel). The variational path uses the per-window HIP adjoint
-gpk_variational_adjoint_f32 (recomputed K_ZX and A = L^-1 K_ZX, dA, L^-T dA, RBF
-adjoint weights); its contractions over points and windows are plain GEMMs (torch ->
-rocBLAS), and the shared M x M K_ZZ factor is differentiated once per call with fp64
-torch ops on the device. Nothing here runs on the CPU.
+RBF adjoints in one kernel). The variational path uses the fused HIP adjoint
+gpk_variational_adjoint_f32 (recomputed K_ZX and A = L^-1 K_ZX, dA, L^-T dA, the RBF
+adjoint contractions and dL^-1 = sum dA K_ZX^T as a split-K fp64-MFMA GEMM); the shared
+K_ZZ factor is ONE autograd node per step (_KzzFactor) whose M x M adjoint runs once for
+all the GP calls that used it. Nothing here runs on the CPU.
 """
 from __future__ import annotations
 
@@ -69,90 +69,142 @@ def exact_log_prob(X, y, lengthscale, outputscale, constant, noise) -> torch.Ten
     return _ExactMLL.apply(X, y, ls, s2, c, nz)
 
 
-def _kzz_linv_t(Z, ls, s2, jitter):
-    """Linv(Z, l, s2) in fp64 torch ops (M x M, differentiable): the shared K_ZZ factor
-    of the forward, for its adjoint only (once per call, not per window)."""
-    M = Z.shape[0]
-    zs = Z / ls
-    Kzz = s2 * torch.exp(-0.5 * _sq_dist(zs, zs))
-    Kzz = Kzz + jitter * torch.eye(M, device=Z.device, dtype=Z.dtype)
-    L = torch.linalg.cholesky(Kzz)
-    return torch.linalg.solve_triangular(L, torch.eye(M, device=Z.device, dtype=Z.dtype), upper=False)
+class _KzzState:
+    """Shared between a _KzzFactor node and the cache entry that may hand it to a second
+    GP call of the same step: once its backward has run, the node is spent."""
+    __slots__ = ("consumed",)
+
+    def __init__(self):
+        self.consumed = False
+
+
+class _KzzFactor(torch.autograd.Function):
+    """Linv = chol(K_ZZ + jitter)^{-1} of the shared inducing points (gpk_kzz_chol_f64).
+    One autograd node per optimizer step: every GP call of the step that uses the same
+    (Z, outputscale, lengthscale) consumes this Linv, autograd sums their dLinv, and the
+    K_ZZ adjoint (ops.kzz_backward) runs once."""
+
+    @staticmethod
+    def forward(ctx, Z, s2, ls, jitter, state, pre):
+        if pre is None:
+            D = Z.shape[-1]
+            lsv = ls.detach().reshape(-1).expand(D).contiguous().float()
+            kz = ops.kzz_cholesky(Z.detach(), None, None, jitter=jitter,
+                                  hyper=torch.cat([s2.detach().reshape(1).float(), lsv]))
+            ops.check_cholesky_info(kz.info, 1e-8, inputs=(Z,), what="K_ZZ cholesky")
+            L, Linv = kz.L, kz.Linv
+        else:
+            L, Linv = pre
+        ctx.state = state
+        ctx.save_for_backward(Z, s2, ls, L, Linv)
+        ctx.mark_non_differentiable(L)
+        return Linv, L
+
+    @staticmethod
+    def backward(ctx, dLinv, _dL):
+        Z, s2, ls, L, Linv = ctx.saved_tensors
+        ctx.state.consumed = True
+        if dLinv is None:
+            return None, None, None, None, None, None
+        dZ, ds2, dls = ops.kzz_backward(dLinv, L, Linv, Z, s2, ls)
+        dls_out = dls.sum().reshape(ls.shape) if ls.numel() == 1 else dls.reshape(ls.shape)
+        return (dZ.to(Z.dtype), ds2.reshape(s2.shape).to(s2.dtype), dls_out.to(ls.dtype),
+                None, None, None)
+
+
+class KzzCache:
+    """Per-VariationalStrategy cache of the shared K_ZZ factor.
+
+    Keyed on the identity and version counters of the inducing points and the raw
+    kernel hyper-parameters plus the jitter. Training: the enc and dec GP calls of a
+    step (denoise_model_2.py:50-51) share one factorisation and one adjoint; after the
+    step's backward the node is spent and the next call refactors. Eval (no grad): the
+    factor is reused across batches until a parameter changes, as GPyTorch's eval-mode
+    ``cholesky_factor`` cache (train.py:197-213, evaluate.py:127-137). Entries are per
+    model instance, so concurrent Optuna threads (train.py:86) never share one.
+    """
+
+    def __init__(self):
+        self._entry = None
+
+    def clear(self):
+        self._entry = None
+
+    @staticmethod
+    def _key(tensors, jitter):
+        return tuple((t.data_ptr(), t._version, tuple(t.shape), str(t.device)) for t in tensors) + (float(jitter),)
+
+    def factor(self, Z, s2, ls, jitter, key_tensors):
+        key = self._key(key_tensors, jitter)
+        grad = torch.is_grad_enabled() and (Z.requires_grad or s2.requires_grad or ls.requires_grad)
+        e = self._entry
+        if e is not None and e["key"] == key:
+            if not grad:
+                return e["Linv"].detach()
+            node = e.get("node")
+            if node is not None and not e["state"].consumed:
+                return node
+            pre = (e["L"], e["Linv"])       # same factor, fresh autograd node
+        else:
+            pre = None
+        state = _KzzState()
+        if grad:
+            Linv, L = _KzzFactor.apply(Z, s2, ls, float(jitter), state, pre)
+            self._entry = {"key": key, "L": L.detach(), "Linv": Linv.detach(), "node": Linv,
+                           "state": state}
+            return Linv
+        with torch.no_grad():
+            Linv, L = _KzzFactor.apply(Z, s2, ls, float(jitter), state, pre)
+        self._entry = {"key": key, "L": L, "Linv": Linv, "node": None, "state": state}
+        return Linv
 
 
 class _VariationalPredict(torch.autograd.Function):
-    """Forward: gpk_kzz_chol_f64 + gpk_variational_f32. Backward: the per-window adjoint
-    gpk_variational_adjoint_f32 (A, dA, L^-T dA, RBF adjoint weights, in HIP), the
-    contractions over points / windows as plain GEMMs, and the M x M K_ZZ adjoint once."""
+    """Forward: gpk_variational_f32 (one column-tiled launch over all points). Backward:
+    gpk_variational_adjoint_f32 (dX, dZ / dl / ds2 of the K_ZX part, dvmean, dvstd and
+    dLinv, fused); dLinv flows into the shared _KzzFactor node."""
 
     @staticmethod
-    def forward(ctx, x, Z, vmean, vstd, s2, ls, w, b0, jitter):
+    def forward(ctx, x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter):
         dev = x.device
         D = x.shape[-1]
         lsv = ls.detach().reshape(-1).expand(D).contiguous().float()
-        kz = ops.kzz_cholesky(Z.detach(), None, None, jitter=jitter,
-                              hyper=torch.cat([s2.detach().reshape(1).float(), lsv]))
-        ops.check_cholesky_info(kz.info, 1e-8, inputs=(Z,), what="K_ZZ cholesky")
         hyper = ops.pack_variational_hyper(s2.detach(), 1.0, jitter, b0.detach(), w.detach(), lsv, D, dev)
-        out = ops.variational_forward(x.detach(), Z.detach(), kz.Linv, vmean.detach(), vstd.detach(),
-                                      hyper=hyper)
-        ctx.jitter = jitter
-        ctx.save_for_backward(x, Z, vmean, vstd, s2, ls, w, b0, kz.Linv, kz.info, hyper)
-        return out.mean, out.var
+        out = ops.variational_forward(x.detach(), Z.detach(), Linv.detach(), vmean.detach(),
+                                      vstd.detach(), hyper=hyper)
+        ctx.save_for_backward(x, Linv, Z, vmean, vstd, s2, ls, w, b0, hyper)
+        ctx.mark_non_differentiable(out.flags)
+        return out.mean, out.var, out.flags
 
     @staticmethod
-    def backward(ctx, gmean, gvar):
-        x, Z, vmean, vstd, s2, ls, w, b0, Linv, kinfo, hyper = ctx.saved_tensors
+    def backward(ctx, gmean, gvar, _gflags):
+        x, Linv, Z, vmean, vstd, s2, ls, w, b0, hyper = ctx.saved_tensors
         B, N, D = x.shape
-        M = Z.shape[0]
         if gmean is None:
             gmean = torch.zeros(B, N, device=x.device)
         if gvar is None:
             gvar = torch.zeros(B, N, device=x.device)
-        adj = ops.variational_adjoint(x.detach(), Z.detach(), Linv, vmean.detach(), vstd.detach(),
-                                      hyper, gmean, gvar)
-        lsv = ls.detach().reshape(-1).expand(D).float()
-        xs = x.detach().float() / lsv
-        zs = Z.detach().float() / lsv
-        Q = adj.Q
-        r = Q.sum(1)                                      # (B, N)
-        q = Q.sum((0, 2))                                 # (M,)
-        QZ = torch.einsum("bmn,md->bnd", Q, zs)
-        gm = gmean.reshape(B, N).float()
-        dX = (QZ - xs * r.unsqueeze(-1)) / lsv + gm.unsqueeze(-1) * w.detach().reshape(1, 1, D).float()
-        P = torch.einsum("bmn,bnd->md", Q, xs)
-        dZ = (P - zs * q.unsqueeze(-1)) / lsv
-        dls = ((q.unsqueeze(-1) * zs * zs).sum(0) - 2.0 * (zs * P).sum(0)
-               + torch.einsum("bn,bnd->d", r, xs * xs)) / lsv
-        ds2 = Q.sum() / s2.detach().float() + adj.part[:, 2 * M].sum()
-        dvm = adj.part[:, :M].sum(0)
-        dvs = 2.0 * vstd.detach().reshape(M).float() * adj.part[:, M:2 * M].sum(0)
-        dw = torch.einsum("bn,bnd->d", gm, x.detach().float())
+        adj = ops.variational_adjoint(x, Z, Linv, vmean, vstd, hyper, gmean, gvar)
+        gm = gmean.reshape(B * N).float()
+        dw = x.detach().reshape(B * N, D).float().transpose(0, 1) @ gm     # LinearMean weights
         db0 = gm.sum()
-        # shared K_ZZ factor: dLinv = sum_b dA K^T (lower part: Linv_mp is used for m >= p)
-        # (batched per window, then summed: a single M x M GEMM with a B*N-long
-        # contraction leaves the GPU idle -- one output tile)
-        dLinv = torch.bmm(adj.dA, adj.K.double().transpose(1, 2)).sum(0).tril()
-        t = int(-kinfo.item()) if int(kinfo.item()) < 0 else 0
-        jit = ctx.jitter + (1e-8 * 10 ** (t - 1) if t > 0 else 0.0)
-        with torch.enable_grad():
-            Z2 = Z.detach().double().requires_grad_(True)
-            l2 = lsv.double().requires_grad_(True)
-            s22 = s2.detach().double().reshape(()).requires_grad_(True)
-            gZ, gl, gs = torch.autograd.grad(_kzz_linv_t(Z2, l2, s22, jit), [Z2, l2, s22], dLinv)
-        dZ = dZ + gZ.float()
-        dls = dls + gl.float()
-        ds2 = ds2 + gs.float()
-        dls_out = dls.sum().reshape(ls.shape) if ls.numel() == 1 else dls.reshape(ls.shape)
-        return (dX.to(x.dtype), dZ.to(Z.dtype), dvm.reshape(vmean.shape).to(vmean.dtype),
-                dvs.reshape(vstd.shape).to(vstd.dtype), ds2.reshape(s2.shape).to(s2.dtype),
-                dls_out.to(ls.dtype), dw.reshape(w.shape).to(w.dtype), db0.reshape(b0.shape).to(b0.dtype),
+        dls = adj.dls.sum().reshape(ls.shape) if ls.numel() == 1 else adj.dls.reshape(ls.shape)
+        return (adj.dX.to(x.dtype), adj.dLinv, adj.dZ.to(Z.dtype),
+                adj.dvmean.reshape(vmean.shape).to(vmean.dtype),
+                adj.dvstd.reshape(vstd.shape).to(vstd.dtype), adj.ds2.reshape(s2.shape).to(s2.dtype),
+                dls.to(ls.dtype), dw.reshape(w.shape).to(w.dtype), db0.reshape(b0.shape).to(b0.dtype),
                 None)
 
 
-def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module, jitter):
-    """q(f) mean / variance for (B, N, D) windows (HIP forward; see module docstring)."""
+def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module, jitter,
+                        cache: Optional[KzzCache] = None, key_tensors=None):
+    """q(f) mean / variance / clamp flag for (B, N, D) windows (HIP forward and backward;
+    see module docstring). ``cache`` shares the K_ZZ factor between calls."""
     w = mean_module.weights.reshape(-1)
     b0 = mean_module.bias.reshape(()) if mean_module.bias is not None else torch.zeros((), device=x.device)
-    return _VariationalPredict.apply(x, Z, vmean, vstd, outputscale.reshape(()),
-                                     lengthscale.reshape(-1), w, b0, float(jitter))
+    s2 = outputscale.reshape(())
+    ls = lengthscale.reshape(-1)
+    if cache is None:
+        cache = KzzCache()
+    Linv = cache.factor(Z, s2, ls, jitter, key_tensors if key_tensors is not None else (Z, s2, ls))
+    return _VariationalPredict.apply(x, Linv, Z, vmean, vstd, s2, ls, w, b0, float(jitter))

@@ -88,14 +88,16 @@ int gpk_exact_mll_grad_f32(const float* X, const float* L, const float* z, const
  *   A    = K_ZZ + jitter (fp32 add, as K_ZZ.add_jitter), then upcast to fp64
  *   L    = psd_safe_cholesky(A) with the fp64 ladder chol_jitter * 10^t
  *   Linv = L^{-1}
- * K_ZZ = s2 * exp(-0.5 ||(z_i - z_j)/l||^2) with ARD lengthscales.
+ * K_ZZ = s2 * exp(-0.5 ||(z_i - z_j)/l||^2) with ARD lengthscales (GPyTorch's centred
+ * GEMM-form squared distance, diagonal not zeroed: Z requires grad in the reference).
+ * One workgroup, blocked (32-column) elimination of [A | I] in fp64.
  *
  * Replaces (reference): the per-window (b-fold redundant) fp64 Cholesky that
  * VariationalStrategy._cholesky_factor runs for ToyDeepGPHiddenLayer
  * (denoising_model/DeepGP.py:33-38, inducing points expanded to the batch by
  * upstream _expand_inputs); SURVEY.md §8a rows a7/a9.
  *
- * Z   : (M, D) float (M <= 256)     hyp : device float[1 + D] = {s2, lengthscale[D]}
+ * Z   : (M, D) float (M <= 256, D <= 64)     hyp : device float[1 + D] = {s2, lengthscale[D]}
  * L, Linv : (M, M) double out (lower, zero upper)   info : (1,) int out, codes as above
  */
 int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitter,
@@ -104,7 +106,7 @@ int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitte
 
 /*
  * Batched variational predictive distribution and expected log likelihood:
- *   K_ZX = s2 * exp(-0.5 ||(z_m - x_i)/l||^2)       (fp32, per window)
+ *   K_ZX = s2 * exp(-0.5 ||(z_m - x_i)/l||^2)       (fp32, GPyTorch's centred GEMM form)
  *   A    = Linv @ K_ZX                              (fp64, then cast to fp32)
  *   mean = A^T m + x @ w + b0                       (LinearMean)
  *   var  = max(s2 + jitter + sum_m A_mi^2 (s_m^2 - 1), 1e-6)
@@ -120,29 +122,37 @@ int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitte
  * vmean, vstd : (M,) float (MeanFieldVariationalDistribution mean / stddev)
  * hyp : device float[4 + 2D] = {s2, noise, jitter, bias, weights[D], lengthscale[D]}
  * y : (B, N) float or NULL;  mean, var : (B, N) float out;  ell : (B,) float out or NULL
+ * (needs y)   flags : (1,) int out or NULL: bit 0 set when the variance clamp fired
+ * (the caller emits GPyTorch's NumericalWarning from MultivariateNormal.variance).
  */
 int gpk_variational_f32(const float* X, const float* Z, const double* Linv, const float* vmean,
                         const float* vstd, const float* hyp, const float* y, int B, int N, int M,
-                        int D, float* mean, float* var, float* ell, void* stream);
+                        int D, float* mean, float* var, float* ell, int* flags, void* stream);
 
 /*
- * Per-window adjoint of gpk_variational_f32 for the objective
- * sum(gmean * mean) + sum(gvar * var)  (var's clamp at 1e-6 passes no gradient):
- *   dA = gmean_i m_m + 2 gvar_i (s_m^2 - 1) A_mi      -> dA   (B, M, N) double out
- *   K_ZX                                                -> K    (B, M, N) float out
- *   Q  = (Linv^T dA) o K_ZX                             -> Q    (B, M, N) float out
- *   part[b] = {sum_i gmean A_mi (M), sum_i gvar A_mi^2 (M), sum_i gvar}  (B, 2M+1) float out
- * The caller contracts these with plain GEMMs (dLinv = sum_b dA K^T; dX, dZ, dl, ds2
- * from Q) and back-propagates dLinv through the shared M x M K_ZZ factor once.
+ * Adjoint of gpk_variational_f32 for the objective sum(gmean * mean) + sum(gvar * var)
+ * (var's clamp at 1e-6 passes no gradient), everything but the K_ZZ factor:
+ *   dA    = gmean_i m_m + 2 gvar_i (s_m^2 - 1) A_mi         (fp32, as the reference's dA)
+ *   dK    = Linv^T dA,  Q = dK o K_ZX
+ *   dX    (B, N, D) float out: RBF adjoint + gmean_i w
+ *   dLinv (M, M) double out: sum over all points of dA K_ZX^T (lower, upper zero) -- the
+ *         caller back-propagates it through the shared K_ZZ factor once per step
+ *   dZ    (M, D) float out: the K_ZX part of dZ
+ *   dpar  (2M + 1 + D) float out: {dvmean (M), dvstd (M), ds2 (K_ZX and variance parts), dl (D)}
+ * (dweights = X^T gmean and dbias = sum gmean are plain reductions left to the caller.)
+ * workspace : gpk_variational_adjoint_workspace_bytes(B, N, M, D) bytes of device memory.
+ * All sums are in a fixed order (run-to-run deterministic).
  *
- * Replaces (reference): the per-window part of the autograd backward that
- * train.py:166 runs through VariationalStrategy / DeepGPLayer for DeepGPp
- * (denoising_model/DeepGP.py:51-99, forecast_denoising.py:86-104); SURVEY.md §8f row 1.
+ * Replaces (reference): the autograd backward that train.py:166 runs through
+ * VariationalStrategy / DeepGPLayer for DeepGPp (denoising_model/DeepGP.py:51-99,
+ * forecast_denoising.py:86-104); SURVEY.md §8f row 1.
  */
+size_t gpk_variational_adjoint_workspace_bytes(int B, int N, int M, int D);
 int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Linv,
                                 const float* vmean, const float* vstd, const float* hyp,
                                 const float* gmean, const float* gvar, int B, int N, int M, int D,
-                                double* dA, float* K, float* Q, float* part, void* stream);
+                                void* workspace, float* dX, double* dLinv, float* dZ, float* dpar,
+                                void* stream);
 
 #ifdef __cplusplus
 }

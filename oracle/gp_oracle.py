@@ -274,7 +274,8 @@ class VariationalResult:
 
 
 def variational_forward(X, Z, lengthscale, outputscale, weights, bias, m, s,
-                        jitter=1e-4, dtype=np.float32, min_var=None, chol_jitter=None):
+                        jitter=1e-4, dtype=np.float32, min_var=None, chol_jitter=None,
+                        var_jitter=None):
     """``VariationalStrategy.forward`` (whitened) + ``LinearMean`` + MeanField q(u):
 
     K_ZZ + jitter (input dtype) -> fp64 -> L = psd_safe_cholesky (fp64 ladder);
@@ -282,6 +283,8 @@ def variational_forward(X, Z, lengthscale, outputscale, weights, bias, m, s,
     var = s2 + jitter + sum_m A_mi^2 (s_m^2 - 1), then MVN ``.variance`` clamp.
     Z is shared (M, D) — the reference expands it to (b, M, D), which changes
     nothing numerically (DeepGP.py:22, upstream ``_expand_inputs``).
+    ``var_jitter`` (test hook) overrides the jitter added to K_XX's diagonal only, to
+    drive the variance clamp in tests; None = ``jitter`` as GPyTorch.
     """
     X = np.asarray(X, dtype=dtype)
     Z = np.asarray(Z, dtype=dtype)
@@ -303,7 +306,8 @@ def variational_forward(X, Z, lengthscale, outputscale, weights, bias, m, s,
     w = np.asarray(weights, dtype=dtype).reshape(-1)
     mean = np.einsum('bmn,m->bn', A, mvec) + (X @ w) + dtype(bias)
     s2m1 = svec * svec - dtype(1.0)
-    var = dtype(outputscale) + dtype(jitter) + np.einsum('bmn,m->bn', A * A, s2m1)
+    vj = jitter if var_jitter is None else var_jitter
+    var = dtype(outputscale) + dtype(vj) + np.einsum('bmn,m->bn', A * A, s2m1)
     if min_var is None:
         min_var = 1e-6 if dtype == np.float32 else 1e-10
     var = np.maximum(var, dtype(min_var)).astype(dtype)
@@ -398,7 +402,7 @@ def _rbf_t(a, b, ls, s2):
 
 
 def variational_grads(X, Z, lengthscale, outputscale, weights, bias, m, s, gmean, gvar,
-                      jitter=1e-4, min_var=1e-6):
+                      jitter=1e-4, min_var=1e-6, var_jitter=None):
     """d/dtheta of sum(gmean * mean) + sum(gvar * var) for ``variational_forward``
     (DeepGP.py:51-99 via VariationalStrategy: K_ZZ + jitter -> fp64 Cholesky,
     A = L^{-1} K_ZX, mean = A^T m + x w + b0, var = s2 + jitter + sum A^2 (s^2-1)
@@ -417,7 +421,8 @@ def variational_grads(X, Z, lengthscale, outputscale, weights, bias, m, s, gmean
     Kzx = _rbf_t(Zt.expand(B, M, D), Xt, lst, s2t)
     A = torch.linalg.solve_triangular(L, Kzx, upper=False)
     mean = (A * mt[:, None]).sum(-2) + Xt @ wt + b0t
-    var = (s2t + jitter + (A * A * (st * st - 1.0)[:, None]).sum(-2)).clamp_min(min_var)
+    vj = jitter if var_jitter is None else var_jitter
+    var = (s2t + vj + (A * A * (st * st - 1.0)[:, None]).sum(-2)).clamp_min(min_var)
     obj = (torch.as_tensor(np.asarray(gmean, np.float64)) * mean).sum() + \
           (torch.as_tensor(np.asarray(gvar, np.float64)) * var).sum()
     names = ["X", "Z", "m", "s", "outputscale", "lengthscale", "weights", "bias"]
@@ -445,3 +450,40 @@ def exact_mll_grads(X, y, lengthscale, outputscale, mean_constant, noise, gout=N
     gs = torch.autograd.grad((g * mll).sum(), [Xt, yt, lst, s2t, ct, nzt])
     names = ["X", "y", "lengthscale", "outputscale", "mean_constant", "noise"]
     return {k: v.detach().numpy() for k, v in zip(names, gs)}
+
+
+def variational_forward_torch_cpu(X, Z, lengthscale, outputscale, weights, bias, m, s, jitter=1e-4):
+    """Torch-CPU restatement of what GPyTorch dispatches for VariationalStrategy.forward
+    (DeepGP.py:51-73): Z expanded to the batch, K over cat[Z, x] in the
+    centred _sq_dist GEMM form, K_ZZ + jitter -> .double() -> torch.linalg.cholesky_ex
+    ONCE PER WINDOW (the reference's b-fold redundant factorisation), fp64
+    solve_triangular for A = L^-1 K_ZX, cast to fp32, mean = A^T m + x w + b0,
+    var = s2 + jitter + sum A^2 (s^2 - 1) clamped. Used as the timed CPU baseline of the
+    variational path in bench.py (CPU only)."""
+    import torch
+    X = torch.as_tensor(X)
+    Z = torch.as_tensor(Z)
+    B, N, D = X.shape
+    M = Z.shape[0]
+    ls = torch.as_tensor(lengthscale, dtype=X.dtype).reshape(-1)
+    full = torch.cat([Z.expand(B, M, D), X], -2) / ls
+    adj = full[..., :M, :].mean(-2, keepdim=True)
+
+    def sqd(a, b):
+        a = a - adj
+        b = b - adj
+        an = a.pow(2).sum(-1, keepdim=True)
+        bn = b.pow(2).sum(-1, keepdim=True)
+        return (torch.cat([-2.0 * a, an, torch.ones_like(an)], -1)
+                @ torch.cat([b, torch.ones_like(bn), bn], -1).transpose(-1, -2)).clamp_min_(0)
+    zz = full[..., :M, :]
+    Kzz = sqd(zz, zz).div_(-2).exp_().mul_(outputscale)
+    Kzz.diagonal(dim1=-2, dim2=-1).add_(jitter)
+    Kzx = sqd(zz, full[..., M:, :]).div_(-2).exp_().mul_(outputscale)
+    L, info = torch.linalg.cholesky_ex(Kzz.double())
+    A = torch.linalg.solve_triangular(L, Kzx.double(), upper=False).to(X.dtype)
+    mvec = torch.as_tensor(m, dtype=X.dtype)
+    svec = torch.as_tensor(s, dtype=X.dtype)
+    mean = (A.transpose(-1, -2) @ mvec.unsqueeze(-1)).squeeze(-1) + X @ torch.as_tensor(weights, dtype=X.dtype).reshape(-1) + bias
+    var = (outputscale + jitter + ((A * A) * (svec * svec - 1.0).unsqueeze(-1)).sum(-2)).clamp_min(1e-6)
+    return mean, var

@@ -133,3 +133,111 @@ def test_denoise_model_2_gp_branch_train_step(cuda_device):
     loss.backward()
     opt.step()
     assert out.shape == (b, pred_len, d) and torch.isfinite(loss)
+
+
+def test_kzz_factor_shared_by_enc_and_dec_calls(cuda_device, monkeypatch):
+    """denoise_model_2.forward calls the GP twice per step with the same inducing points
+    (denoise_model_2.py:50-51): ONE K_ZZ factorisation and ONE K_ZZ adjoint per step; the
+    optimizer step invalidates it; eval batches reuse it. The summed
+    gradients of both calls match the fp64 oracle."""
+    from fine_grained_gaussian_process_forcasting_amd import ops, settings
+    calls = {"chol": 0, "adj": 0}
+    real_chol, real_adj = ops.kzz_cholesky, ops.kzz_backward
+
+    def chol(*a, **k):
+        calls["chol"] += 1
+        return real_chol(*a, **k)
+
+    def adj(*a, **k):
+        calls["adj"] += 1
+        return real_adj(*a, **k)
+    monkeypatch.setattr(ops, "kzz_cholesky", chol)
+    monkeypatch.setattr(ops, "kzz_backward", adj)
+    d, b = 16, 4
+    model = _deepgp(d, 5, cuda_device)
+    g = torch.Generator().manual_seed(2)
+    enc = (torch.randn(b, 40, d, generator=g) / 4).to(cuda_device)
+    dec = (torch.randn(b, 24, d, generator=g) / 4).to(cuda_device)
+    ge = torch.randn(1, b, 40, generator=g).to(cuda_device)
+    gd = torch.randn(1, b, 24, generator=g).to(cuda_device)
+    opt = torch.optim.SGD(model.parameters(), lr=1e-3)
+    with settings.num_likelihood_samples(1):
+        me, de = model.predict(enc)
+        md, dd = model.predict(dec)
+        obj = (ge * me).sum() + (gd * md).sum() + (gd * dd.variance).sum()
+    assert calls["chol"] == 1
+    obj.backward()
+    assert calls["adj"] == 1
+    # gradients of the two-call objective vs the oracle (sum of per-call grads)
+    hl = model.hidden_layer
+    vs = hl.variational_strategy
+    P = {k: v.detach().cpu().double().numpy() for k, v in dict(
+        Z=vs.inducing_points, m=vs._variational_distribution.variational_mean,
+        s=vs._variational_distribution._variational_stddev, w=hl.mean_module.weights.reshape(-1),
+        ls=hl.covar_module.base_kernel.lengthscale.reshape(-1)).items()}
+    s2 = float(hl.covar_module.outputscale.item())
+    b0 = float(hl.mean_module.bias.item())
+    r1 = O.variational_grads(enc.cpu().double().numpy(), P["Z"], P["ls"], s2, P["w"], b0, P["m"], P["s"],
+                             ge[0].cpu().double().numpy(), np.zeros((b, 40)), jitter=1e-4)
+    r2 = O.variational_grads(dec.cpu().double().numpy(), P["Z"], P["ls"], s2, P["w"], b0, P["m"], P["s"],
+                             gd[0].cpu().double().numpy(), gd[0].cpu().double().numpy(), jitter=1e-4)
+    gZ = vs.inducing_points.grad.cpu().double().numpy()
+    want = r1["Z"] + r2["Z"]
+    assert np.linalg.norm(gZ - want) / np.linalg.norm(want) <= 1e-4
+    gm = vs._variational_distribution.variational_mean.grad.cpu().double().numpy()
+    want = r1["m"] + r2["m"]
+    assert np.linalg.norm(gm - want) / np.linalg.norm(want) <= 1e-4
+    # after the optimizer step the inducing points changed: the next step refactors
+    opt.step()
+    with settings.num_likelihood_samples(1):
+        model.predict(enc)
+    assert calls["chol"] == 2
+    # eval / no-grad: reused across batches until a parameter changes
+    model.eval()
+    with torch.no_grad(), settings.num_likelihood_samples(1):
+        model.predict(enc)
+        model.predict(dec)
+        model.predict(enc[:2])
+    assert calls["chol"] == 3
+
+
+def test_concurrent_callers_match_serial(cuda_device):
+    """Optuna trains n_jobs=4 models in 4 host threads on one device (train.py:86):
+    the C ABI is re-entrant and stream-ordered, so each thread's forward + ELBO +
+    backward equals the same model run alone (bitwise: fixed-order sums)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from fine_grained_gaussian_process_forcasting_amd import settings
+    from fine_grained_gaussian_process_forcasting_amd.mlls import DeepApproximateMLL, VariationalELBO
+    d, b = 16, 8
+    # Model construction seeds the process-global RNG (DeepGP.py:17-19) and q(u) is drawn
+    # with the global RNG at the first call: build and initialise serially (as the
+    # reference itself would need to), then run the GP work concurrently.
+    models, data = [], []
+    with settings.num_likelihood_samples(1):
+        for seed in range(4):
+            model = _deepgp(d, seed, cuda_device)
+            with torch.no_grad():
+                model.predict(torch.zeros(1, 4, d, device=cuda_device))
+            g = torch.Generator().manual_seed(seed)
+            x = (torch.randn(b, 64, d, generator=g) / 4).to(cuda_device)
+            y = torch.randn(b, 64, 1, generator=g).to(cuda_device)
+            models.append(model)
+            data.append((x, y))
+
+    def run(i):
+        model, (x, y) = models[i], data[i]
+        model.zero_grad(set_to_none=True)
+        _, dist = model.predict(x)
+        loss = -DeepApproximateMLL(VariationalELBO(model.likelihood, model, d))(dist, y.permute(2, 0, 1)).mean()
+        loss.backward()
+        torch.cuda.synchronize()
+        return float(loss), {n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()}
+
+    with settings.num_likelihood_samples(1):
+        serial = [run(i) for i in range(4)]
+        with ThreadPoolExecutor(4) as ex:
+            threaded = list(ex.map(run, range(4)))
+    for (l1, g1), (l2, g2) in zip(serial, threaded):
+        assert l1 == l2
+        for n in g1:
+            assert torch.equal(g1[n], g2[n]), n

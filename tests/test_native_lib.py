@@ -39,8 +39,31 @@ def test_argument_validation_without_device():
     assert lib.gpk_exact_mll_f32(one, one, one, 1, 1, 8, 2, -1.0, 3, None, None, one, one, None) == -8
     assert lib.gpk_exact_mll_f32(one, one, one, 1, 0, 8, 2, 1e-6, 3, None, None, one, one, None) == 0
     assert lib.gpk_kzz_chol_f64(one, one, 300, 4, 1e-4, 1e-8, 3, one, one, one, None) == -3
-    assert lib.gpk_variational_f32(one, one, one, one, one, one, None, 1, 8, 8, 65, one, one, None, None) == -11
+    assert lib.gpk_variational_f32(one, one, one, one, one, one, None, 1, 8, 8, 65, one, one, None, None, None) == -11
+    # ell requested without targets
+    assert lib.gpk_variational_f32(one, one, one, one, one, one, None, 1, 8, 8, 4, one, one, one, None, None) == -7
+    assert lib.gpk_kzz_chol_f64(one, one, 64, 65, 1e-4, 1e-8, 3, one, one, one, None) == -4
     assert b"N exceeds" in lib.gpk_strerror(-6)
+
+
+def test_variational_adjoint_entry_validation_without_device():
+    from fine_grained_gaussian_process_forcasting_amd import _native
+    lib = _native.lib()
+    one = ctypes.c_void_p(16)
+    ws = lib.gpk_variational_adjoint_workspace_bytes(4, 192, 256, 32)
+    # dA and K_ZX (M x B*N fp32 each) dominate the workspace
+    assert ws >= 2 * 256 * 4 * 192 * 4
+    assert lib.gpk_variational_adjoint_workspace_bytes(4, 192, 257, 32) == 0
+    assert lib.gpk_variational_adjoint_workspace_bytes(4, 192, 64, 65) == 0
+    args = [one] * 8 + [2, 16, 8, 4] + [one] * 5 + [None]
+    assert lib.gpk_variational_adjoint_f32(*args) != 0 or True  # (pointer validity not checkable)
+    for idx, code in [(0, -1), (6, -7), (12, -13), (13, -14), (14, -15), (15, -16), (16, -17)]:
+        bad = list(args); bad[idx] = None
+        assert lib.gpk_variational_adjoint_f32(*bad) == code
+    bad = list(args); bad[10] = 300
+    assert lib.gpk_variational_adjoint_f32(*bad) == -11
+    bad = list(args); bad[11] = 65
+    assert lib.gpk_variational_adjoint_f32(*bad) == -12
 
 
 def test_ops_refuse_cpu_tensors():

@@ -43,13 +43,81 @@ def test_variational_grads_vs_oracle(cuda_device, B, N, M, D):
     lsd = torch.tensor(ls, dtype=torch.float32, device=dev, requires_grad=True)
     s2d = torch.tensor(s2, device=dev, requires_grad=True)
     mm = types.SimpleNamespace(weights=wd, bias=b0d)
-    mean, var = ops_autograd.variational_predict(Xd, Zd, md, sd, s2d, lsd, mm, 1e-4)
+    mean, var, _ = ops_autograd.variational_predict(Xd, Zd, md, sd, s2d, lsd, mm, 1e-4)
     ((gmean.to(dev) * mean).sum() + (gvar.to(dev) * var).sum()).backward()
     ref = O.variational_grads(X.double().numpy(), Z.double().numpy(), ls, s2, w.double().numpy(), b0,
                               m.double().numpy(), s.double().numpy(), gmean.double().numpy(),
                               gvar.double().numpy(), jitter=1e-4)
     got = {"X": Xd.grad, "Z": Zd.grad, "m": md.grad, "s": sd.grad, "outputscale": s2d.grad,
            "lengthscale": lsd.grad, "weights": wd.grad, "bias": b0d.grad}
+    for k, v in got.items():
+        e = _rel(v.detach().cpu().numpy(), ref[k])
+        print(f"B={B} N={N} M={M} D={D} {k:12s} {e:.2e}")
+        assert e <= TOL, (k, e)
+
+
+def _op_level_grads(dev, X, Z, m, s, w, b0, ls, s2, gmean, gvar, jitter, var_jitter):
+    """The product backward composed from the op-level entry points (what
+    _VariationalPredict + _KzzFactor do), with a separate K_XX jitter (test hook)."""
+    from fine_grained_gaussian_process_forcasting_amd import ops
+    D = X.shape[-1]
+    lst = torch.tensor(ls, dtype=torch.float32, device=dev)
+    f = ops.kzz_cholesky(Z.to(dev), s2, lst, jitter=jitter)
+    hyper = ops.pack_variational_hyper(s2, 1.0, var_jitter, b0, w.to(dev), lst, D, dev)
+    adj = ops.variational_adjoint(X.to(dev), Z.to(dev), f.Linv, m.to(dev), s.to(dev), hyper,
+                                  gmean.to(dev), gvar.to(dev))
+    dZk, ds2k, dlsk = ops.kzz_backward(adj.dLinv, f.L, f.Linv, Z.to(dev), torch.tensor(s2, device=dev), lst)
+    return {"X": adj.dX, "Z": adj.dZ.double() + dZk, "m": adj.dvmean, "s": adj.dvstd,
+            "outputscale": adj.ds2.double() + ds2k, "lengthscale": adj.dls.double() + dlsk}
+
+
+def test_variance_clamp_gradient_mask(cuda_device):
+    """Where the variance clamp is active (MVN.variance clamp_min), gvar passes no
+    gradient: driven with a negative K_XX jitter (test hook) so ~half the points clamp."""
+    B, N, M, D = 3, 48, 32, 8
+    g = torch.Generator().manual_seed(77)
+    X = torch.randn(B, N, D, generator=g) / np.sqrt(D)
+    Z = torch.randn(M, D, generator=g) / np.sqrt(D)
+    m = 0.3 * torch.randn(M, generator=g)
+    s = 0.1 + 0.2 * torch.rand(M, generator=g)
+    w = torch.randn(D, generator=g)
+    ls = np.linspace(0.7, 1.3, D)
+    s2, b0 = 0.69, 0.1
+    gmean = torch.randn(B, N, generator=g)
+    gvar = torch.randn(B, N, generator=g)
+    ref_fwd = O.variational_forward(X.double().numpy(), Z.double().numpy(), ls, s2, w.double().numpy(), b0,
+                                    m.double().numpy(), s.double().numpy(), jitter=1e-4,
+                                    dtype=np.float64, var_jitter=-0.15)
+    frac = float((ref_fwd.var <= 1e-6).mean())
+    assert 0.05 < frac < 0.95, frac
+    got = _op_level_grads(cuda_device, X, Z, m, s, w, b0, ls, s2, gmean, gvar, 1e-4, -0.15)
+    ref = O.variational_grads(X.double().numpy(), Z.double().numpy(), ls, s2, w.double().numpy(), b0,
+                              m.double().numpy(), s.double().numpy(), gmean.double().numpy(),
+                              gvar.double().numpy(), jitter=1e-4, var_jitter=-0.15)
+    for k, v in got.items():
+        e = _rel(v.detach().cpu().numpy(), ref[k])
+        print(f"clamp-mask {k:12s} {e:.2e}")
+        assert e <= TOL, (k, e)
+
+
+@pytest.mark.parametrize("B,N,M,D", [(8, 192, 256, 32), (16, 256, 64, 32), (5, 96, 256, 16)])
+def test_variational_grads_reference_shapes(cuda_device, B, N, M, D):
+    """The backward at the reference's GP shapes (M=256 default, DeepGP.py:15; cfg 5's
+    M=64) on a window sample, every gradient block vs the fp64 oracle."""
+    g = torch.Generator().manual_seed(B + N + M)
+    X = torch.randn(B, N, D, generator=g) / np.sqrt(D)
+    Z = torch.randn(M, D, generator=g) / np.sqrt(D)
+    m = 0.3 * torch.randn(M, generator=g)
+    s = 0.5 + 0.5 * torch.rand(M, generator=g)
+    w = torch.randn(D, generator=g)
+    ls = np.linspace(0.7, 1.3, D)
+    s2, b0 = 0.9, 0.3
+    gmean = torch.randn(B, N, generator=g)
+    gvar = torch.randn(B, N, generator=g)
+    got = _op_level_grads(cuda_device, X, Z, m, s, w, b0, ls, s2, gmean, gvar, 1e-4, 1e-4)
+    ref = O.variational_grads(X.double().numpy(), Z.double().numpy(), ls, s2, w.double().numpy(), b0,
+                              m.double().numpy(), s.double().numpy(), gmean.double().numpy(),
+                              gvar.double().numpy(), jitter=1e-4)
     for k, v in got.items():
         e = _rel(v.detach().cpu().numpy(), ref[k])
         print(f"B={B} N={N} M={M} D={D} {k:12s} {e:.2e}")
