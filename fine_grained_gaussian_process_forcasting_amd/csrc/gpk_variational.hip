@@ -329,7 +329,11 @@ GPK_DEVICE void build_kzx(const float* zs, const float* xs, const float* zn, con
 }
 
 // A = L^{-1} K_ZX for the wave's row tiles (fp64 MFMA). acc[j][q][r] = A[16 rt_j + g + 4r][16 ct_q + c].
-// Linv loads run one k-step ahead of the MFMAs that use them.
+// The contraction runs in k-blocks of 16 inducing points; inside a block MFMA step u
+// takes p = 16 kb + 4 g + u on lane group g (any consistent k-order is legal), so a
+// lane's four A operands of a block are 4 consecutive doubles of one L^{-1} row. The
+// whole next block's A operands are loaded while the current block's MFMAs run (row
+// tile rt only needs blocks kb <= rt: L^{-1} is lower triangular).
 template <int MB>
 GPK_DEVICE void gemm_linv_k(const double* __restrict__ Linv, const float* Kl, int M,
                             f64x4 (&acc)[VarGeo<MB>::RT][VarGeo<MB>::CT]) {
@@ -345,32 +349,43 @@ GPK_DEVICE void gemm_linv_k(const double* __restrict__ Linv, const float* Kl, in
 #pragma unroll
   for (int j = 0; j < G::RT; ++j)
     if (wr + G::WR * j < MB) last = wr + G::WR * j;
-  const int smax = 4 * (last + 1);
-  double an[G::RT];
-  auto load_a = [&](int s, double (&dst)[G::RT]) {
+  double an[G::RT][4];
+  auto load_blk = [&](int kb, double (&dst)[G::RT][4]) {
 #pragma unroll
     for (int j = 0; j < G::RT; ++j) {
       const int rt = wr + G::WR * j;
-      const int m = 16 * rt + c, p = 4 * s + g;
-      dst[j] = (rt < MB && s < 4 * (rt + 1) && m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
+      const int m = 16 * rt + c;
+      const bool ok = rt < MB && kb <= rt && m < M;
+      const double* row = Linv + (size_t)(ok ? m : 0) * M;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = 16 * kb + 4 * g + u;
+        dst[j][u] = (ok && p < M) ? row[p] : 0.0;
+      }
     }
   };
-  load_a(0, an);
-  for (int s = 0; s < smax; ++s) {
-    double a[G::RT];
+  load_blk(0, an);
+  for (int kb = 0; kb <= last; ++kb) {
+    double a[G::RT][4];
 #pragma unroll
-    for (int j = 0; j < G::RT; ++j) a[j] = an[j];
-    if (s + 1 < smax) load_a(s + 1, an);
-    const int p = 4 * s + g;
-    double b[G::CT];
+    for (int j = 0; j < G::RT; ++j)
 #pragma unroll
-    for (int q = 0; q < G::CT; ++q) b[q] = (double)Kl[p * G::TW + 16 * (wc * G::CT + q) + c];
+      for (int u = 0; u < 4; ++u) a[j][u] = an[j][u];
+    if (kb < last) load_blk(kb + 1, an);
+    float bf[G::CT][4];
 #pragma unroll
-    for (int j = 0; j < G::RT; ++j) {
-      const int rt = wr + G::WR * j;
-      if (rt < MB && s < 4 * (rt + 1)) {
+    for (int q = 0; q < G::CT; ++q)
 #pragma unroll
-        for (int q = 0; q < G::CT; ++q) acc[j][q] = mfma64(a[j], b[q], acc[j][q]);
+      for (int u = 0; u < 4; ++u) bf[q][u] = Kl[(16 * kb + 4 * g + u) * G::TW + 16 * (wc * G::CT + q) + c];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int j = 0; j < G::RT; ++j) {
+        const int rt = wr + G::WR * j;
+        if (rt < MB && kb <= rt) {
+#pragma unroll
+          for (int q = 0; q < G::CT; ++q) acc[j][q] = mfma64(a[j][u], (double)bf[q][u], acc[j][q]);
+        }
       }
     }
   }
@@ -634,33 +649,55 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       if (col < nvalid) wsK[(size_t)p * BN + col0 + col] = Kl[p * TW + col];
     }
     __syncthreads();
-    // dK = L^{-T} dA (fp64 MFMA): output rows p = the wave's row tiles, k = m >= p
+    // dK = L^{-T} dA (fp64 MFMA): output rows p = the wave's row tiles, k = m >= p, in
+    // k-blocks of 16 (k-order m = 16 kb + 4 g + u), next block's operands prefetched
     {
-      int first = MB, last = 0;
+      int first = MB;
 #pragma unroll
       for (int j = 0; j < G::RT; ++j) {
         const int rt = wr + G::WR * j;
-        if (rt < MB) { first = rt < first ? rt : first; last = rt; }
+        if (rt < MB) first = rt < first ? rt : first;
       }
 #pragma unroll
       for (int j = 0; j < G::RT; ++j)
 #pragma unroll
         for (int q = 0; q < G::CT; ++q) acc[j][q] = f64x4{0.0, 0.0, 0.0, 0.0};
-      (void)last;
-
-      for (int s = 4 * first; s < 4 * MB; ++s) {
-        const int m = 4 * s + g;
-        double bq[G::CT];
+      double an[G::RT][4];
+      auto load_blk = [&](int kb, double (&dst)[G::RT][4]) {
 #pragma unroll
-        for (int q = 0; q < G::CT; ++q) bq[q] = (double)dAl[m * TW + 16 * (wc * G::CT + q) + c];
+        for (int u = 0; u < 4; ++u) {
+          const int m = 16 * kb + 4 * g + u;
+          const double* row = Linv + (size_t)(m < M ? m : 0) * M;
 #pragma unroll
-        for (int j = 0; j < G::RT; ++j) {
-          const int rt = wr + G::WR * j;
-          if (rt < MB && s >= 4 * rt) {
+          for (int j = 0; j < G::RT; ++j) {
+            const int rt = wr + G::WR * j;
             const int p = 16 * rt + c;
-            const double a = (m < M && p < M) ? Linv[(size_t)m * M + p] : 0.0;
+            dst[j][u] = (rt < MB && kb >= rt && m < M && p < M) ? row[p] : 0.0;
+          }
+        }
+      };
+      load_blk(first, an);
+      for (int kb = first; kb < MB; ++kb) {
+        double a[G::RT][4];
 #pragma unroll
-            for (int q = 0; q < G::CT; ++q) acc[j][q] = mfma64(a, bq[q], acc[j][q]);
+        for (int j = 0; j < G::RT; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) a[j][u] = an[j][u];
+        if (kb + 1 < MB) load_blk(kb + 1, an);
+        float bf[G::CT][4];
+#pragma unroll
+        for (int q = 0; q < G::CT; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) bf[q][u] = dAl[(16 * kb + 4 * g + u) * TW + 16 * (wc * G::CT + q) + c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int j = 0; j < G::RT; ++j) {
+            const int rt = wr + G::WR * j;
+            if (rt < MB && kb >= rt) {
+#pragma unroll
+              for (int q = 0; q < G::CT; ++q) acc[j][q] = mfma64(a[j][u], (double)bf[q][u], acc[j][q]);
+            }
           }
         }
       }
@@ -817,21 +854,52 @@ gpk_dlinv_kernel(const float* __restrict__ dA, const float* __restrict__ Kz, int
   const long long c0 = (long long)split * cols_per_split;
   long long c1 = c0 + cols_per_split;
   c1 = c1 < BN ? c1 : BN;
+  const bool vec = (BN & 3) == 0;   // 16-B loads need 16-B aligned rows
   f64x4 acc[2][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int v = 0; v < 2; ++v) acc[u][v] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // each thread stages 2 x 4 consecutive columns of one row of each operand per step:
+  // e = tid + 256 h (h = 0, 1) -> row e / 8, columns 4 (e % 8) .. +3
+  float4 ra[2], rb[2];
+  auto load = [&](long long cb, float4 (&xa)[2], float4 (&xb)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + 256 * h, rr = e >> 3, k4 = 4 * (e & 7);
+      const long long col = cb + k4;
+      float4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
+      if (vec && col + 3 < c1) {
+        if (m0 + rr < M) va = *(const float4*)&dA[(size_t)(m0 + rr) * BN + col];
+        if (p0 + rr < M) vb = *(const float4*)&Kz[(size_t)(p0 + rr) * BN + col];
+      } else {
+        float ta[4], tb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool ok = col + u < c1;
+          ta[u] = (ok && m0 + rr < M) ? dA[(size_t)(m0 + rr) * BN + col + u] : 0.f;
+          tb[u] = (ok && p0 + rr < M) ? Kz[(size_t)(p0 + rr) * BN + col + u] : 0.f;
+        }
+        va = float4{ta[0], ta[1], ta[2], ta[3]};
+        vb = float4{tb[0], tb[1], tb[2], tb[3]};
+      }
+      xa[h] = va;
+      xb[h] = vb;
+    }
+  };
+  load(c0, ra, rb);
   for (long long cb = c0; cb < c1; cb += DLKC) {
-    __syncthreads();
-    for (int e = tid; e < 64 * DLKC; e += 256) {
-      const int rr = e / DLKC, kk = e - rr * DLKC;
-      const long long col = cb + kk;
-      const bool okc = col < c1;
-      sa[rr * DLST + kk] = (m0 + rr < M && okc) ? dA[(size_t)(m0 + rr) * BN + col] : 0.f;
-      sb[rr * DLST + kk] = (p0 + rr < M && okc) ? Kz[(size_t)(p0 + rr) * BN + col] : 0.f;
+    __syncthreads();  // previous step's MFMA operand reads are done
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + 256 * h, rr = e >> 3, k4 = 4 * (e & 7);
+      *(float2*)&sa[rr * DLST + k4] = float2{ra[h].x, ra[h].y};
+      *(float2*)&sa[rr * DLST + k4 + 2] = float2{ra[h].z, ra[h].w};
+      *(float2*)&sb[rr * DLST + k4] = float2{rb[h].x, rb[h].y};
+      *(float2*)&sb[rr * DLST + k4 + 2] = float2{rb[h].z, rb[h].w};
     }
     __syncthreads();
+    if (cb + DLKC < c1) load(cb + DLKC, ra, rb);   // next step's loads overlap the MFMAs
 #pragma unroll
     for (int k = 0; k < DLKC / 4; ++k) {
       double a[2], bb[2];
@@ -858,30 +926,50 @@ gpk_dlinv_kernel(const float* __restrict__ dA, const float* __restrict__ Kz, int
       }
 }
 
-// Fixed-order reductions: (a) the per-workgroup adjoint partials (fp64 sums),
-// (b) the split-K dL^{-1} partials -> dLinv (M x M, upper zero).
+// Fixed-order reductions, 32 outputs per workgroup, 8 lanes per output each summing
+// every 8th partial, then the 8 lane sums in a fixed order (fp64):
+//   (a) the per-workgroup adjoint partials -> tot (P doubles);
+//   (b) the split-K dL^{-1} partials -> dLinv (M x M, upper zero).
 __global__ void __launch_bounds__(256)
 gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __restrict__ tot,
                    const double* __restrict__ dlpart, int nsplit, int ntiles, int M,
                    double* __restrict__ dLinv) {
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e < P) {
-    double s = 0.0;
-    for (int q = 0; q < nwg; ++q) s += (double)wspart[(size_t)q * P + e];
-    tot[e] = s;
-    return;
-  }
-  const long long f = e - P;
-  if (f >= (long long)M * M) return;
-  const int m = (int)(f / M), p = (int)(f - (long long)m * M);
+  __shared__ double red[8][33];
+  const int tid = threadIdx.x, o = tid & 31, q0 = tid >> 5;
+  const int nblk_a = (P + 31) / 32;
   double s = 0.0;
-  if (p <= m) {
-    const int ti = m >> 6, tj = p >> 6;
-    const int tile = ti * (ti + 1) / 2 + tj;
-    const int o = (m & 63) * 64 + (p & 63);
-    for (int q = 0; q < nsplit; ++q) s += dlpart[((size_t)q * ntiles + tile) * 4096 + o];
+  long long out;
+  if ((int)blockIdx.x < nblk_a) {
+    out = (long long)blockIdx.x * 32 + o;
+    if (out < P) {
+#pragma unroll 4
+      for (int q = q0; q < nwg; q += 8) s += (double)wspart[(size_t)q * P + out];
+    }
+  } else {
+    out = (long long)(blockIdx.x - nblk_a) * 32 + o;
+    if (out < (long long)M * M) {
+      const int m = (int)(out / M), p = (int)(out - (long long)m * M);
+      if (p <= m) {
+        const int ti = m >> 6, tj = p >> 6;
+        const int tile = ti * (ti + 1) / 2 + tj;
+        const int off = (m & 63) * 64 + (p & 63);
+#pragma unroll 4
+        for (int q = q0; q < nsplit; q += 8) s += dlpart[((size_t)q * ntiles + tile) * 4096 + off];
+      }
+    }
   }
-  dLinv[f] = s;
+  red[q0][o] = s;
+  __syncthreads();
+  if (q0 == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += red[q][o];
+    if ((int)blockIdx.x < nblk_a) {
+      if (out < P) tot[out] = t;
+    } else if (out < (long long)M * M) {
+      dLinv[out] = t;
+    }
+  }
 }
 
 // Outputs from the reduced totals (one workgroup):
@@ -1048,8 +1136,8 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
                      a.M, p.BN, p.ntiles, p.cols_per_split, dl);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const long long nred = (long long)p.P + (long long)a.M * a.M;
-  hipLaunchKernelGGL(gpk_var_red_kernel, dim3((unsigned)((nred + 255) / 256)), dim3(256), 0, stream,
+  const long long nred = (p.P + 31) / 32 + ((long long)a.M * a.M + 31) / 32;
+  hipLaunchKernelGGL(gpk_var_red_kernel, dim3((unsigned)nred), dim3(256), 0, stream,
                      wspart, p.nwg, p.P, tot, dl, p.nsplit, p.ntiles, a.M, a.dLinv);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;

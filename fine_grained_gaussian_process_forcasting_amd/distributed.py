@@ -81,21 +81,30 @@ def allreduce_shared_grads(params, group=None, scale: float = 1.0) -> Optional[t
 
 
 class ObjectiveAccumulator:
-    """Per-step objective partials kept on the device and reduced across ranks with ONE
-    all-reduce for many steps (the per-step value is only logged): no collective sits
-    on the critical path of a step, which matters at 64 windows per GPU."""
+    """Per-step objective values kept on the device and reduced across ranks with ONE
+    all-reduce for many steps (the per-step value is only logged): no collective and no
+    extra launch sits on the critical path of a step, which matters at 64 windows per
+    GPU. ``slot()`` hands the kernel a (B,) row to write its per-window
+    objective into; ``add()`` stores an already-reduced scalar instead."""
 
-    def __init__(self, steps: int, device, group=None):
-        self.buf = torch.zeros(max(1, steps), dtype=torch.float64, device=device)
+    def __init__(self, steps: int, device, group=None, width: int = 1):
+        self.rows = torch.zeros(max(1, steps), width, dtype=torch.float32, device=device)
         self.n = 0
         self.group = group
 
+    def slot(self) -> torch.Tensor:
+        r = self.rows[self.n]
+        self.n += 1
+        return r
+
     def add(self, partial: torch.Tensor) -> None:
-        self.buf[self.n].copy_(partial.detach().reshape(()).to(torch.float64))
+        self.rows[self.n, :1].copy_(partial.detach().reshape(1).to(self.rows.dtype))
         self.n += 1
 
     def reduce(self, async_op: bool = False):
+        """(per-step sums over the rows, fp64, summed over ranks; work handle or None)."""
+        tot = self.rows[:self.n].sum(1, dtype=torch.float64)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
-            work = dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
-            return self.buf[:self.n], work
-        return self.buf[:self.n], None
+            work = dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            return tot, work
+        return tot, None

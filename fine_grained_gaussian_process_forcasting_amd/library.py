@@ -1,0 +1,195 @@
+"""torch.library registration of the gfx950 GP kernels (namespace ``gpk``).
+
+SURVEY.md §8b ("Who calls it"): the model classes reach the kernels through
+``torch.library`` custom ops with registered autograd formulas, so the ops are visible
+to the dispatcher (FakeTensor shape propagation, ``torch.library.opcheck``, tracing)
+instead of being opaque Python. Each op is one C-ABI call of include/gpk.h on
+``torch.cuda.current_stream()`` (ops.py); nothing here computes on the CPU.
+
+  gpk::exact_mll(X, y, hyper, jitter, max_tries) -> (mll, L, z, info)         [autograd]
+  gpk::exact_mll_grad(X, L, z, hyper, gout) -> (dX, dy, dhyp)
+  gpk::kzz_factor(Z, s2, ls, jitter, chol_jitter, max_tries) -> (Linv, L, info) [autograd]
+  gpk::variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter) -> (mean, var, flags)
+                                                                               [autograd]
+  gpk::variational_adj(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter, gmean, gvar)
+      -> (dX, dLinv, dZ, dvmean, dvstd, ds2, dls, dw, db0)
+
+Reference call sites they serve: GPModel.py:10-13 + ExactMarginalLogLikelihood
+(exact_mll), DeepGP.py:33-73 VariationalStrategy (kzz_factor, variational_fwd), and
+the backward of train.py:166 (the *_grad / *_adj ops).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+from torch import Tensor
+
+from . import ops
+
+# ---------------------------------------------------------------------------
+# exact GP marginal log likelihood (gpk_exact_mll_f32 / gpk_exact_mll_grad_f32)
+# ---------------------------------------------------------------------------
+
+
+@torch.library.custom_op("gpk::exact_mll", mutates_args=(), device_types="cuda")
+def exact_mll(X: Tensor, y: Tensor, hyper: Tensor, jitter: float, max_tries: int,
+              want_factor: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """want_factor=False (no gradient needed) skips writing L and z (empty outputs)."""
+    out = ops.exact_mll(X, y, None, None, None, None, jitter=jitter, max_tries=max_tries,
+                        want_L=want_factor, want_z=want_factor, hyper=hyper)
+    if not want_factor:
+        return out.mll, X.new_empty(0), X.new_empty(0), out.info
+    return out.mll, out.L, out.z, out.info
+
+
+@exact_mll.register_fake
+def _(X, y, hyper, jitter, max_tries, want_factor):
+    B, N, _ = X.shape
+    if not want_factor:
+        return X.new_empty(B), X.new_empty(0), X.new_empty(0), X.new_empty(B, dtype=torch.int32)
+    return (X.new_empty(B), X.new_empty(B, N, N), X.new_empty(B, N),
+            X.new_empty(B, dtype=torch.int32))
+
+
+@torch.library.custom_op("gpk::exact_mll_grad", mutates_args=(), device_types="cuda")
+def exact_mll_grad(X: Tensor, L: Tensor, z: Tensor, hyper: Tensor,
+                   gout: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    g = ops.exact_mll_grad(X, L, z, hyper, gout)
+    return g.dX, g.dy, g.dhyp
+
+
+@exact_mll_grad.register_fake
+def _(X, L, z, hyper, gout):
+    B, N, D = X.shape
+    return X.new_empty(B, N, D), X.new_empty(B, N), X.new_empty(B, hyper.numel())
+
+
+def _exact_setup(ctx, inputs, output):
+    X, y, hyper, jitter, max_tries, want_factor = inputs
+    mll, L, z, info = output
+    ctx.save_for_backward(X, L, z, hyper)
+    ctx.mark_non_differentiable(L, z, info)
+
+
+def _exact_backward(ctx, gmll, _gL, _gz, _ginfo):
+    X, L, z, hyper = ctx.saved_tensors
+    if L.numel() == 0:
+        raise RuntimeError("gpk::exact_mll was called with want_factor=False; no backward")
+    dX, dy, dhyp = torch.ops.gpk.exact_mll_grad(X, L, z, hyper, gmll.contiguous())
+    return dX, dy, dhyp.sum(0), None, None, None
+
+
+exact_mll.register_autograd(_exact_backward, setup_context=_exact_setup)
+
+# ---------------------------------------------------------------------------
+# shared K_ZZ factor (gpk_kzz_chol_f64) + its M x M adjoint (ops.kzz_backward)
+# ---------------------------------------------------------------------------
+
+
+@torch.library.custom_op("gpk::kzz_factor", mutates_args=(), device_types="cuda")
+def kzz_factor(Z: Tensor, s2: Tensor, ls: Tensor, jitter: float, chol_jitter: float,
+               max_tries: int) -> Tuple[Tensor, Tensor, Tensor]:
+    D = Z.shape[-1]
+    lsv = ls.detach().reshape(-1).expand(D).contiguous().float()
+    kz = ops.kzz_cholesky(Z.detach(), None, None, jitter=jitter, chol_jitter=chol_jitter,
+                          max_tries=max_tries, hyper=torch.cat([s2.detach().reshape(1).float(), lsv]))
+    return kz.Linv, kz.L, kz.info
+
+
+@kzz_factor.register_fake
+def _(Z, s2, ls, jitter, chol_jitter, max_tries):
+    M = Z.shape[0]
+    return (Z.new_empty(M, M, dtype=torch.float64), Z.new_empty(M, M, dtype=torch.float64),
+            Z.new_empty(1, dtype=torch.int32))
+
+
+def _kzz_setup(ctx, inputs, output):
+    Z, s2, ls = inputs[:3]
+    Linv, L, info = output
+    ctx.save_for_backward(Z, s2, ls, L, Linv)
+    ctx.mark_non_differentiable(L, info)
+
+
+def _kzz_backward(ctx, dLinv, _dL, _dinfo):
+    Z, s2, ls, L, Linv = ctx.saved_tensors
+    if dLinv is None:
+        return None, None, None, None, None, None
+    dZ, ds2, dls = ops.kzz_backward(dLinv, L, Linv, Z, s2, ls)
+    dls_out = dls.sum().reshape(ls.shape) if ls.numel() == 1 else dls.reshape(ls.shape)
+    return (dZ.to(Z.dtype), ds2.reshape(s2.shape).to(s2.dtype), dls_out.to(ls.dtype),
+            None, None, None)
+
+
+kzz_factor.register_autograd(_kzz_backward, setup_context=_kzz_setup)
+
+# ---------------------------------------------------------------------------
+# variational predictive distribution (gpk_variational_f32 / gpk_variational_adjoint_f32)
+# ---------------------------------------------------------------------------
+
+
+def _var_hyper(x, s2, ls, w, b0, jitter):
+    D = x.shape[-1]
+    lsv = ls.detach().reshape(-1).expand(D).contiguous().float()
+    return ops.pack_variational_hyper(s2.detach(), 1.0, jitter, b0.detach(), w.detach(), lsv, D, x.device)
+
+
+@torch.library.custom_op("gpk::variational_fwd", mutates_args=(), device_types="cuda")
+def variational_fwd(x: Tensor, Linv: Tensor, Z: Tensor, vmean: Tensor, vstd: Tensor, s2: Tensor,
+                    ls: Tensor, w: Tensor, b0: Tensor, jitter: float) -> Tuple[Tensor, Tensor, Tensor]:
+    out = ops.variational_forward(x, Z, Linv, vmean, vstd, hyper=_var_hyper(x, s2, ls, w, b0, jitter))
+    return out.mean, out.var, out.flags
+
+
+@variational_fwd.register_fake
+def _(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter):
+    B, N, _ = x.shape
+    return x.new_empty(B, N), x.new_empty(B, N), x.new_empty(1, dtype=torch.int32)
+
+
+@torch.library.custom_op("gpk::variational_adj", mutates_args=(), device_types="cuda")
+def variational_adj(x: Tensor, Linv: Tensor, Z: Tensor, vmean: Tensor, vstd: Tensor, s2: Tensor,
+                    ls: Tensor, w: Tensor, b0: Tensor, jitter: float, gmean: Tensor,
+                    gvar: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor,
+                                           Tensor, Tensor]:
+    B, N, D = x.shape
+    adj = ops.variational_adjoint(x, Z, Linv, vmean, vstd, _var_hyper(x, s2, ls, w, b0, jitter),
+                                  gmean, gvar)
+    gm = gmean.reshape(B * N).float()
+    dw = x.detach().reshape(B * N, D).float().transpose(0, 1) @ gm     # LinearMean weights
+    db0 = gm.sum()
+    dls = adj.dls.sum().reshape(ls.shape) if ls.numel() == 1 else adj.dls.reshape(ls.shape)
+    return (adj.dX.to(x.dtype), adj.dLinv, adj.dZ.to(Z.dtype),
+            adj.dvmean.reshape(vmean.shape).to(vmean.dtype).clone(),
+            adj.dvstd.reshape(vstd.shape).to(vstd.dtype).clone(),
+            adj.ds2.reshape(s2.shape).to(s2.dtype).clone(), dls.to(ls.dtype).clone(),
+            dw.reshape(w.shape).to(w.dtype), db0.reshape(b0.shape).to(b0.dtype))
+
+
+@variational_adj.register_fake
+def _(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter, gmean, gvar):
+    return (torch.empty_like(x), torch.empty_like(Linv), torch.empty_like(Z), torch.empty_like(vmean),
+            torch.empty_like(vstd), torch.empty_like(s2), torch.empty_like(ls), torch.empty_like(w),
+            torch.empty_like(b0))
+
+
+def _var_setup(ctx, inputs, output):
+    x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter = inputs
+    ctx.jitter = jitter
+    ctx.save_for_backward(x, Linv, Z, vmean, vstd, s2, ls, w, b0)
+    ctx.mark_non_differentiable(output[2])
+
+
+def _var_backward(ctx, gmean, gvar, _gflags):
+    x, Linv, Z, vmean, vstd, s2, ls, w, b0 = ctx.saved_tensors
+    B, N, _ = x.shape
+    if gmean is None:
+        gmean = x.new_zeros(B, N)
+    if gvar is None:
+        gvar = x.new_zeros(B, N)
+    grads = torch.ops.gpk.variational_adj(x, Linv, Z, vmean, vstd, s2, ls, w, b0, ctx.jitter,
+                                          gmean.contiguous(), gvar.contiguous())
+    return (*grads, None)
+
+
+variational_fwd.register_autograd(_var_backward, setup_context=_var_setup)

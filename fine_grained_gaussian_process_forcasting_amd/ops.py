@@ -52,7 +52,8 @@ class ExactMLLOut:
 
 def exact_mll(X: torch.Tensor, y: torch.Tensor, lengthscale, outputscale, mean_constant, noise,
               jitter: float = 1e-6, max_tries: int = 3, want_L: bool = True,
-              want_z: bool = False, hyper: Optional[torch.Tensor] = None) -> ExactMLLOut:
+              want_z: bool = False, hyper: Optional[torch.Tensor] = None,
+              mll_out: Optional[torch.Tensor] = None, info_out: Optional[torch.Tensor] = None) -> ExactMLLOut:
     """Fused exact-GP log marginal likelihood per window (one gfx950 kernel launch).
 
     X: (B, N, D) float32, y: (B, N) float32 on the same ROCm device. ``lengthscale``
@@ -73,8 +74,14 @@ def exact_mll(X: torch.Tensor, y: torch.Tensor, lengthscale, outputscale, mean_c
     n_ls = hyper.numel() - 3
     if n_ls not in (1, D):
         raise ValueError(f"lengthscale must have 1 or D={D} entries, got {n_ls}")
-    mll = torch.empty(B, device=dev, dtype=torch.float32)
-    info = torch.empty(B, device=dev, dtype=torch.int32)
+    if mll_out is not None and (mll_out.shape != (B,) or mll_out.dtype != torch.float32
+                                or not mll_out.is_contiguous() or mll_out.device != dev):
+        raise ValueError("mll_out must be a contiguous (B,) float32 tensor on X's device")
+    if info_out is not None and (info_out.shape != (B,) or info_out.dtype != torch.int32
+                                 or not info_out.is_contiguous() or info_out.device != dev):
+        raise ValueError("info_out must be a contiguous (B,) int32 tensor on X's device")
+    mll = mll_out if mll_out is not None else torch.empty(B, device=dev, dtype=torch.float32)
+    info = info_out if info_out is not None else torch.empty(B, device=dev, dtype=torch.int32)
     L = torch.empty(B, N, N, device=dev, dtype=torch.float32) if want_L else None
     z = torch.empty(B, N, device=dev, dtype=torch.float32) if want_z else None
     rc = _native.lib().gpk_exact_mll_f32(

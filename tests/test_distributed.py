@@ -85,6 +85,11 @@ def _grad_worker(rank, world, port, q):
     acc = ObjectiveAccumulator(3, "cpu")
     for k in range(3):
         acc.add(torch.tensor(float(rank + k)))
+    rows = ObjectiveAccumulator(2, "cpu", width=3)
+    for k in range(2):
+        rows.slot().copy_(torch.tensor([1.0, 2.0, float(rank + k)]))
+    rv, rw = rows.reduce()
+    ok = ok and rv.tolist() == [6.0 + 1.0, 6.0 + 3.0]
     vals, work = acc.reduce(async_op=True)
     work.wait()
     q.put((rank, ok, vals.tolist()))

@@ -111,3 +111,26 @@ def test_grad_entry_validation_without_device():
     assert lib.gpk_exact_mll_grad_f32(*bad) == -13
     bad = list(args); bad[5] = 0
     assert lib.gpk_exact_mll_grad_f32(*bad) == 0   # B = 0: nothing to do
+
+
+def test_custom_ops_registered_with_fake_and_autograd():
+    """The kernels are torch.library custom ops (SURVEY §8b "Who calls it"): schemas,
+    FakeTensor impls (shape propagation without a GPU) and autograd formulas."""
+    import fine_grained_gaussian_process_forcasting_amd.library  # noqa: F401
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    names = ["exact_mll", "exact_mll_grad", "kzz_factor", "variational_fwd", "variational_adj"]
+    for n in names:
+        assert hasattr(torch.ops.gpk, n), n
+    with FakeTensorMode():
+        X = torch.empty(3, 16, 4)
+        y = torch.empty(3, 16)
+        h = torch.empty(4)
+        mll, L, z, info = torch.ops.gpk.exact_mll(X, y, h, 1e-6, 3, True)
+        assert mll.shape == (3,) and L.shape == (3, 16, 16) and info.dtype == torch.int32
+        Z = torch.empty(8, 4)
+        Linv, Lz, inf = torch.ops.gpk.kzz_factor(Z, torch.empty(()), torch.empty(4), 1e-4, 1e-8, 3)
+        assert Linv.shape == (8, 8) and Linv.dtype == torch.float64
+        mean, var, flags = torch.ops.gpk.variational_fwd(X, Linv, Z, torch.empty(8), torch.empty(8),
+                                                         torch.empty(()), torch.empty(4), torch.empty(4),
+                                                         torch.empty(()), 1e-4)
+        assert mean.shape == (3, 16) and var.shape == (3, 16) and flags.shape == (1,)
