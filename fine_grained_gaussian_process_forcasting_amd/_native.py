@@ -44,6 +44,8 @@ SIGNATURES = {
                                             c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                             c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p]),
+    "gpk_window_gather_f32": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_void_p, c_int, c_int, c_int,
+                                      c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 DEBUG_SIGNATURES = {
     "gpk_debug_exact_stamps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

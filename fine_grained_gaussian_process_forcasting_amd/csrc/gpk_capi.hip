@@ -132,6 +132,26 @@ int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Li
   return gpk_launch_var_adjoint(a, (hipStream_t)stream);
 }
 
+int gpk_window_gather_f32(const float* table, long long n_rows, int F, const long long* rows, int B,
+                          int T, int n_enc, int pred_len, int target_col, float* enc, float* dec,
+                          float* y, void* stream) {
+  if (table == nullptr) return -1;
+  if (n_rows < 0) return -2;
+  if (F < 1) return -3;
+  if (rows == nullptr && B > 0) return -4;
+  if (B < 0) return -5;
+  if (T < 1) return -6;
+  if (n_enc < 0 || n_enc > T) return -7;
+  if (pred_len < 0 || n_enc + pred_len > T) return -8;
+  if (target_col < 0 || target_col >= F) return -9;
+  if (enc == nullptr && B > 0 && n_enc > 0) return -10;
+  if (dec == nullptr && B > 0 && T - n_enc - pred_len > 0) return -11;
+  if (y == nullptr && B > 0 && pred_len > 0) return -12;
+  if (B == 0) return 0;
+  return gpk_launch_window_gather(table, F, rows, B, n_enc, T - n_enc - pred_len, pred_len,
+                                  target_col, enc, dec, y, (hipStream_t)stream);
+}
+
 // Diagnostic (not part of the product ABI): same as gpk_exact_mll_f32 for N in
 // (240, 256], plus per-workgroup phase clocks (32 x u64 per window) in `stamps`.
 int gpk_debug_exact_stamps(const float* X, const float* y, const float* hyp, int n_lengthscale,

@@ -85,6 +85,16 @@ GPK_DEVICE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier ordering LDS only: unlike __syncthreads() it does not wait for the
+// wave's outstanding global stores (s_waitcnt vmcnt(0)), so result stores and spills
+// stay in flight across the barrier. Only for kernels whose threads never read global
+// data another thread of the same launch wrote.
+GPK_DEVICE void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 GPK_DEVICE float readlane_f(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }

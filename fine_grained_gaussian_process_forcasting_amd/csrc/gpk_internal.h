@@ -83,3 +83,7 @@ int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream);
 size_t gpk_var_adjoint_ws_bytes(int B, int N, int M, int D);
 int gpk_launch_var_adjoint(const GpkVarAdjArgs& a, hipStream_t stream);
 int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream);
+
+int gpk_launch_window_gather(const float* table, int F, const long long* rows, int B, int n_enc,
+                             int n_dec, int pred_len, int tcol, float* enc, float* dec, float* y,
+                             hipStream_t stream);

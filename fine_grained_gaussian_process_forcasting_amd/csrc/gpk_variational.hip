@@ -10,8 +10,8 @@
 //     ELL  = sum_i -0.5 [((y_i - mean_i)^2 + var_i)/noise + log noise + log 2pi]
 //
 // Kernels:
-//   gpk_kzz_kernel      ONE workgroup: K_ZZ of the shared inducing points, blocked fp64
-//                       Cholesky + L^{-1} (32-column blocks, GPyTorch's fp64 ladder). The
+//   gpk_kzz_kernel      ONE workgroup: K_ZZ of the shared inducing points, register-resident
+//                       fp64 Cholesky + L^{-1} (4-column steps, GPyTorch's fp64 ladder). The
 //                       reference factors the same matrix b times (Z expanded over the batch).
 //   gpk_var_fwd_kernel  the per-point work as ONE column-tiled GEMM A = L^{-1} [K_ZX(b=0) | ...]:
 //                       a workgroup owns a chunk of TW points of one window and all M rows of A;
@@ -45,54 +45,135 @@ GPK_DEVICE f32x4 mfma32(float a, float b, f32x4 c) {
 }
 
 // ---------------------------------------------------------------------------
-// Blocked K_ZZ factorisation (one workgroup, 1024 threads, KR = 32-column blocks).
-// K_ZZ (fp32, centred GEMM-form distances as GPyTorch's _sq_dist, + jitter) -> fp64,
-// GPyTorch's cumulative fp64 ladder, L and L^{-1} of [K | I] by blocked elimination:
-//   (1) the KR x KR diagonal block and an identity are eliminated in LDS (one
-//       element per thread, one barrier per column) -> L11, L11^{-1};
-//   (2) V = L11^{-1} [Linv rows k.. (cols < k+KR) | A21^T] in LDS, one column per
-//       thread -> the final rows of L^{-1} and the final L21 (written to L2/HBM);
-//   (3) ONE trailing update of every remaining row i: target[i][c] -= sum_p V[p][i]
-//       V[p][c] (c < k+KR: L^{-1}; k+KR <= c <= i: the Schur complement), 4 x 4
-//       register tiles, lanes along c (coalesced), operands from LDS.
-// M/KR block steps instead of M serial column steps through L2.
+// K_ZZ factorisation on fp64 MFMA tiles (one workgroup of KT = 512 threads).
+// The lower triangle (M padded to Mp = multiple of 16, identity padding) is held as
+// 16 x 16 tiles in v_mfma_f64_16x16x4f64 accumulators (lane (c, g), reg r <-> row
+// g + 4r, column c), NS tiles per wave for the whole factorisation (Mp = 256: 136
+// tiles, 17 per wave, 136 VGPRs). Step s eliminates columns j0 = 4s .. j0+3:
+//   publish  the owners of tile column j0/16 write those 4 columns (rows >= j0) to LDS;
+//   panel    every thread factors the 4 x 4 pivot block redundantly (hardware rsq / rcp
+//            + Newton steps; GPyTorch's fp64 ladder restarts with more jitter on a
+//            non-positive pivot); one thread per row forms l_i = P_i L4^-T -> LDS and
+//            writes the final L entries;
+//   update   every tile right of the panel takes A -= l_rows l_cols^T: ONE f64 MFMA
+//            (rank 4 = the instruction's k) with both operands read from LDS.
+// Then the same tiles, reset to I, run the forward elimination of [L | I] 4 rows per
+// step (X -= L[:, panel] X_panel, again one MFMA per tile) -> L^{-1}.
 // ---------------------------------------------------------------------------
-constexpr int KR = 32;
+constexpr int KT = 512;   // 8 waves
 
-__global__ void __launch_bounds__(1024)
+GPK_DEVICE double rsq64(double x) {   // 1/sqrt(x), x > 0: hardware estimate + 2 Newton steps
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * (1.5 - 0.5 * x * y * y);
+  y = y * (1.5 - 0.5 * x * y * y);
+  return y;
+}
+GPK_DEVICE double rcp64(double x) {   // 1/x: hardware estimate + 2 Newton steps
+  double y = __builtin_amdgcn_rcp(x);
+  y = y * (2.0 - x * y);
+  y = y * (2.0 - x * y);
+  return y;
+}
+
+// 4 x 4 lower Cholesky l of the symmetric d and li = l^{-1}; false on a non-positive /
+// NaN pivot (bad = its column)
+GPK_DEVICE bool chol4(const double (&d)[4][4], double (&l)[4][4], double (&li)[4][4], int& bad) {
+  double rd[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double sm = d[j][j];
+#pragma unroll
+    for (int q = 0; q < j; ++q) sm -= l[j][q] * l[j][q];
+    if (!(sm > 0.0)) { bad = j; return false; }
+    const double r = rsq64(sm);
+    l[j][j] = sm * r;
+    rd[j] = r;
+#pragma unroll
+    for (int i = j + 1; i < 4; ++i) {
+      double t = d[i][j];
+#pragma unroll
+      for (int q = 0; q < j; ++q) t -= l[i][q] * l[j][q];
+      l[i][j] = t * r;
+    }
+#pragma unroll
+    for (int i = 0; i < j; ++i) l[i][j] = 0.0;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (r < c) { li[r][c] = 0.0; continue; }
+      double v = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int q = c; q < r; ++q) v -= l[r][q] * li[q][c];
+      li[r][c] = v * rd[r];
+    }
+  return true;
+}
+
+GPK_DEVICE void tri_of(int t, int& it, int& jt) {   // lower tiles row-major: row it holds 0..it
+  int r = (int)((__builtin_sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  while (r * (r + 1) / 2 > t) --r;
+  it = r;
+  jt = t - r * (r + 1) / 2;
+}
+
+template <int NS>
+__global__ void __launch_bounds__(KT, 1)
 gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
                float jitter_var, double jitter_chol, int max_tries, double* __restrict__ L,
                double* __restrict__ Linv, int* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) float vsm[];
-  const int Mp = (M + 3) & ~3;
-  double* V = (double*)vsm;                  // KR x Mp
-  double* dg = V + KR * Mp;                  // KR x 2KR  [A11 | I] elimination
-  double* li = dg + KR * 2 * KR;             // KR x KR   L11^{-1}
-  float* zt = (float*)(li + KR * KR);        // M x D     Z / l, centred
-  float* zn = zt + M * D;                    // M
-  float* cm = zn + M;                        // D
-  const int tid = threadIdx.x, T = blockDim.x;
+  const int Mp = (M + 15) & ~15;
+  double* P = (double*)vsm;            // Mp x 4  panel columns (phase 1) / L panel (phase 2)
+  double* lb = P + Mp * 4;             // Mp x 4  l rows (phase 1) / X_k as 4 x Mp (phase 2)
+  double* xr = lb + Mp * 4;            // 4 x Mp  published X rows (phase 2)
+  const int D4 = (D + 3) & ~3;
+  float* zt = (float*)(xr + Mp * 4);   // M x D4  Z / l, centred (zero padded)
+  float* zn = zt + M * D4;             // M
+  float* cm = zn + M;                  // D
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float s2 = hyp[0];
   const float* ls = hyp + 1;
 
-  for (int e = tid; e < M * D; e += T) zt[e] = Z[e] / ls[e % D];
-  __syncthreads();
-  for (int d = tid; d < D; d += T) {
-    float s = 0.f;
-    for (int m = 0; m < M; ++m) s += zt[m * D + d];
-    cm[d] = s / (float)M;
+  for (int e = tid; e < M * D4; e += KT) {
+    const int m = e / D4, d = e - m * D4;
+    zt[e] = d < D ? Z[m * D + d] / ls[d] : 0.f;
   }
-  __syncthreads();
-  for (int e = tid; e < M * D; e += T) zt[e] -= cm[e % D];
-  __syncthreads();
-  for (int m = tid; m < M; m += T) {
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) s = __builtin_fmaf(zt[m * D + d], zt[m * D + d], s);
-    zn[m] = s;
+  for (int e = tid; e < Mp * 4; e += KT) { lb[e] = 0.0; P[e] = 0.0; xr[e] = 0.0; }
+  lds_barrier();
+  for (int d = tid; d < D; d += KT) {
+    float sm = 0.f;
+    for (int m = 0; m < M; ++m) sm += zt[m * D4 + d];
+    cm[d] = sm / (float)M;
   }
-  __syncthreads();
+  lds_barrier();
+  for (int e = tid; e < M * D4; e += KT) {
+    const int d = e % D4;
+    if (d < D) zt[e] -= cm[d];
+  }
+  lds_barrier();
+  for (int m = tid; m < M; m += KT) {
+    float sm = 0.f;
+    for (int d = 0; d < D; ++d) sm = __builtin_fmaf(zt[m * D4 + d], zt[m * D4 + d], sm);
+    zn[m] = sm;
+  }
+  lds_barrier();
 
-  const int jr = tid >> 5, jc = tid & 31;  // (row, column) of this thread in a KR x KR block
+  const int T16 = Mp >> 4;
+  const int ntile = T16 * (T16 + 1) / 2;
+  int its[NS], jts[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const int t = wave + 8 * q;
+    int it = T16, jt = T16;   // no tile: coordinates past the end (skipped everywhere)
+    if (t < ntile) tri_of(t, it, jt);
+    its[q] = __builtin_amdgcn_readfirstlane(it);
+    jts[q] = __builtin_amdgcn_readfirstlane(jt);
+  }
+  f64x4 acc[NS];
   int status = 0;
   for (int attempt = 0; attempt <= max_tries; ++attempt) {
     double ladder = 0.0;  // GPyTorch adds (jitter_new - jitter_prev) cumulatively
@@ -105,127 +186,179 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
         p10 *= 10.0;
       }
     }
-    for (int e = tid; e < M * M; e += T) {
-      const int i = e / M, j = e - i * M;
-      double a = 0.0;
-      if (j <= i) {
-        float dot = 0.f;
-        for (int d = 0; d < D; ++d) dot = __builtin_fmaf(zt[i * D + d], zt[j * D + d], dot);
-        float dist = zn[i] + zn[j] - 2.f * dot;
-        dist = dist < 0.f ? 0.f : dist;
-        float kv = s2 * __expf(-0.5f * dist);
-        if (i == j) kv = kv + jitter_var;
-        a = (double)kv;
-        if (i == j) a += ladder;
+    // K_ZZ tiles (fp32 arithmetic as the reference's kernel, + jitter, -> fp64 + ladder)
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
+      const int j = 16 * jts[q] + c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * its[q] + g + 4 * r;
+        double v = (i == j) ? 1.0 : 0.0;
+        if (its[q] < T16 && i < M && j < M) {
+          float dot = 0.f;
+          for (int d = 0; d < D4; d += 4) {
+            const float4 zi = *(const float4*)&zt[i * D4 + d];
+            const float4 zj = *(const float4*)&zt[j * D4 + d];
+            dot = __builtin_fmaf(zi.x, zj.x, dot);
+            dot = __builtin_fmaf(zi.y, zj.y, dot);
+            dot = __builtin_fmaf(zi.z, zj.z, dot);
+            dot = __builtin_fmaf(zi.w, zj.w, dot);
+          }
+          float dist = zn[i] + zn[j] - 2.f * dot;
+          dist = dist < 0.f ? 0.f : dist;
+          float kv = s2 * __expf(-0.5f * dist);
+          if (i == j) kv = kv + jitter_var;
+          v = (double)kv;
+          if (i == j) v += ladder;
+        }
+        acc[q][r] = v;
       }
-      L[e] = a;
-      Linv[e] = (i == j) ? 1.0 : 0.0;
     }
-    __syncthreads();
-
     int failed = 0;
-    for (int k = 0; k < M && !failed; k += KR) {
-      const int r = M - k < KR ? M - k : KR;
-      // (1) diagonal block, symmetric fill from the lower storage, identity padding
-      {
-        double a;
-        if (jr < r && jc < r) {
-          const int hi = jr > jc ? jr : jc, lo = jr > jc ? jc : jr;
-          a = L[(size_t)(k + hi) * M + k + lo];
-        } else {
-          a = (jr == jc) ? 1.0 : 0.0;
-        }
-        dg[jr * 2 * KR + jc] = a;
-        dg[jr * 2 * KR + KR + jc] = (jr == jc) ? 1.0 : 0.0;
-      }
-      __syncthreads();
-      for (int j = 0; j < r; ++j) {
-        const double piv = dg[j * 2 * KR + j];
-        if (!(piv > 0.0)) { failed = k + j + 1; break; }  // uniform (same LDS word)
-        if (jr > j) {
-          const double f = dg[jr * 2 * KR + j] / piv;
-          if (jc > j) dg[jr * 2 * KR + jc] -= f * dg[j * 2 * KR + jc];
-          if (jc <= j) dg[jr * 2 * KR + KR + jc] -= f * dg[j * 2 * KR + KR + jc];
-        }
-        __syncthreads();
-      }
-      if (failed) break;
-      {
-        const double s = 1.0 / __builtin_sqrt(dg[jr * 2 * KR + jr]);
-        // L11[jc][jr] = U[jr][jc] / sqrt(d_jr) for jc >= jr
-        if (jr < r && jc < r && jc >= jr) L[(size_t)(k + jc) * M + k + jr] = dg[jr * 2 * KR + jc] * s;
-        li[jr * KR + jc] = (jr < r && jc <= jr) ? dg[jr * 2 * KR + KR + jc] * s : 0.0;
-      }
-      // (2) stage V = [Linv rows k..k+r (cols < k+r) | A21^T]
-      for (int e = tid; e < KR * M; e += T) {
-        const int p = e / M, c = e - p * M;
-        double v = 0.0;
-        if (p < r) v = c < k + r ? Linv[(size_t)(k + p) * M + c] : L[(size_t)c * M + k + p];
-        V[p * Mp + c] = v;
-      }
-      __syncthreads();
-      for (int c = tid; c < M; c += T) {
-        double vin[KR];
+    for (int s = 0; s < (Mp >> 2); ++s) {
+      const int j0 = 4 * s, jt0 = s >> 2, sub = s & 3;
+      // opaque tile coordinates: the compiler must not hoist every tile's derived LDS
+      // addresses out of the step loop (they would cost more registers than the tiles)
 #pragma unroll
-        for (int p = 0; p < KR; ++p) vin[p] = V[p * Mp + c];
+      for (int q = 0; q < NS; ++q) asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
+      // publish columns j0..j0+3 (tile column jt0, columns 4 sub .. 4 sub + 3), rows >= j0
 #pragma unroll
-        for (int j = 0; j < KR; ++j) {
-          double acc = 0.0;
+      for (int q = 0; q < NS; ++q) {
+        if (jts[q] == jt0 && (c >> 2) == sub) {
 #pragma unroll
-          for (int p = 0; p <= j; ++p) acc = __builtin_fma(li[j * KR + p], vin[p], acc);
-          V[j * Mp + c] = acc;
-          if (j < r) {
-            if (c < k + r) Linv[(size_t)(k + j) * M + c] = acc;
-            else L[(size_t)c * M + k + j] = acc;
+          for (int r = 0; r < 4; ++r) {
+            const int i = 16 * its[q] + g + 4 * r;
+            if (i >= j0) P[i * 4 + (c & 3)] = acc[q][r];
           }
         }
       }
-      __syncthreads();
-      // (3) trailing update of rows k+r .. M-1
-      const int i0 = k + r;
-      const int nrt = (M - i0 + 3) >> 2, nct = Mp >> 2;
-      for (int t = tid; t < nrt * nct; t += T) {
-        const int rt = t / nct, ct = t - rt * nct;
-        const int ib = i0 + 4 * rt, cb = 4 * ct;
-        if (cb > ib + 3) continue;  // tile entirely above the diagonal
-        double acc[4][4];
+      lds_barrier();
+      double dd[4][4], l4[4][4], l4i[4][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int w = 0; w < 4; ++w) acc[u][w] = 0.0;
-#pragma unroll 8
-        for (int p = 0; p < KR; ++p) {
-          const double* vr = V + p * Mp;
-          double a[4], b[4];
+        for (int t = 0; t < 4; ++t) dd[r][t] = P[(j0 + r) * 4 + t];
+      int bad = 0;
+      if (!chol4(dd, l4, l4i, bad)) {   // uniform: every thread factors the same LDS block
+        failed = j0 + bad + 1;
+        break;
+      }
+      for (int i = j0 + tid; i < Mp; i += KT) {   // l_i = P_i L4^{-T}
+        double p[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) { a[u] = vr[ib + u < Mp ? ib + u : 0]; b[u] = vr[cb + u]; }
+        for (int t = 0; t < 4; ++t) p[t] = P[i * 4 + t];
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+        for (int t = 0; t < 4; ++t) {
+          double v = 0.0;
 #pragma unroll
-            for (int w = 0; w < 4; ++w) acc[u][w] = __builtin_fma(a[u], b[w], acc[u][w]);
-        }
-        double* tgt = cb < i0 ? Linv : L;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = ib + u;
-          if (i >= M) continue;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const int c = cb + w;
-            if (c <= i && c < M) tgt[(size_t)i * M + c] -= acc[u][w];
-          }
+          for (int q = 0; q <= t; ++q) v = __builtin_fma(p[q], l4i[t][q], v);
+          lb[i * 4 + t] = v;
+          if (i < M && j0 + t < M && j0 + t <= i) L[(size_t)i * M + j0 + t] = v;
         }
       }
-      __syncthreads();
+      lds_barrier();
+      // rank-4 update of every tile with columns beyond the panel: one f64 MFMA each
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        if (its[q] < T16 && 16 * jts[q] + 15 >= j0 + 4) {
+          const double av = lb[(16 * its[q] + c) * 4 + g];
+          const double bv = lb[(16 * jts[q] + c) * 4 + g];
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc[q], 0, 0, 0);
+        }
+      }
     }
     if (!failed) {
       status = attempt > 0 ? -attempt : 0;
       break;
     }
     status = failed;
-    __syncthreads();
+    lds_barrier();
   }
-  for (int e = tid; e < M * M; e += T) {
+  __threadfence_block();
+  __syncthreads();   // L (global) complete and visible before the inverse phase reads it
+  if (status <= 0) {
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc[q][r] = (its[q] == jts[q] && g + 4 * r == c) ? 1.0 : 0.0;
+    // L[i][j0..j0+3] (rows i >= j0; identity beyond M) of step s: loaded during step s-1
+    auto load_panel = [&](int j0n, double (&v)[4]) {
+      const int i = j0n + tid;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int cl = j0n + t;
+        double x = (i == cl) ? 1.0 : 0.0;
+        if (i < M && cl < M && cl <= i) x = L[(size_t)i * M + cl];
+        v[t] = x;
+      }
+    };
+    double pn[4];
+    if (tid < Mp) load_panel(0, pn);
+    for (int s = 0; s < (Mp >> 2); ++s) {
+      const int j0 = 4 * s, it0 = s >> 2, sub = s & 3;
+#pragma unroll
+      for (int q = 0; q < NS; ++q) asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
+      if (j0 + tid < Mp) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) P[(j0 + tid) * 4 + t] = pn[t];
+      }
+      if (j0 + 4 + tid < Mp) load_panel(j0 + 4, pn);
+      // publish X rows j0..j0+3 (tile row it0, register r = sub holds rows 4 sub + g)
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        if (its[q] == it0) xr[g * Mp + 16 * jts[q] + c] = acc[q][sub];
+      }
+      lds_barrier();
+      // X_k = L4^{-1} X rows, one column per thread; final rows -> Linv
+      {
+        double l4[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) l4[r][t] = P[(j0 + r) * 4 + t];
+        double rd[4], l4i[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rd[r] = rcp64(l4[r][r]);
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (r < cc) { l4i[r][cc] = 0.0; continue; }
+            double v = (r == cc) ? 1.0 : 0.0;
+#pragma unroll
+            for (int q = cc; q < r; ++q) v -= l4[r][q] * l4i[q][cc];
+            l4i[r][cc] = v * rd[r];
+          }
+        for (int col = tid; col < Mp; col += KT) {
+          double x[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[r] = xr[r * Mp + col];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            double v = 0.0;
+#pragma unroll
+            for (int q = 0; q <= r; ++q) v = __builtin_fma(l4i[r][q], x[q], v);
+            lb[r * Mp + col] = v;
+            if (j0 + r < M && col < M && col <= j0 + r) Linv[(size_t)(j0 + r) * M + col] = v;
+          }
+        }
+      }
+      lds_barrier();
+      // X[i] -= L[i][j0..j0+3] X_k for tiles below the pivot rows and left of j0+4
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        if (its[q] < T16 && 16 * its[q] + 15 >= j0 + 4 && 16 * jts[q] <= j0 + 3) {
+          const double av = P[(16 * its[q] + c) * 4 + g];
+          const double bv = lb[g * Mp + 16 * jts[q] + c];
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc[q], 0, 0, 0);
+        }
+      }
+      lds_barrier();
+    }
+  }
+  for (int e = tid; e < M * M; e += KT) {
     const int i = e / M, j = e - i * M;
     if (j > i) { L[e] = 0.0; Linv[e] = 0.0; }
   }
@@ -269,18 +402,18 @@ GPK_DEVICE void stage_inducing(const float* __restrict__ Z, const float* __restr
     const float sd = (m < M) ? vstd[m] : 1.f;
     sm1[m] = sd * sd - 1.f;
   }
-  __syncthreads();
+  lds_barrier();
   for (int d = tid; d < Dq; d += T) {
     float s = 0.f;
     for (int m = 0; m < M; ++m) s += zs[m * ds + d];
     cm[d] = d < D ? s / (float)M : 0.f;  // GPyTorch _sq_dist centres by x1 = Z
   }
-  __syncthreads();
+  lds_barrier();
   for (int e = tid; e < M * Dq; e += T) {
     const int m = e / Dq, d = e - m * Dq;
     zs[m * ds + d] -= cm[d];
   }
-  __syncthreads();
+  lds_barrier();
   for (int m = tid; m < MP; m += T) {
     float s = 0.f;
     for (int d = 0; d < Dq; ++d) s = __builtin_fmaf(zs[m * ds + d], zs[m * ds + d], s);
@@ -296,7 +429,7 @@ GPK_DEVICE void stage_points(const float* __restrict__ Xw, const float* __restri
     const int j = e / Dq, d = e - j * Dq;
     xs[j * ds + d] = (j < nvalid && d < D) ? Xw[(size_t)j * D + d] / ls[d] - cm[d] : 0.f;
   }
-  __syncthreads();
+  lds_barrier();
   for (int j = tid; j < TW; j += T) {
     float s = 0.f;
     for (int d = 0; d < Dq; ++d) s = __builtin_fmaf(xs[j * ds + d], xs[j * ds + d], s);
@@ -433,11 +566,11 @@ gpk_var_fwd_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     const int i0 = ch * TW;
     const int nvalid = N - i0 < TW ? N - i0 : TW;
     const float* Xw = X + ((size_t)b * N + i0) * D;
-    __syncthreads();  // previous chunk done with xs / Kl / red; zs staged
+    lds_barrier();  // previous chunk done with xs / Kl / red; zs staged
     stage_points(Xw, ls, nvalid, D, TW, Dq, ds, cm, xs, xn);
-    __syncthreads();
+    lds_barrier();
     build_kzx<MB, TW>(zs, xs, zn, xn, M, nvalid, Dq, ds, s2, Kl);
-    __syncthreads();
+    lds_barrier();
     f64x4 acc[G::RT][G::CT];
     gemm_linv_k<MB>(Linv, Kl, M, acc);
     // epilogue: partial sum_m A m_m and sum_m A^2 (s_m^2 - 1) over the wave's rows
@@ -464,7 +597,7 @@ gpk_var_fwd_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         redv[wr * TW + 16 * (wc * G::CT + q) + c] = vp;
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (int col = tid; col < nvalid; col += blockDim.x) {
       float mm = 0.f, vv = 0.f;
 #pragma unroll
@@ -503,7 +636,7 @@ gpk_var_ell_kernel(const float* __restrict__ mean, const float* __restrict__ var
   }
   acc = wave_sum(acc);
   if ((tid & 63) == 0) red[tid >> 6] = acc;
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) ell[b] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
@@ -577,15 +710,15 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     const int nvalid = N - i0 < TW ? N - i0 : TW;
     const size_t col0 = (size_t)b * N + i0;
     const float* Xw = X + col0 * D;
-    __syncthreads();
+    lds_barrier();
     stage_points(Xw, ls, nvalid, D, TW, Dq, ds, cm, xs, xn);
     for (int j = tid; j < TW; j += blockDim.x) {
       gmc[j] = j < nvalid ? gmean[col0 + j] : 0.f;
       gvc[j] = j < nvalid ? gvar[col0 + j] : 0.f;
     }
-    __syncthreads();
+    lds_barrier();
     build_kzx<MB, TW>(zs, xs, zn, xn, M, nvalid, Dq, ds, s2, Kl);
-    __syncthreads();
+    lds_barrier();
     f64x4 acc[G::RT][G::CT];
     gemm_linv_k<MB>(Linv, Kl, M, acc);
     // variance -> clamp mask (no gradient below the clamp)
@@ -604,14 +737,14 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       vp += __shfl_xor(vp, 32, 64);
       if (g == 0) redw[wr * TW + 16 * (wc * G::CT + q) + c] = vp;
     }
-    __syncthreads();
+    lds_barrier();
     for (int col = tid; col < TW; col += blockDim.x) {
       float vv = 0.f;
       for (int q = 0; q < G::WR; ++q) vv += redw[q * TW + col];
       if (s2 + jit + vv < 1e-6f) gvc[col] = 0.f;  // clamp_min(1e-6): gradient masked
       sumgv += gvc[col];
     }
-    __syncthreads();
+    lds_barrier();
     // dA (fp32) -> LDS + workspace; partial sums for dvmean / dvstd
 #pragma unroll
     for (int j = 0; j < G::RT; ++j) {
@@ -648,7 +781,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       const int p = e / TW, col = e - p * TW;
       if (col < nvalid) wsK[(size_t)p * BN + col0 + col] = Kl[p * TW + col];
     }
-    __syncthreads();
+    lds_barrier();
     // dK = L^{-T} dA (fp64 MFMA): output rows p = the wave's row tiles, k = m >= p, in
     // k-blocks of 16 (k-order m = 16 kb + 4 g + u), next block's operands prefetched
     {
@@ -702,7 +835,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         }
       }
     }
-    __syncthreads();  // every wave is done reading dAl
+    lds_barrier();  // every wave is done reading dAl
     // Q = dK o K_ZX: Q^T -> LDS (over dAl), sum Q, r_i partials, and Q^T zs on f32 MFMA
     f32x4 xz[G::CT][NDT];
 #pragma unroll
@@ -742,7 +875,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       v += __shfl_xor(v, 32, 64);
       if (g == 0) redw[wr * TW + 16 * (wc * G::CT + q) + c] = v;
     }
-    __syncthreads();  // Q^T complete, K_ZX no longer needed, r partials in redw
+    lds_barrier();  // Q^T complete, K_ZX no longer needed, r partials in redw
     // Q^T zs partials -> LDS (over Kl): [wr][col][d]; xz[q][dt][r] = (Q^T zs)[16ct + 4g + r][16dt + c]
 #pragma unroll
     for (int q = 0; q < G::CT; ++q)
@@ -774,7 +907,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       for (int i = 0; i < TW; ++i) v += dAl[i * QST + p];
       qacc[p] += v;
     }
-    __syncthreads();  // Q^T zs partials and r complete
+    lds_barrier();  // Q^T zs partials and r complete
     // dX per point; sum_i r_i xs_i^2 per d (thread tid always sees d = tid % Dq)
     for (int e = tid; e < TW * Dq; e += blockDim.x) {
       const int col = e / Dq, d = e - col * Dq;
@@ -788,7 +921,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   // per-workgroup partials: [QX (M x D) | q (M) | dvm (M) | dsm (M) | rx2 (D) | sumQ | sumgv]
   const int P = M * D + 3 * M + D + 2;
   float* po = wspart + (size_t)blockIdx.x * P;
@@ -819,9 +952,9 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   }
   sumQ = wave_sum(sumQ);
   if (lane == 0) redw[wave] = sumQ;
-  __syncthreads();  // rx2 read, sumQ partials out
+  lds_barrier();  // rx2 read, sumQ partials out
   rx2[tid] = sumgv;  // accumulated by the column threads
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {
     float v = 0.f;
     for (int t = 0; t < 256; ++t) v += rx2[t];
@@ -889,7 +1022,7 @@ gpk_dlinv_kernel(const float* __restrict__ dA, const float* __restrict__ Kz, int
   };
   load(c0, ra, rb);
   for (long long cb = c0; cb < c1; cb += DLKC) {
-    __syncthreads();  // previous step's MFMA operand reads are done
+    lds_barrier();  // previous step's MFMA operand reads are done
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int e = tid + 256 * h, rr = e >> 3, k4 = 4 * (e & 7);
@@ -898,7 +1031,7 @@ gpk_dlinv_kernel(const float* __restrict__ dA, const float* __restrict__ Kz, int
       *(float2*)&sb[rr * DLST + k4] = float2{rb[h].x, rb[h].y};
       *(float2*)&sb[rr * DLST + k4 + 2] = float2{rb[h].z, rb[h].w};
     }
-    __syncthreads();
+    lds_barrier();
     if (cb + DLKC < c1) load(cb + DLKC, ra, rb);   // next step's loads overlap the MFMAs
 #pragma unroll
     for (int k = 0; k < DLKC / 4; ++k) {
@@ -959,7 +1092,7 @@ gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __r
     }
   }
   red[q0][o] = s;
-  __syncthreads();
+  lds_barrier();
   if (q0 == 0) {
     double t = 0.0;
 #pragma unroll
@@ -990,7 +1123,7 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
     for (int m = 0; m < M; ++m) s += Z[m * D + d] / ls[d];
     cmd[d] = (double)(s / (float)M);
   }
-  __syncthreads();
+  lds_barrier();
   const double* QX = tot;
   const double* q = tot + (size_t)M * D;
   const double* dvm = q + M;
@@ -1010,7 +1143,7 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
     }
     dld[d] = acc / (double)ls[d];
   }
-  __syncthreads();
+  lds_barrier();
   for (int m = tid; m < M; m += 256) {
     dpar[m] = (float)dvm[m];
     dpar[M + m] = (float)(2.0 * (double)vstd[m] * dsm[m]);
@@ -1159,16 +1292,27 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
 
 }  // namespace
 
-int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
-  const int Mp = (a.M + 3) & ~3;
-  const size_t lds = (size_t)(KR * Mp + KR * 2 * KR + KR * KR) * sizeof(double) +
-                     (size_t)(a.M * a.D + a.M + a.D) * sizeof(float);
-  if (lds > 160 * 1024) return -4;
-  set_lds_once<gpk_kzz_kernel>();
-  hipLaunchKernelGGL(gpk_kzz_kernel, dim3(1), dim3(1024), lds, stream, a.Z, a.hyp, a.M, a.D,
+template <int NS>
+int launch_kzz(const GpkKzzArgs& a, size_t lds, hipStream_t stream) {
+  set_lds_once<gpk_kzz_kernel<NS>>();
+  hipLaunchKernelGGL((gpk_kzz_kernel<NS>), dim3(1), dim3(KT), lds, stream, a.Z, a.hyp, a.M, a.D,
                      a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.Linv, a.info);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
+}
+
+int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
+  const int Mp = (a.M + 15) & ~15;
+  const size_t lds = (size_t)(3 * Mp * 4) * sizeof(double) +
+                     (size_t)(a.M * ((a.D + 3) & ~3) + a.M + a.D) * sizeof(float);
+  if (lds > 160 * 1024) return -4;
+  const int T16 = Mp >> 4;
+  const int ns = (T16 * (T16 + 1) / 2 + 7) / 8;   // tiles per wave
+  if (ns <= 2) return launch_kzz<2>(a, lds, stream);
+  if (ns <= 5) return launch_kzz<5>(a, lds, stream);
+  if (ns <= 10) return launch_kzz<10>(a, lds, stream);
+  if (ns <= 17) return launch_kzz<17>(a, lds, stream);
+  return -3;
 }
 
 int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream) {

@@ -154,6 +154,27 @@ int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Li
                                 void* workspace, float* dX, double* dLinv, float* dZ, float* dpar,
                                 void* stream);
 
+/*
+ * GPU-resident training-window gather:
+ *   for window b with first row r = rows[b] of the (id, time)-sorted table:
+ *     enc[b] = table[r      : r + n_enc]                  (n_enc, F)
+ *     dec[b] = table[r + n_enc : r + T - pred_len]        (T - n_enc - pred_len, F)
+ *     y[b]   = table[r + T - pred_len : r + T, target_col] (pred_len,)
+ *   r = -1 gives an all-zero window (the reference's zero-filled tail when max_samples
+ *   exceeds the valid sampling locations). Bit-exact copies (float32 table).
+ *
+ * Replaces (reference): the host NumPy windowing of Utils/base_train.py:29-97
+ * (sample_train_val_test; windows chosen as in batch_sampled_data :100-153) and the
+ * per-step host->device copies of train.py:160-161; the window CHOICE stays on the host
+ * (the reference's np.random sequence, reproduced by the caller).
+ *
+ * table : (n_rows, F) float, device    rows : (B,) int64, device (each r + T <= n_rows, or -1)
+ * enc : (B, n_enc, F) float out   dec : (B, T - n_enc - pred_len, F) float out   y : (B, pred_len) float out
+ */
+int gpk_window_gather_f32(const float* table, long long n_rows, int F, const long long* rows, int B,
+                          int T, int n_enc, int pred_len, int target_col, float* enc, float* dec,
+                          float* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
