@@ -76,7 +76,7 @@ struct GpkVarAdjArgs {
   float* dX;           // (B, N, D) out
   double* dLinv;       // (M, M) out (lower; upper zero)
   float* dZ;           // (M, D) out: the K_ZX part of dZ
-  float* dpar;         // (2M + 1 + D) out: dvmean, dvstd, ds2, dlengthscale
+  float* dpar;         // (2M + 2D + 2) out: dvmean, dvstd, ds2, dlengthscale, dweights, dbias
 };
 
 int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream);

@@ -677,7 +677,8 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   float* dvma = qacc + MP;            // WC x MP
   float* dsma = dvma + G::WC * MP;    // WC x MP
   float* rx2 = dsma + G::WC * MP;     // 256  per-thread sum r_i xs_i^2 (thread -> one d)
-  float* redw = rx2 + 256;            // 2 x WR x TW
+  float* gxa = rx2 + 256;             // 256  per-thread sum gmean_i xs_i (thread -> one d)
+  float* redw = gxa + 256;            // 2 x WR x TW
   float* Kl = redw + 2 * G::WR * TW;  // MP x TW     (later: Q^T zs partials, WR x TW x Dq)
   constexpr int KLN = MP * TW > G::WR * TW * DQ ? MP * TW : G::WR * TW * DQ;
   float* dAl = Kl + KLN;              // MP x TW dA  (later: Q^T, TW x QST)
@@ -695,7 +696,8 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     for (int q = 0; q < G::WC; ++q) { dvma[q * MP + m] = 0.f; dsma[q * MP + m] = 0.f; }
   }
   rx2[tid] = 0.f;
-  float sumQ = 0.f, sumgv = 0.f;
+  gxa[tid] = 0.f;
+  float sumQ = 0.f, sumgv = 0.f, sumgm = 0.f;
   // persistent f32 accumulators of QX = sum_i Q_pi xs_i: tiles (pt, dt) dealt over the waves
   constexpr int MAXQT = (MB * NDT + 3) / 4;  // QX tiles (MB x NDT) dealt over 4 waves
   f32x4 qx[MAXQT];
@@ -743,6 +745,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       for (int q = 0; q < G::WR; ++q) vv += redw[q * TW + col];
       if (s2 + jit + vv < 1e-6f) gvc[col] = 0.f;  // clamp_min(1e-6): gradient masked
       sumgv += gvc[col];
+      sumgm += gmc[col];
     }
     lds_barrier();
     // dA (fp32) -> LDS + workspace; partial sums for dvmean / dvstd
@@ -918,12 +921,14 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       if (col < nvalid && d < D) {
         dX[(col0 + col) * D + d] = (v - xv * r) / ls[d] + gmc[col] * w[d];
         rx2[tid] += r * xv * xv;
+        gxa[tid] += gmc[col] * xv;   // LinearMean: dw = l (sum gmean xs + cm sum gmean)
       }
     }
   }
   lds_barrier();
-  // per-workgroup partials: [QX (M x D) | q (M) | dvm (M) | dsm (M) | rx2 (D) | sumQ | sumgv]
-  const int P = M * D + 3 * M + D + 2;
+  // per-workgroup partials:
+  //   [QX (M x D) | q (M) | dvm (M) | dsm (M) | rx2 (D) | sumQ | sumgv | gx (D) | sumgm]
+  const int P = M * D + 3 * M + 2 * D + 3;
   float* po = wspart + (size_t)blockIdx.x * P;
 #pragma unroll
   for (int u = 0; u < MAXQT; ++u) {
@@ -944,22 +949,25 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     po[M * D + M + m] = a;
     po[M * D + 2 * M + m] = s;
   }
-  // sum r xs^2 over the threads that accumulated the same d (d = tid % Dq)
+  // sum r xs^2 and gmean xs over the threads that accumulated the same d (d = tid % Dq)
   for (int d = tid; d < D; d += blockDim.x) {
-    float v = 0.f;
-    for (int t = d; t < 256; t += Dq) v += rx2[t];
+    float v = 0.f, u = 0.f;
+    for (int t = d; t < 256; t += Dq) { v += rx2[t]; u += gxa[t]; }
     po[M * D + 3 * M + d] = v;
+    po[M * D + 3 * M + D + 2 + d] = u;
   }
   sumQ = wave_sum(sumQ);
   if (lane == 0) redw[wave] = sumQ;
-  lds_barrier();  // rx2 read, sumQ partials out
+  lds_barrier();  // rx2 / gxa read, sumQ partials out
   rx2[tid] = sumgv;  // accumulated by the column threads
+  gxa[tid] = sumgm;
   lds_barrier();
   if (tid == 0) {
-    float v = 0.f;
-    for (int t = 0; t < 256; ++t) v += rx2[t];
+    float v = 0.f, u = 0.f;
+    for (int t = 0; t < 256; ++t) { v += rx2[t]; u += gxa[t]; }
     po[M * D + 3 * M + D] = (redw[0] + redw[1]) + (redw[2] + redw[3]);
     po[M * D + 3 * M + D + 1] = v;
+    po[M * D + 3 * M + 2 * D + 2] = u;
   }
 }
 
@@ -1105,24 +1113,31 @@ gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __r
   }
 }
 
-// Outputs from the reduced totals (one workgroup):
+// Outputs from the reduced totals (one workgroup; zs staged in LDS, the d-sums split
+// over 256 / D threads each and combined in a fixed order):
 //   dZ_p = (QX_p - zs_p q_p) / l;   dl_d = (sum_p q_p zs_pd^2 - 2 sum_p zs_pd QX_pd + sum_i r_i xs_id^2) / l_d
 //   ds2 = sum Q / s2 + sum gvar;    dvmean = sum gmean A;   dvstd = 2 s sum gvar A^2
-// dpar = [dvmean (M) | dvstd (M) | ds2 | dl (D)]
+//   dw_d = l_d (sum_i gmean_i xs_id + cm_d sum_i gmean_i);   db0 = sum_i gmean_i
+// dpar = [dvmean (M) | dvstd (M) | ds2 | dl (D) | dw (D) | db0]
 __global__ void __launch_bounds__(256)
 gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
                    const float* __restrict__ hyp, const double* __restrict__ tot, int M, int D,
                    float* __restrict__ dZ, float* __restrict__ dpar) {
-  __shared__ double cmd[64];
-  __shared__ double dld[64];
+  extern __shared__ __attribute__((aligned(16))) float fzs[];   // M x D zs (centred Z / l)
+  __shared__ double red[256];
+  __shared__ float cmf[64];
   const int tid = threadIdx.x;
   const float s2 = hyp[0];
   const float* ls = hyp + 4 + D;
+  for (int e = tid; e < M * D; e += 256) fzs[e] = Z[e] / ls[e % D];
+  lds_barrier();
   for (int d = tid; d < D; d += 256) {
-    float s = 0.f;  // the same fp32 sum as stage_inducing: the identical centre
-    for (int m = 0; m < M; ++m) s += Z[m * D + d] / ls[d];
-    cmd[d] = (double)(s / (float)M);
+    float sm = 0.f;  // the same fp32 sum as stage_inducing: the identical centre
+    for (int m = 0; m < M; ++m) sm += fzs[m * D + d];
+    cmf[d] = sm / (float)M;
   }
+  lds_barrier();
+  for (int e = tid; e < M * D; e += 256) fzs[e] -= cmf[e % D];
   lds_barrier();
   const double* QX = tot;
   const double* q = tot + (size_t)M * D;
@@ -1130,26 +1145,37 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
   const double* dsm = dvm + M;
   const double* rx2 = dsm + M;
   const double sumQ = rx2[D], sumgv = rx2[D + 1];
+  const double* gx = rx2 + D + 2;
+  const double sumgm = gx[D];
   for (int e = tid; e < M * D; e += 256) {
     const int p = e / D, d = e - p * D;
-    const double zsv = (double)(Z[p * D + d] / ls[d] - (float)cmd[d]);
-    dZ[e] = (float)((QX[e] - zsv * q[p]) / (double)ls[d]);
+    dZ[e] = (float)((QX[e] - (double)fzs[e] * q[p]) / (double)ls[d]);
   }
-  for (int d = tid; d < D; d += 256) {
-    double acc = rx2[d];
-    for (int p = 0; p < M; ++p) {
-      const double zsv = (double)(Z[p * D + d] / ls[d] - (float)cmd[d]);
+  const int nk = 256 / D;
+  double acc = 0.0;
+  if (tid < nk * D) {
+    const int d = tid % D, k = tid / D;
+    for (int p = k; p < M; p += nk) {
+      const double zsv = (double)fzs[p * D + d];
       acc += q[p] * zsv * zsv - 2.0 * zsv * QX[(size_t)p * D + d];
     }
-    dld[d] = acc / (double)ls[d];
   }
+  red[tid] = acc;
   lds_barrier();
+  if (tid < D) {
+    double v = rx2[tid];
+    for (int k = 0; k < nk; ++k) v += red[k * D + tid];
+    dpar[2 * M + 1 + tid] = (float)(v / (double)ls[tid]);
+    dpar[2 * M + 1 + D + tid] = (float)((double)ls[tid] * (gx[tid] + (double)cmf[tid] * sumgm));
+  }
   for (int m = tid; m < M; m += 256) {
     dpar[m] = (float)dvm[m];
     dpar[M + m] = (float)(2.0 * (double)vstd[m] * dsm[m]);
   }
-  if (tid == 0) dpar[2 * M] = (float)(sumQ / (double)s2 + sumgv);
-  for (int d = tid; d < D; d += 256) dpar[2 * M + 1 + d] = (float)dld[d];
+  if (tid == 0) {
+    dpar[2 * M] = (float)(sumQ / (double)s2 + sumgv);
+    dpar[2 * M + 1 + 2 * D] = (float)sumgm;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1172,17 +1198,17 @@ size_t var_adj_lds() {
   const size_t da = (size_t)G::MP * G::TW > (size_t)G::TW * G::QST ? (size_t)G::MP * G::TW
                                                                    : (size_t)G::TW * G::QST;
   return ((size_t)G::MP * ds + G::TW * ds + G::MP + G::TW + 2 * G::MP + Dq + 3 * G::TW + G::MP +
-          2 * G::WC * G::MP + 256 + 2 * G::WR * G::TW + kl + da) * sizeof(float);
+          2 * G::WC * G::MP + 2 * 256 + 2 * G::WR * G::TW + kl + da) * sizeof(float);
 }
 
 // hipFuncSetAttribute once per kernel instantiation (thread-safe; the C ABI has no
 // mutable global state beyond this idempotent one-time setup).
-template <auto Kernel>
+template <auto Kernel, int Bytes = 160 * 1024>
 void set_lds_once() {
   static std::once_flag once;  // one flag per kernel instantiation
   std::call_once(once, [] {
-    (void)hipFuncSetAttribute((const void*)Kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)Kernel, hipFuncAttributeMaxDynamicSharedMemorySize, Bytes);
+    (void)hipGetLastError();   // never leave a sticky error for the launch check to pick up
   });
 }
 
@@ -1218,6 +1244,7 @@ struct AdjPlan {
   int nchunks, nwg, P, ntiles, nsplit;
   long long BN, cols_per_split;
   size_t off_dA, off_K, off_part, off_tot, off_dl, total;  // byte offsets
+  size_t fin_lds;
 };
 
 template <int MB>
@@ -1226,7 +1253,8 @@ AdjPlan adj_plan(int B, int N, int M, int D) {
   AdjPlan p{};
   p.nchunks = B * ((N + G::TW - 1) / G::TW);
   p.nwg = chunk_grid(p.nchunks, 2);
-  p.P = M * D + 3 * M + D + 2;
+  p.P = M * D + 3 * M + 2 * D + 3;
+  p.fin_lds = (size_t)M * D * sizeof(float);
   p.BN = (long long)B * N;
   const int MT = (M + 63) / 64;
   p.ntiles = MT * (MT + 1) / 2;
@@ -1274,8 +1302,9 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
                      wspart, p.nwg, p.P, tot, dl, p.nsplit, p.ntiles, a.M, a.dLinv);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(1), dim3(256), 0, stream, a.Z, a.vstd, a.hyp, tot,
-                     a.M, a.D, a.dZ, a.dpar);
+  set_lds_once<gpk_var_fin_kernel, 64 * 1024>();   // + ~2.3 KB static
+  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(1), dim3(256), p.fin_lds, stream, a.Z, a.vstd, a.hyp,
+                     tot, a.M, a.D, a.dZ, a.dpar);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }

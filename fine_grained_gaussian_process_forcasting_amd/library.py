@@ -155,15 +155,13 @@ def variational_adj(x: Tensor, Linv: Tensor, Z: Tensor, vmean: Tensor, vstd: Ten
     B, N, D = x.shape
     adj = ops.variational_adjoint(x, Z, Linv, vmean, vstd, _var_hyper(x, s2, ls, w, b0, jitter),
                                   gmean, gvar)
-    gm = gmean.reshape(B * N).float()
-    dw = x.detach().reshape(B * N, D).float().transpose(0, 1) @ gm     # LinearMean weights
-    db0 = gm.sum()
+    dw, db0 = adj.dw, adj.db0                                        # LinearMean (in-kernel)
     dls = adj.dls.sum().reshape(ls.shape) if ls.numel() == 1 else adj.dls.reshape(ls.shape)
     return (adj.dX.to(x.dtype), adj.dLinv, adj.dZ.to(Z.dtype),
             adj.dvmean.reshape(vmean.shape).to(vmean.dtype).clone(),
             adj.dvstd.reshape(vstd.shape).to(vstd.dtype).clone(),
             adj.ds2.reshape(s2.shape).to(s2.dtype).clone(), dls.to(ls.dtype).clone(),
-            dw.reshape(w.shape).to(w.dtype), db0.reshape(b0.shape).to(b0.dtype))
+            dw.reshape(w.shape).to(w.dtype).clone(), db0.reshape(b0.shape).to(b0.dtype).clone())
 
 
 @variational_adj.register_fake

@@ -272,6 +272,8 @@ class VariationalAdjoint:
     dvstd: torch.Tensor   # (M,)
     ds2: torch.Tensor     # () K_ZX + variance parts
     dls: torch.Tensor     # (D,) the K_ZX part
+    dw: torch.Tensor      # (D,) LinearMean weights
+    db0: torch.Tensor     # () LinearMean bias
 
 
 def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vmean: torch.Tensor,
@@ -298,13 +300,15 @@ def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
     dX = torch.empty(B, N, D, device=dev, dtype=torch.float32)
     dLinv = torch.empty(M, M, device=dev, dtype=torch.float64)
     dZ = torch.empty(M, D, device=dev, dtype=torch.float32)
-    dpar = torch.empty(2 * M + 1 + D, device=dev, dtype=torch.float32)
+    dpar = torch.empty(2 * M + 2 * D + 2, device=dev, dtype=torch.float32)
     rc = lib.gpk_variational_adjoint_f32(
         X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
         hyper.data_ptr(), gmean.data_ptr(), gvar.data_ptr(), B, N, M, D, ws.data_ptr(),
         dX.data_ptr(), dLinv.data_ptr(), dZ.data_ptr(), dpar.data_ptr(), _stream_ptr(dev))
     _native.check(rc, "gpk_variational_adjoint_f32")
-    return VariationalAdjoint(dX, dLinv, dZ, dpar[:M], dpar[M:2 * M], dpar[2 * M], dpar[2 * M + 1:])
+    return VariationalAdjoint(dX, dLinv, dZ, dpar[:M], dpar[M:2 * M], dpar[2 * M],
+                              dpar[2 * M + 1:2 * M + 1 + D], dpar[2 * M + 1 + D:2 * M + 1 + 2 * D],
+                              dpar[2 * M + 1 + 2 * D])
 
 
 def kzz_backward(dLinv: torch.Tensor, L: torch.Tensor, Linv: torch.Tensor, Z: torch.Tensor,

@@ -64,8 +64,7 @@ class KzzCache:
         if e is not None and e["key"] == key and e["grad"] == grad and not e["spent"]:
             return e["Linv"]
         Linv, _, info = torch.ops.gpk.kzz_factor(Z, s2, ls, float(jitter), 1e-8, 3)
-        ops.check_cholesky_info(info, 1e-8, inputs=(Z,), what="K_ZZ cholesky")
-        entry = {"key": key, "grad": grad, "Linv": Linv, "spent": False}
+        entry = {"key": key, "grad": grad, "Linv": Linv, "spent": False, "info": info, "Z": Z}
         if grad:
             def _spent(g, entry=entry):
                 entry["spent"] = True        # this step's backward consumed the node
@@ -73,6 +72,17 @@ class KzzCache:
             Linv.register_hook(_spent)
         self._entry = entry
         return Linv
+
+    def check_pending(self):
+        """psd_safe_cholesky's verdict on a freshly computed factor (one host sync). Called
+        after the first kernel that consumes the factor has been queued, so the GPU is
+        not idle while the host waits; raises / warns exactly as GPyTorch during the call."""
+        e = self._entry
+        if e is not None and e.get("info") is not None:
+            info, Z = e["info"], e["Z"]
+            e["info"] = None
+            e["Z"] = None
+            ops.check_cholesky_info(info, 1e-8, inputs=(Z,), what="K_ZZ cholesky")
 
 
 def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module, jitter,
@@ -86,4 +96,6 @@ def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module
     if cache is None:
         cache = KzzCache()
     Linv = cache.factor(Z, s2, ls, jitter, key_tensors if key_tensors is not None else (Z, s2, ls))
-    return torch.ops.gpk.variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, float(jitter))
+    out = torch.ops.gpk.variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, float(jitter))
+    cache.check_pending()
+    return out

@@ -138,8 +138,8 @@ int gpk_variational_f32(const float* X, const float* Z, const double* Linv, cons
  *   dLinv (M, M) double out: sum over all points of dA K_ZX^T (lower, upper zero) -- the
  *         caller back-propagates it through the shared K_ZZ factor once per step
  *   dZ    (M, D) float out: the K_ZX part of dZ
- *   dpar  (2M + 1 + D) float out: {dvmean (M), dvstd (M), ds2 (K_ZX and variance parts), dl (D)}
- * (dweights = X^T gmean and dbias = sum gmean are plain reductions left to the caller.)
+ *   dpar  (2M + 2D + 2) float out: {dvmean (M), dvstd (M), ds2 (K_ZX and variance parts),
+ *         dl (D, K_ZX part), dweights (D), dbias}  (LinearMean: dweights = X^T gmean)
  * workspace : gpk_variational_adjoint_workspace_bytes(B, N, M, D) bytes of device memory.
  * All sums are in a fixed order (run-to-run deterministic).
  *
