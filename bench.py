@@ -15,6 +15,8 @@ Side legs in the same JSON line (not the headline):
                mean / variance / ELL (gpk_variational_f32), and the fused adjoint
                (gpk_variational_adjoint_f32), with its compute roofline (SURVEY §8d);
   backward     the exact path's analytic adjoint on the headline windows;
+  posterior    the exact path's eval-mode posterior (mean + variance at N new points per
+               window) from the headline windows' factor;
   cpu_baseline the reference's CPU arithmetic (GPyTorch's torch-CPU calls restated in
                oracle/) on the GPU box's host cores, all threads and 1 thread, plus the
                variational path; and the MLL relative error of the GPU kernel vs the
@@ -299,7 +301,7 @@ def main():
         elapsed, kern_ms = (float(v) for v in t.tolist())
     mean_mll = float(totals[-1].item()) / B_total
 
-    grad_ms = None
+    grad_ms = post_ms = None
     if not args.no_grad:
         fw = ops.exact_mll(X, y, None, None, None, None, hyper=hyper, want_L=True, want_z=True)
         gout = torch.ones(B, device=dev)
@@ -311,6 +313,16 @@ def main():
                 ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
         torch.cuda.synchronize()
         grad_ms = gt.mean_ms()
+        # eval-mode posterior at Ns = N new points per window from the same factor
+        Xs = make_inputs(B, N, D, dev, seed=77 + rank)[0]
+        ops.exact_posterior(X, fw.L, fw.z, hyper, Xs)
+        torch.cuda.synchronize()
+        pt = EventTimer(5)
+        for _ in range(5):
+            with pt:
+                ops.exact_posterior(X, fw.L, fw.z, hyper, Xs)
+        torch.cuda.synchronize()
+        post_ms = pt.mean_ms()
 
     var = None
     if not args.no_var:
@@ -351,6 +363,15 @@ def main():
             line["backward"] = {"kernel": "gpk_exact_mll_grad_f32", "kernel_ms": grad_ms,
                                 "windows_per_s_per_gpu": B / (grad_ms * 1e-3),
                                 "note": "analytic dX/dy/dhyper of the same windows; not the headline"}
+        if post_ms is not None:
+            pb = 4 * (2 * N * D + N * (N + 1) // 2 + N + 2 * N)     # X, Xs, lower L, z; mean + var
+            pf = 2 * N * N * D + N * N * N + 2 * N * N + 10 * N * N  # Gram, TRSM, mean/var, RBF
+            line["posterior"] = {"kernel": "gpk_exact_posterior_f32", "kernel_ms": post_ms,
+                                 "test_points_per_window": N,
+                                 "windows_per_s_per_gpu": B / (post_ms * 1e-3),
+                                 "hbm_frac": pb * B / (post_ms * 1e-3) / HBM_PEAK,
+                                 "fp32_frac": pf * B / (post_ms * 1e-3) / FP32_PEAK,
+                                 "note": "eval-mode exact posterior mean + variance; not the headline"}
         if var is not None:
             line["variational"] = var
         if world == 1 and not args.no_cpu_baseline:

@@ -4,6 +4,6 @@ class surface."""
 from . import _native, ops  # noqa: F401
 from . import gp, mlls, likelihoods  # noqa: F401
 from .gp import settings  # noqa: F401
-from .errors import GpkInternalError, NanError, NotPSDError, NumericalWarning  # noqa: F401
+from .errors import GPInputWarning, GpkInternalError, NanError, NotPSDError, NumericalWarning  # noqa: F401
 
 __version__ = "0.1.0"

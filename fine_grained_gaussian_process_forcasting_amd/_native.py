@@ -34,6 +34,8 @@ SIGNATURES = {
     "gpk_exact_mll_grad_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p]),
+    "gpk_exact_posterior_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                                        c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "gpk_kzz_chol_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_float, c_double, c_int,
                                  c_void_p, c_void_p, c_void_p, c_void_p]),
     "gpk_variational_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

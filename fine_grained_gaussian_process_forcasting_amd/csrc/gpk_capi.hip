@@ -65,6 +65,26 @@ int gpk_exact_mll_grad_f32(const float* X, const float* L, const float* z, const
   return gpk_launch_exact_grad(a, (hipStream_t)stream);
 }
 
+int gpk_exact_posterior_f32(const float* X, const float* L, const float* z, const float* hyp,
+                            int n_lengthscale, const float* Xs, int B, int N, int Ns, int D,
+                            float* mean, float* var, void* stream) {
+  if (X == nullptr) return -1;
+  if (L == nullptr) return -2;
+  if (z == nullptr) return -3;
+  if (hyp == nullptr) return -4;
+  if (n_lengthscale != 1 && n_lengthscale != D) return -5;
+  if (Xs == nullptr) return -6;
+  if (B < 0) return -7;
+  if (N < 1 || N > gpk_exact_max_n()) return -8;
+  if (Ns < 0) return -9;
+  if (D < 1 || D > 64) return -10;
+  if (mean == nullptr) return -11;
+  if (var == nullptr) return -12;
+  if (B == 0 || Ns == 0) return 0;
+  GpkPostArgs a{X, L, z, hyp, n_lengthscale, Xs, B, N, Ns, D, mean, var};
+  return gpk_launch_exact_posterior(a, (hipStream_t)stream);
+}
+
 int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitter,
                      double chol_jitter, int max_tries, double* L, double* Linv, int* info,
                      void* stream) {

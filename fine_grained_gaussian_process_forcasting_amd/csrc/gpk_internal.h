@@ -87,3 +87,18 @@ int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream);
 int gpk_launch_window_gather(const float* table, int F, const long long* rows, int B, int n_enc,
                              int n_dec, int pred_len, int tcol, float* enc, float* dec, float* y,
                              hipStream_t stream);
+
+struct GpkPostArgs {
+  const float* X;      // (B, N, D) training inputs
+  const float* L;      // (B, N, N) training factor chol(K + noise I (+ jitter)), lower
+  const float* z;      // (B, N) L^{-1}(y - c)
+  const float* hyp;    // as GpkExactArgs: [outputscale, noise, mean_constant, lengthscale[n_ls]]
+  int n_ls;
+  const float* Xs;     // (B, Ns, D) test inputs
+  int B, N, Ns, D;
+  float* mean;         // (B, Ns) posterior mean of f
+  float* var;          // (B, Ns) posterior variance of f (unclamped)
+};
+
+size_t gpk_post_lds_bytes(int N, int D);
+int gpk_launch_exact_posterior(const GpkPostArgs& a, hipStream_t stream);

@@ -1,16 +1,47 @@
 """ExactGPModel on the gfx950 kernels (reference denoising_model/GPModel.py:4-13).
 
-``model(x)`` returns the prior MultivariateNormal(mean_x, covar_x) lazily;
-``ExactMarginalLogLikelihood(likelihood, model)(model(train_x), train_y)`` evaluates
-the per-window marginal log likelihood / N with ONE fused kernel (RBF Gram +
+Training mode: ``model(x)`` returns the prior MultivariateNormal(mean_x, covar_x)
+lazily; ``ExactMarginalLogLikelihood(likelihood, model)(model(train_x), train_y)``
+evaluates the per-window marginal log likelihood / N with ONE fused kernel (RBF Gram +
 jittered Cholesky + forward solve + logdet): include/gpk.h::gpk_exact_mll_f32.
+
+Eval mode: ``model(x)`` is the posterior of f at x (upstream
+models/exact_gp.py __call__ -> exact_prediction_strategies.py): the training factor L
+and z = L^{-1}(y - c) come from gpk_exact_mll_f32 once and are cached until a
+parameter or the training data changes or ``train()`` is called (GPyTorch's
+``prediction_strategy`` cache); mean and variance at x come from
+gpk_exact_posterior_f32. ``likelihood(model(x))`` adds the noise. As in GPyTorch,
+calling the model in eval mode on the training inputs warns (GPInputWarning) and
+returns the posterior there.
+
+Inputs may be batched (B, N, D) windows, a single (N, D) window or 1-D (N,) points,
+as GPyTorch accepts; targets follow (B, N) / (N,).
 """
 from __future__ import annotations
+
+import warnings
 
 import torch
 import torch.nn as nn
 
+from .. import ops
+from ..errors import GPInputWarning
 from ..gp import ConstantMean, MultivariateNormal, RBFKernel, ScaleKernel
+
+
+def _as_batch(x: torch.Tensor) -> torch.Tensor:
+    """(N,) -> (1, N, 1); (N, D) -> (1, N, D); (B, N, D) unchanged."""
+    if x.dim() == 1:
+        return x.reshape(1, -1, 1)
+    if x.dim() == 2:
+        return x.unsqueeze(0)
+    if x.dim() == 3:
+        return x
+    raise ValueError(f"inputs must be (N,), (N, D) or (B, N, D), got {tuple(x.shape)}")
+
+
+def _version_key(*ts):
+    return tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in ts)
 
 
 class ExactGPModel(nn.Module):
@@ -21,16 +52,79 @@ class ExactGPModel(nn.Module):
         self.likelihood = likelihood
         self.mean_module = ConstantMean()
         self.covar_module = ScaleKernel(RBFKernel())
+        self._prediction_cache = None
+
+    def set_train_data(self, inputs=None, targets=None, strict=True):
+        if inputs is not None:
+            x = inputs[0] if isinstance(inputs, (tuple, list)) else inputs
+            if strict and x.shape != self.train_inputs[0].shape:
+                raise RuntimeError("Cannot modify the shape of train inputs with strict=True")
+            self.train_inputs = (x,)
+        if targets is not None:
+            if strict and targets.shape != self.train_targets.shape:
+                raise RuntimeError("Cannot modify the shape of train targets with strict=True")
+            self.train_targets = targets
+        self._prediction_cache = None
+
+    def train(self, mode: bool = True):
+        self._prediction_cache = None       # GPyTorch drops its prediction strategy here
+        return super().train(mode)
 
     def forward(self, x):
-        mean_x = self.mean_module(x)
+        xb = _as_batch(x)
+        mean_x = self.mean_module(x if x.dim() > 1 else x.unsqueeze(-1))
         return MultivariateNormal(mean_x, None,
-                                  exact=(x, self.covar_module.base_kernel.lengthscale,
+                                  exact=(xb, self.covar_module.base_kernel.lengthscale,
                                          self.covar_module.outputscale, self.mean_module.constant))
 
     def __call__(self, x=None):
         if x is None:
             x = self.train_inputs[0]
-        if not self.training and not torch.equal(x, self.train_inputs[0]):
-            raise NotImplementedError("exact-GP posterior prediction at new inputs is §8f 'next' work")
-        return self.forward(x)
+        if self.training:
+            return self.forward(x)
+        train_x = self.train_inputs[0]
+        if x.shape == train_x.shape and torch.equal(x, train_x):
+            warnings.warn("The input matches the stored training data. Did you forget to call "
+                          "model.train()?", GPInputWarning)
+        return self._posterior(x)
+
+    # ---- eval mode -------------------------------------------------------------
+    def _hyper(self, device):
+        kern = self.covar_module
+        return ops.pack_exact_hyper(kern.outputscale, self.likelihood.noise, self.mean_module.constant,
+                                    kern.base_kernel.lengthscale, device)
+
+    def _train_factor(self):
+        train_x, train_y = self.train_inputs[0], self.train_targets
+        kern = self.covar_module
+        key = _version_key(train_x, train_y, kern.raw_outputscale, kern.base_kernel.raw_lengthscale,
+                           self.mean_module.constant, self.likelihood.noise_covar.raw_noise)
+        cache = self._prediction_cache
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        Xb = _as_batch(train_x).detach().float()
+        yb = train_y.detach().reshape(Xb.shape[0], Xb.shape[1]).float()
+        hyper = self._hyper(Xb.device).detach()
+        out = ops.exact_mll(Xb, yb, None, None, None, None, want_L=True, want_z=True, hyper=hyper)
+        ops.check_cholesky_info(out.info, 1e-6, inputs=(Xb, yb))
+        entry = (Xb, out.L, out.z, hyper)
+        self._prediction_cache = (key, entry)
+        return entry
+
+    def _posterior(self, x):
+        params = [p for p in self.parameters()] + [x, self.train_inputs[0], self.train_targets]
+        if torch.is_grad_enabled() and any(t.requires_grad for t in params):
+            raise NotImplementedError(
+                "gradients through the exact-GP posterior are not provided; evaluate predictions "
+                "under torch.no_grad() (as GPyTorch's prediction examples do)")
+        Xb, L, z, hyper = self._train_factor()
+        xs = _as_batch(x).float()
+        if xs.shape[0] != Xb.shape[0]:
+            xs = xs.expand(Xb.shape[0], *xs.shape[1:])
+        from .. import library  # noqa: F401  (registers torch.ops.gpk)
+        mean, var = torch.ops.gpk.exact_posterior(Xb, L, z, hyper, xs.contiguous())
+        if x.dim() == 3 or Xb.shape[0] > 1:
+            shape = mean.shape                    # (B, Ns): one posterior per training window
+        else:
+            shape = x.shape[:-1] if x.dim() > 1 else x.shape
+        return MultivariateNormal(mean.reshape(shape), var.reshape(shape))

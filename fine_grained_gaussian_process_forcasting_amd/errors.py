@@ -18,3 +18,8 @@ class GpkInternalError(RuntimeError):
 class NumericalWarning(RuntimeWarning):
     """Mirror of gpytorch.utils.warnings.NumericalWarning."""
     pass
+
+
+class GPInputWarning(UserWarning):
+    """Mirror of gpytorch.utils.warnings.GPInputWarning."""
+    pass

@@ -246,7 +246,8 @@ class MultivariateNormal:
         noise = self._added_noise if self._added_noise is not None else torch.zeros((), device=X.device)
         from .ops_autograd import exact_log_prob
         n = X.shape[-2]
-        return exact_log_prob(X, value, lengthscale, outputscale, constant, noise) * n
+        res = exact_log_prob(X, value.reshape(X.shape[:-1]), lengthscale, outputscale, constant, noise) * n
+        return res.reshape(value.shape[:-1])      # (N,) targets of an unbatched model -> scalar
 
 
 # ---------------------------------------------------------------------------

@@ -8,6 +8,7 @@ instead of being opaque Python. Each op is one C-ABI call of include/gpk.h on
 
   gpk::exact_mll(X, y, hyper, jitter, max_tries) -> (mll, L, z, info)         [autograd]
   gpk::exact_mll_grad(X, L, z, hyper, gout) -> (dX, dy, dhyp)
+  gpk::exact_posterior(X, L, z, hyper, Xs) -> (mean, var)                     [eval only]
   gpk::kzz_factor(Z, s2, ls, jitter, chol_jitter, max_tries) -> (Linv, L, info) [autograd]
   gpk::variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter) -> (mean, var, flags)
                                                                                [autograd]
@@ -15,7 +16,7 @@ instead of being opaque Python. Each op is one C-ABI call of include/gpk.h on
       -> (dX, dLinv, dZ, dvmean, dvstd, ds2, dls, dw, db0)
 
 Reference call sites they serve: GPModel.py:10-13 + ExactMarginalLogLikelihood
-(exact_mll), DeepGP.py:33-73 VariationalStrategy (kzz_factor, variational_fwd), and
+(exact_mll), ExactGPModel in eval mode (exact_posterior), DeepGP.py:33-73 VariationalStrategy (kzz_factor, variational_fwd), and
 the backward of train.py:166 (the *_grad / *_adj ops).
 """
 from __future__ import annotations
@@ -63,6 +64,18 @@ def exact_mll_grad(X: Tensor, L: Tensor, z: Tensor, hyper: Tensor,
 def _(X, L, z, hyper, gout):
     B, N, D = X.shape
     return X.new_empty(B, N, D), X.new_empty(B, N), X.new_empty(B, hyper.numel())
+
+
+@torch.library.custom_op("gpk::exact_posterior", mutates_args=(), device_types="cuda")
+def exact_posterior(X: Tensor, L: Tensor, z: Tensor, hyper: Tensor, Xs: Tensor) -> Tuple[Tensor, Tensor]:
+    p = ops.exact_posterior(X, L, z, hyper, Xs)
+    return p.mean, p.var
+
+
+@exact_posterior.register_fake
+def _(X, L, z, hyper, Xs):
+    B, Ns, _ = Xs.shape
+    return Xs.new_empty(B, Ns), Xs.new_empty(B, Ns)
 
 
 def _exact_setup(ctx, inputs, output):

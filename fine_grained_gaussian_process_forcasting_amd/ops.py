@@ -126,6 +126,40 @@ def exact_mll_grad(X: torch.Tensor, L: torch.Tensor, z: torch.Tensor, hyper: tor
     return ExactMLLGrad(dX, dy, dhyp)
 
 
+@dataclass
+class ExactPosterior:
+    mean: torch.Tensor   # (B, Ns) posterior mean of f
+    var: torch.Tensor    # (B, Ns) posterior variance of f (unclamped)
+
+
+def exact_posterior(X: torch.Tensor, L: torch.Tensor, z: torch.Tensor, hyper: torch.Tensor,
+                    Xs: torch.Tensor) -> ExactPosterior:
+    """Exact-GP posterior at the test inputs ``Xs`` (B, Ns, D) from the training factor
+    ``L`` and ``z = L^{-1}(y - c)`` of ``exact_mll`` (one gfx950 kernel launch, see
+    include/gpk.h::gpk_exact_posterior_f32). ``hyper`` is the exact path's device vector."""
+    if X.dim() != 3 or Xs.dim() != 3:
+        raise ValueError("X and Xs must be (B, N, D) and (B, Ns, D)")
+    B, N, D = X.shape
+    if Xs.shape[0] != B or Xs.shape[2] != D:
+        raise ValueError(f"Xs must be (B, Ns, D) = ({B}, Ns, {D}), got {tuple(Xs.shape)}")
+    if L.shape != (B, N, N) or z.shape != (B, N):
+        raise ValueError("L / z do not match X")
+    _require_device(X, L, z, hyper, Xs)
+    X = X.detach().contiguous().float()
+    Xs = Xs.detach().contiguous().float()
+    L = L.detach().contiguous().float()
+    z = z.detach().contiguous().float()
+    Ns = Xs.shape[1]
+    dev = X.device
+    mean = torch.empty(B, Ns, device=dev, dtype=torch.float32)
+    var = torch.empty(B, Ns, device=dev, dtype=torch.float32)
+    rc = _native.lib().gpk_exact_posterior_f32(
+        X.data_ptr(), L.data_ptr(), z.data_ptr(), hyper.data_ptr(), hyper.numel() - 3, Xs.data_ptr(),
+        B, N, Ns, D, mean.data_ptr(), var.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_exact_posterior_f32")
+    return ExactPosterior(mean, var)
+
+
 INFO_TIMEOUT = 1 << 20   # gpk_exact.hip kInfoTimeout: a bounded LDS spin-wait expired
 
 

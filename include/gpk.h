@@ -84,6 +84,26 @@ int gpk_exact_mll_grad_f32(const float* X, const float* L, const float* z, const
                            float* dX, float* dy, float* dhyp, void* stream);
 
 /*
+ * Exact-GP posterior at new inputs (eval mode), per window b, from the training
+ * factor of gpk_exact_mll_f32 (nothing is refactored):
+ *   K*   = s2 * exp(-0.5 ||(x_n - xs_t)/l||^2)       (N x Ns, training x test)
+ *   V    = L^{-1} K*
+ *   mean = c + V^T z          = c + K*^T K_hat^{-1} (y - c)
+ *   var  = s2 - colsum(V o V) = diag(K** - K*^T K_hat^{-1} K*)   (latent f, unclamped)
+ *
+ * Replaces (reference): ExactGPModel in eval mode (denoising_model/GPModel.py:10-13;
+ * SURVEY.md §3.3) -> upstream models/exact_gp.py __call__ ->
+ * exact_prediction_strategies.py exact_predictive_mean / exact_predictive_covar (diag).
+ *
+ * X : (B, N, D) float training inputs   L : (B, N, N) float   z : (B, N) float
+ * hyp : as gpk_exact_mll_f32   Xs : (B, Ns, D) float test inputs (D <= 64, N <= 256)
+ * mean, var : (B, Ns) float out
+ */
+int gpk_exact_posterior_f32(const float* X, const float* L, const float* z, const float* hyp,
+                            int n_lengthscale, const float* Xs, int B, int N, int Ns, int D,
+                            float* mean, float* var, void* stream);
+
+/*
  * Shared inducing-point factorisation of the whitened VariationalStrategy:
  *   A    = K_ZZ + jitter (fp32 add, as K_ZZ.add_jitter), then upcast to fp64
  *   L    = psd_safe_cholesky(A) with the fp64 ladder chol_jitter * 10^t

@@ -118,7 +118,8 @@ def test_custom_ops_registered_with_fake_and_autograd():
     FakeTensor impls (shape propagation without a GPU) and autograd formulas."""
     import fine_grained_gaussian_process_forcasting_amd.library  # noqa: F401
     from torch._subclasses.fake_tensor import FakeTensorMode
-    names = ["exact_mll", "exact_mll_grad", "kzz_factor", "variational_fwd", "variational_adj"]
+    names = ["exact_mll", "exact_mll_grad", "exact_posterior", "kzz_factor", "variational_fwd",
+             "variational_adj"]
     for n in names:
         assert hasattr(torch.ops.gpk, n), n
     with FakeTensorMode():
@@ -127,6 +128,8 @@ def test_custom_ops_registered_with_fake_and_autograd():
         h = torch.empty(4)
         mll, L, z, info = torch.ops.gpk.exact_mll(X, y, h, 1e-6, 3, True)
         assert mll.shape == (3,) and L.shape == (3, 16, 16) and info.dtype == torch.int32
+        pm, pv = torch.ops.gpk.exact_posterior(X, L, z, h, torch.empty(3, 40, 4))
+        assert pm.shape == (3, 40) and pv.shape == (3, 40)
         Z = torch.empty(8, 4)
         Linv, Lz, inf = torch.ops.gpk.kzz_factor(Z, torch.empty(()), torch.empty(4), 1e-4, 1e-8, 3)
         assert Linv.shape == (8, 8) and Linv.dtype == torch.float64
@@ -134,3 +137,39 @@ def test_custom_ops_registered_with_fake_and_autograd():
                                                          torch.empty(()), torch.empty(4), torch.empty(4),
                                                          torch.empty(()), 1e-4)
         assert mean.shape == (3, 16) and var.shape == (3, 16) and flags.shape == (1,)
+
+
+def test_posterior_entry_validation_without_device():
+    from fine_grained_gaussian_process_forcasting_amd import _native
+    lib = _native.lib()
+    one = ctypes.c_void_p(16)  # never dereferenced: validation returns first
+    args = [one, one, one, one, 1, one, 2, 16, 40, 4, one, one, None]
+    for idx, code in [(0, -1), (1, -2), (2, -3), (3, -4), (5, -6), (10, -11), (11, -12)]:
+        bad = list(args); bad[idx] = None
+        assert lib.gpk_exact_posterior_f32(*bad) == code
+    bad = list(args); bad[4] = 3
+    assert lib.gpk_exact_posterior_f32(*bad) == -5
+    bad = list(args); bad[7] = 257
+    assert lib.gpk_exact_posterior_f32(*bad) == -8
+    bad = list(args); bad[9] = 65
+    assert lib.gpk_exact_posterior_f32(*bad) == -10
+    bad = list(args); bad[8] = 0
+    assert lib.gpk_exact_posterior_f32(*bad) == 0    # no test points: nothing to do
+
+
+def test_exact_model_input_shapes_and_eval_guard():
+    """ExactGPModel accepts (N,), (N, D) and (B, N, D) inputs (GPyTorch's shapes); the
+    eval-mode posterior refuses to build an autograd graph it cannot differentiate."""
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.GPModel import ExactGPModel, _as_batch
+    from fine_grained_gaussian_process_forcasting_amd.gp import GaussianLikelihood
+    assert _as_batch(torch.zeros(7)).shape == (1, 7, 1)
+    assert _as_batch(torch.zeros(7, 3)).shape == (1, 7, 3)
+    assert _as_batch(torch.zeros(2, 7, 3)).shape == (2, 7, 3)
+    with pytest.raises(ValueError):
+        _as_batch(torch.zeros(1, 2, 7, 3))
+    m = ExactGPModel(torch.zeros(7, 3), torch.zeros(7), GaussianLikelihood())
+    prior = m(torch.zeros(7, 3))
+    assert prior.mean.shape == (7,) and prior._exact[0].shape == (1, 7, 3)
+    m.eval()
+    with pytest.raises(NotImplementedError, match="no_grad"):
+        m(torch.ones(5, 3))
