@@ -316,6 +316,42 @@ GPK_DEVICE f32x4 mma_tn_split_regs(const half4_t h, const half4_t l, f32x4 d) {
   return d;
 }
 
+// Panel operand of the trailing updates. GPK_SPLIT_UPDATE=1 (default): factor tiles
+// are rounded to hi + lo f16 planes (22 significant bits) and the updates run on
+// mfma_f32_16x16x32_f16 (2 MFMAs per K=16 tile product, every product exact);
+// GPK_SPLIT_UPDATE=0: fp32 tiles (24 bits) and mfma_f32_16x16x4f32 (4 MFMAs per
+// tile product). Same LDS footprint (16 B per lane per tile). DESIGN.md §4.1 states
+// the measured speed / precision trade of the two.
+#if GPK_SPLIT_UPDATE
+typedef half8_t pan_op_t;
+GPK_DEVICE pan_op_t pan_load(const float* tile, int lane) { return load_split_hl(tile, lane); }
+GPK_DEVICE f32x4 pan_mma(const pan_op_t q, const float* ptile, int lane, f32x4 d) {
+  return mma_tn_split(q, ptile, lane, d);
+}
+GPK_DEVICE f32x4 pan_store(float* tile, int lane, const f32x4 v) {
+  half4_t h, l;
+  const f32x4 o = round_split_f16(v, h, l);
+  store_split_planes(tile, lane, h, l);
+  return o;
+}
+GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) {   // d += V^T V of the rounded tile
+  half4_t h, l;
+  (void)round_split_f16(v, h, l);
+  return mma_tn_split_regs(h, l, d);
+}
+#else
+typedef f32x4 pan_op_t;
+GPK_DEVICE pan_op_t pan_load(const float* tile, int lane) { return *(const f32x4*)&tile[4 * lane]; }
+GPK_DEVICE f32x4 pan_mma(const pan_op_t q, const float* ptile, int lane, f32x4 d) {
+  return mma_tn(q, *(const f32x4*)&ptile[4 * lane], d);
+}
+GPK_DEVICE f32x4 pan_store(float* tile, int lane, const f32x4 v) {
+  *(f32x4*)&tile[4 * lane] = v;
+  return v;
+}
+GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) { return mma_tn(v, v, d); }
+#endif
+
 // Factor one 16x16 diagonal tile T in ONE wave (the diagonal wave).
 //   lanes  0-15 (column c): v[m] <- R[m][c]             (R^T R = T, upper)
 //   lanes 16-31 (column c): v[m] <- W[m][c], W = R^{-T}  (lower), started from I
@@ -567,7 +603,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // wave-specialised gets hoisted out of the attempt loop)
   auto upd_ij = [&](f32x4& d, auto I, auto J) {
     constexpr int i = decltype(I)::value, j = decltype(J)::value;
-    d = mma_tn_split(load_split_hl(pprev + i * 256, lane), pprev + j * 256, lane, d);
+    d = pan_mma(pan_load(pprev + i * 256, lane), pprev + j * 256, lane, d);
   };
   if constexpr (K > 0) {
     if constexpr (!LAST) {
@@ -588,7 +624,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     auto upd = [&](f32x4& d, auto I) {
       constexpr int s = decltype(I)::value;
       const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(wv + WK * s);
-      d = mma_tn_split(load_split_hl(pprev + (p & 255) * 256, lane), pprev + (p >> 8) * 256, lane, d);
+      d = pan_mma(pan_load(pprev + (p & 255) * 256, lane), pprev + (p >> 8) * 256, lane, d);
     };
     constexpr int Pkm1 = plan_P<NB>(K - 1);
     constexpr int NALL = Pkm1 / WK;
@@ -630,7 +666,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     for (int i = rfirst; i < NB; i += WK) {
       f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
-      d = mma_tn_split(load_split_hl(pprev + i * 256, lane), pprev + NB * 256, lane, d);
+      d = pan_mma(pan_load(pprev + i * 256, lane), pprev + NB * 256, lane, d);
       if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
     }
   }
@@ -669,9 +705,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
         const int t = wv + WK * s;
         if (t >= TLO && t <= THI) {
           const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
-          half4_t h, l;
-          const f32x4 rkj = round_split_f16(trsm_tile(q, acc[s]), h, l);
-          store_split_planes(pcur + j * 256, lane, h, l);
+          const f32x4 rkj = pan_store(pcur + j * 256, lane, trsm_tile(q, acc[s]));
           // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
           if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
         }
@@ -680,9 +714,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     if (rfirst == K) {
       f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
-      half4_t h, l;
-      const f32x4 zk = round_split_f16(trsm_tile(q, d), h, l);
-      store_split_planes(pcur + NB * 256, lane, h, l);
+      const f32x4 zk = pan_store(pcur + NB * 256, lane, trsm_tile(q, d));
       if (c == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
@@ -996,9 +1028,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         const f32x4 q = load_w(wb, c, grp);
         const f32x4 ta = *(const f32x4*)&hk[lane * 4];
         f32x4 tb = *(const f32x4*)&hk[256 + lane * 4];
-        half4_t h, l;
-        (void)round_split_f16(trsm_tile(q, ta), h, l);
-        tb = mma_tn_split_regs(h, l, tb);
+        tb = pan_self(trsm_tile(q, ta), tb);
         *(f32x4*)&dsc[lane * 4] = tb;
         if constexpr (STAMPS) {
           if (lane == 0) ((unsigned long long*)(red + 4 * W + 28))[0] += __builtin_amdgcn_s_memtime() - hw0;
