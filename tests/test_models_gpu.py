@@ -267,3 +267,8 @@ def test_custom_ops_opcheck(cuda_device):
     Xr = X.clone().requires_grad_(True)
     torch.library.opcheck(torch.ops.gpk.exact_mll.default, (Xr, y, h, 1e-6, 3, True),
                           test_utils=("test_autograd_registration",))
+    # eval-only posterior op: schema + fake impl
+    _, L, z, _ = torch.ops.gpk.exact_mll(X, y, h, 1e-6, 3, True)
+    Xs = (torch.randn(B, 30, D, generator=g) / 2).to(dev)
+    torch.library.opcheck(torch.ops.gpk.exact_posterior.default, (X, L, z, h, Xs),
+                          test_utils=("test_schema", "test_faketensor"))
