@@ -58,7 +58,7 @@ int gpk_exact_mll_grad_f32(const float* X, const float* L, const float* z, const
   if (N < 1 || N > gpk_exact_max_n()) return -7;
   if (D < 1 || D > 64) return -8;
   if (gout == nullptr) return -9;
-  if (workspace == nullptr && B > 0) return -10;
+  if (workspace == nullptr && B > 0 && gpk_exact_grad_ws_floats(B, N) > 0) return -10;
   if (dhyp == nullptr) return -13;
   if (B == 0) return 0;
   GpkExactGradArgs a{X, L, z, hyp, n_lengthscale, B, N, D, gout, (float*)workspace, dX, dy, dhyp};

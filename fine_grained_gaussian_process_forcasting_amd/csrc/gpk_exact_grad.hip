@@ -14,47 +14,70 @@
 // linear_operator inv_quad_logdet + psd_safe_cholesky backward) when train.py:166
 // calls loss.backward(); oracle: oracle/gp_oracle.py::exact_mll_grads.
 //
-// Inputs are the forward's outputs (L, z), so nothing is refactored. One workgroup
-// (8 waves) per window, three phases separated by workgroup barriers:
-//   0. inverses of the 16 diagonal blocks of L (forward substitution, one lane
-//      per column, L entries read as uniform scalars);
-//   1. L^-1 by block columns (wave w owns columns J = w mod 8):
-//      Linv_IJ = -Linv_II sum_{K=J}^{I-1} L_IK Linv_KJ   (fp32 MFMA 16x16x4),
-//      tiles kept in a caller workspace in acc layout (one float4 per lane);
-//   2. alpha = Linv^T z; then for every tile (I <= J): K^-1_IJ = sum_K Linv_KI^T
-//      Linv_KJ, G, the RBF recomputed from xs (MFMA Gram), and the reductions:
-//      ds2 / dnoise in registers, w1 and Wx = W xs (both MFMA orientations) as
-//      LDS float atomics;
-//   3. per-row dx, dy and the lengthscale sums.
+// Design: one workgroup of 8 waves per window, inputs are the forward's
+// L and z (nothing is refactored, no workspace). Block column J of K^-1 (lower part,
+// rows I >= J) is produced by ONE wave with its tiles held in registers (acc layout):
+//   forward   V = L^-1 e_J       V_I = -Linv_II sum_{K=J}^{I-1} L_IK V_K   (rows I >= J)
+//   backward  U = L^-T V         U_I =  Linv_II^T (V_I - sum_{K>I} L_KI^T U_K), I = NB-1..J
+// (fp32 MFMA; L tiles are read straight from L2 as MFMA A operands, the 16 diagonal-block
+// inverses Linv_II live in LDS), and every tile U_I = K^-1_IJ is consumed as soon as it
+// is final: the RBF tile is recomputed (fp32-MFMA Gram of the LDS-staged xs), and
+//   column side (rows of J, in registers):  w1_J += colsum W_IJ,  Wx_J += W_IJ^T xs_I
+//   row side (rows of I > J, LDS adds):     w1_I += rowsum W_IJ,  Wx_I += W_IJ xs_J
+// Only the lower half of K^-1 is formed (N^3/3 flops for both solves). Columns are
+// dealt to waves in mirrored pairs (w, NB-1-w) to balance the (NB-J)^2 work.
 #include "gpk_common.h"
 #include "gpk_internal.h"
+
+#include <mutex>
 
 namespace {
 
 constexpr int kNW = 8;           // waves per workgroup (one window)
 constexpr int kT = 64 * kNW;
 
-// acc-layout tile of L^T for block (I, K): lane (g, c) reg r <- L[16I + c][16K + 4g + r]
-// (padding beyond N is the identity).
-GPK_DEVICE f32x4 load_LT(const float* Lb, int N, int I, int K, int lane) {
-  const int c = lane & 15, g = lane >> 4;
-  const int row = 16 * I + c, col = 16 * K + 4 * g;
-  f32x4 v;
-  if ((N & 3) == 0 && row < N && col + 3 < N) {
-    v = *(const f32x4*)&Lb[(size_t)row * N + col];
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      v[r] = (row < N && col + r < N) ? Lb[(size_t)row * N + col + r] : (row == col + r ? 1.f : 0.f);
-  }
-  return v;
+struct GradLds {
+  int xs, wx, dinv, w1, alpha, sv, nrm, tsc, red, total;   // float offsets
+};
+
+// xs row stride: padded by 4 floats for DP <= 32; at DP = 64 (LDS-bound) unpadded with
+// the 16-B column groups XOR-swizzled by row instead (xs_at)
+__host__ __device__ constexpr int grad_xs_stride(int DP) { return DP == 64 ? DP : DP + 4; }
+
+template <int DP>
+GPK_DEVICE int xs_at(int n, int d) {
+  if constexpr (DP == 64) return n * DP + (d ^ ((n & 15) << 2));
+  else return n * (DP + 4) + d;
+}
+// same, for row n = i16 + m with i16 a multiple of 16 and m < 16
+template <int DP>
+GPK_DEVICE int xs_at2(int i16, int m, int d) {
+  if constexpr (DP == 64) return (i16 + m) * DP + (d ^ (m << 2));
+  else return (i16 + m) * (DP + 4) + d;
 }
 
-GPK_DEVICE f32x4 ws_load(const float* ws, int NB, int I, int J, int lane) {
-  return *(const f32x4*)&ws[((size_t)(I * NB + J) * 64 + lane) * 4];
+__host__ __device__ inline GradLds grad_lds_layout(int NB, int DP) {
+  GradLds o;
+  const int NP = 16 * NB, XS = grad_xs_stride(DP);
+  o.xs = 0;                         // NP x XS   centred x / l (zero padded)
+  o.wx = o.xs + NP * XS;            // NP x DP   Wx (prologue: staged diagonal blocks of L)
+  o.dinv = o.wx + NP * DP;          // NB x 16 x 16, row-major Linv_II
+  o.w1 = o.dinv + NB * 256;         // NP
+  o.alpha = o.w1 + NP;              // NP
+  o.sv = o.alpha + NP;              // NP   back-substitution right-hand side
+  o.nrm = o.sv + NP;                // NP   ||xs_n||^2
+  o.tsc = o.nrm + NP;               // kNW x 256 per-wave transpose scratch
+  o.red = o.tsc + kNW * 256;        // 256 reductions
+  o.total = o.red + 256;
+  return o;
 }
-GPK_DEVICE void ws_store(float* ws, int NB, int I, int J, int lane, const f32x4 v) {
-  *(f32x4*)&ws[((size_t)(I * NB + J) * 64 + lane) * 4] = v;
+
+GPK_DEVICE f32x4 mfma4(const f32x4 a, const f32x4 b, f32x4 d) {
+  d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], d, 0, 0, 0);
+  return d;
 }
 
 GPK_DEVICE void lds_add(float* p, float v) {
@@ -70,259 +93,329 @@ GPK_DEVICE float row16_sum(float v) {
   return v;
 }
 
-template <int NB>
-__global__ void __launch_bounds__(kT, 1)
-gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
-                      const float* __restrict__ zg, const float* __restrict__ hyp, int n_ls,
-                      int N, int D, int DP, const float* __restrict__ gout,
-                      float* __restrict__ ws_all, float* __restrict__ dX, float* __restrict__ dy,
-                      float* __restrict__ dhyp) {
-  constexpr int NP = NB * 16;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* dinvT = smem;                 // NB tiles: acc layout of Linv_II^T
-  float* xs = dinvT + NB * 256;        // NP x DP, centred x / l
-  float* Wx = xs + NP * DP;            // NP x DP
-  float* w1 = Wx + NP * DP;            // NP
-  float* alpha = w1 + NP;              // NP
-  float* nrm = alpha + NP;             // NP
-  float* scr = nrm + NP;               // kNW waves x 256 (transposes)
-  float* part = scr + kNW * 256;       // kT partial sums
-  float* red = part + kT;              // 3 * kNW
+// Uniform value the compiler must treat as unknown at this point: keeps per-tile
+// addresses from being hoisted out of the column loop (hundreds of live 64-bit
+// addresses would spill).
+GPK_DEVICE int opaque_s(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
 
+// A operand L_IK (lane (c, g), step r: L[16I + c][16K + 4g + r]); padding = identity.
+// FULL: one 16-B load at (scalar tile base) + (per-lane offset c N + 4g).
+template <bool FULL>
+GPK_DEVICE f32x4 load_L_rows(const float* Lb, int N, int I, int K, int c, int g) {
+  if (FULL) {
+    const float* t = Lb + opaque_s(16 * I * N + 16 * K);
+    return *(const f32x4*)&t[c * N + 4 * g];
+  }
+  // (masks from laundered block offsets: hoisted per-site lane masks would spill SGPRs)
+  const int i16 = opaque_s(16 * I), k16 = opaque_s(16 * K);
+  const int row = i16 + c, col = k16 + 4 * g;
+  f32x4 v;
+  const float* t = Lb + i16 * N;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    v[r] = (row < N && col + r < N) ? t[c * N + col + r] : (row == col + r ? 1.f : 0.f);
+  return v;
+}
+
+// A operand L_KI^T (lane (c, g), step r: L[16K + 4g + r][16I + c])
+template <bool FULL>
+GPK_DEVICE f32x4 load_L_cols(const float* Lb, int N, int K, int I, int c, int g) {
+  f32x4 v;
+  if (FULL) {
+    const float* t = Lb + opaque_s(16 * K * N + 16 * I) + 4 * g * N + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = t[r * N];
+    return v;
+  }
+  const int i16 = opaque_s(16 * I), k16 = opaque_s(16 * K);
+  const int col = i16 + c;
+  const float* t = Lb + k16 * N;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = k16 + 4 * g + r;
+    v[r] = (row < N && col < N) ? t[(4 * g + r) * N + col] : (row == col ? 1.f : 0.f);
+  }
+  return v;
+}
+
+template <int NB, int DQ, bool FULL>
+__global__ void __launch_bounds__(kT, 1) gpk_exact_grad_kernel(GpkExactGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int DP = 16 * DQ, NP = 16 * NB;
+  const GradLds lay = grad_lds_layout(NB, DP);
+  float* xs = smem + lay.xs;
+  float* wx = smem + lay.wx;
+  float* dinv = smem + lay.dinv;
+  float* w1 = smem + lay.w1;
+  float* alpha = smem + lay.alpha;
+  float* sv = smem + lay.sv;
+  float* nrm = smem + lay.nrm;
+  float* red = smem + lay.red;
+
+  const int N = FULL ? NP : a.N;
+  const int D = a.D;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
   const int b = blockIdx.x;
-  const float* Lb = Lg + (size_t)b * N * N;
-  float* ws = ws_all + (size_t)b * NB * NB * 256;
+  const float* Lb = a.L + (size_t)b * N * N;
+  const float* hyp = a.hyp;
+  const int n_ls = a.n_ls;
   const float s2 = hyp[0];
-  const float gw = gout[b];
+  const float gw = a.gout[b];
   const float gs = gw / (2.f * (float)N);
 
-  // ---- 0. diagonal block inverses: lane c < 16 solves column c of L_II X = I
-  for (int I = wave; I < NB; I += kNW) {
-    if (lane < 16) {
+  // ---- prologue: stage the diagonal blocks of L, xs = x / l, z
+  {
+    const int bi = tid >> 4, m = tid & 15;
+    if (bi < NB) {
+      const int row = 16 * bi + m;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int col = 16 * bi + k;
+        float v = (row == col) ? 1.f : 0.f;
+        if (k <= m && row < N) v = Lb[(size_t)row * N + col];
+        wx[bi * 256 + m * 16 + k] = v;
+      }
+    }
+  }
+  for (int e = tid; e < NP * DP; e += kT) {
+    const int n = e / DP, d = e - n * DP;
+    float v = 0.f;
+    if (n < N && d < D) v = a.X[((size_t)b * N + n) * D + d] / hyp[3 + (n_ls == 1 ? 0 : d)];
+    xs[xs_at<DP>(n, d)] = v;
+  }
+  for (int n = tid; n < NP; n += kT) {
+    sv[n] = n < N ? a.z[(size_t)b * N + n] : 0.f;
+    w1[n] = 0.f;
+  }
+  lds_barrier();
+  {  // column sums of xs (partials) and the diagonal-block inverses
+    constexpr int P = kT / DP;
+    const int d = tid % DP, part = tid / DP;
+    float s = 0.f;
+    for (int n = part; n < N; n += P) s += xs[xs_at<DP>(n, d)];
+    smem[lay.tsc + tid] = s;
+    const int bi = tid >> 4, cc = tid & 15;
+    if (bi < NB) {
+      const float* Lt = wx + bi * 256;
       float x[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int gi = 16 * I + i;
-        float s = (i == c) ? 1.f : 0.f;
+      for (int m = 0; m < 16; ++m) {
+        float t = (m == cc) ? 1.f : 0.f;
 #pragma unroll
-        for (int k = 0; k < i; ++k) {
-          const int gk = 16 * I + k;
-          const float lik = (gi < N && gk < N) ? Lb[(size_t)gi * N + gk] : 0.f;
-          s = __builtin_fmaf(-lik, x[k], s);
-        }
-        const float lii = (gi < N) ? Lb[(size_t)gi * N + gi] : 1.f;
-        x[i] = s / lii;
+        for (int k = 0; k < m; ++k) t = __builtin_fmaf(-Lt[m * 16 + k], x[k], t);
+        x[m] = (m < cc) ? 0.f : t / Lt[m * 16 + m];
       }
-      // Linv_II (acc layout) -> workspace; Linv_II^T (acc layout) -> LDS
-      float* t = dinvT + I * 256;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) t[(16 * (c >> 2) + i) * 4 + (c & 3)] = x[i];  // X^T[c][i]
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        ws[((size_t)(I * NB + I) * 64 + 16 * (i >> 2) + c) * 4 + (i & 3)] = x[i];  // X[i][c]
+      for (int m = 0; m < 16; ++m) dinv[bi * 256 + m * 16 + cc] = x[m];
     }
   }
-  __syncthreads();
+  lds_barrier();
+  if (tid < DP) {
+    float s = 0.f;
+    for (int p = 0; p < kT / DP; ++p) s += smem[lay.tsc + p * DP + tid];
+    red[tid] = s / (float)N;
+  }
+  for (int e = tid; e < NP * DP; e += kT) wx[e] = 0.f;
+  lds_barrier();
+  for (int e = tid; e < N * DP; e += kT) {
+    const int n = e / DP, d = e - n * DP;
+    if (d < D) xs[xs_at<DP>(n, d)] -= red[d];
+  }
+  lds_barrier();
+  for (int n = tid; n < NP; n += kT) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < DP; ++d) s = __builtin_fmaf(xs[xs_at<DP>(n, d)], xs[xs_at<DP>(n, d)], s);
+    nrm[n] = s;
+  }
+  // alpha = L^-T z: blocked back substitution (alpha_I = Linv_II^T s_I, then s_i -= L_Ii^T alpha_I)
+  for (int I = NB - 1; I >= 0; --I) {
+    if (tid < 16) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) t = __builtin_fmaf(dinv[I * 256 + k * 16 + tid], sv[16 * I + k], t);
+      alpha[16 * I + tid] = t;
+    }
+    lds_barrier();
+    if (tid < 16 * I) {
+      float t = sv[tid];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int row = 16 * I + k;
+        if (FULL || row < N) t = __builtin_fmaf(-Lb[(size_t)row * N + tid], alpha[row], t);
+      }
+      sv[tid] = t;
+    }
+    lds_barrier();
+  }
 
-  // ---- 1. block columns of L^-1
-  for (int J = wave; J < NB; J += kNW) {
-    for (int I = J + 1; I < NB; ++I) {
-      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-      int K = J;
-      for (; K + 1 < I; K += 2) {
-        const f32x4 a0 = load_LT(Lb, N, I, K, lane), p0 = ws_load(ws, NB, K, J, lane);
-        const f32x4 a1 = load_LT(Lb, N, I, K + 1, lane), p1 = ws_load(ws, NB, K + 1, J, lane);
-        s0 = mma_tn(a0, p0, s0);
-        s1 = mma_tn(a1, p1, s1);
-      }
-      if (K < I) s0 = mma_tn(load_LT(Lb, N, I, K, lane), ws_load(ws, NB, K, J, lane), s0);
-      const f32x4 qt = *(const f32x4*)&dinvT[I * 256 + lane * 4];
-      const f32x4 v = mma_tn(qt, s0 + s1, f32x4{0.f, 0.f, 0.f, 0.f});
-      ws_store(ws, NB, I, J, lane, -v);
-    }
-  }
-  // ---- 2a. xs = x / l (centred over the N real rows), norms, zeroed accumulators
-  for (int q = tid; q < NP * DP; q += kT) {
-    const int n = q / DP, d = q - n * DP;
-    float v = 0.f;
-    if (n < N && d < D) v = X[((size_t)b * N + n) * D + d] / hyp[3 + (n_ls == 1 ? 0 : d)];
-    xs[q] = v;
-    Wx[q] = 0.f;
-  }
-  for (int q = tid; q < NP; q += kT) w1[q] = 0.f;
-  __syncthreads();  // also publishes the workspace tiles of phase 1
-  {
-    const int parts = kT / DP;
-    const int p = tid / DP, d = tid - p * DP;
-    if (p < parts) {
-      float s = 0.f;
-      for (int n = p; n < N; n += parts) s += xs[n * DP + d];
-      part[p * DP + d] = s;
-    }
-    __syncthreads();
-    if (tid < DP) {
-      float s = 0.f;
-      for (int q = 0; q < parts; ++q) s += part[q * DP + tid];
-      part[kT - DP + tid] = s / (float)N;  // (only read after the barrier below)
-    }
-    __syncthreads();
-    for (int q = tid; q < N * DP; q += kT) {
-      const int d = q % DP;
-      if (d < D) xs[q] -= part[kT - DP + d];
-    }
-    __syncthreads();
-    for (int n = tid; n < NP; n += kT) {
-      float s = 0.f;
-      for (int d = 0; d < DP; ++d) s = __builtin_fmaf(xs[n * DP + d], xs[n * DP + d], s);
-      nrm[n] = s;
-    }
-  }
-  // alpha = L^-T z (block rows I = wave mod 4); column 0 of each Z tile is live
-  for (int I = wave; I < NB; I += kNW) {
-    f32x4 a = {0.f, 0.f, 0.f, 0.f};
-    for (int K = I; K < NB; ++K) {
-      f32x4 zt;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * K + 4 * g + r;
-        zt[r] = (c == 0 && row < N) ? zg[(size_t)b * N + row] : 0.f;
-      }
-      a = mma_tn(ws_load(ws, NB, K, I, lane), zt, a);
-    }
-    if (c == 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) alpha[16 * I + 4 * g + r] = a[r];
-    }
-  }
-  __syncthreads();
-
-  // ---- 2b. tiles (I <= J)
+  // ---- block columns of K^-1 (lower part) and their consumers
+  constexpr float nhalf_log2e = -0.72134752044448170f;
+  float* tsc = smem + lay.tsc + wave * 256;
   float ds2 = 0.f, dnz = 0.f;
-  float* sc = scr + wave * 256;
-  int t = 0;
-  for (int J = 0; J < NB; ++J) {
-    for (int I = 0; I <= J; ++I, ++t) {
-      if (t % kNW != wave) continue;
-      // K^-1_IJ
-      f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = {0.f, 0.f, 0.f, 0.f};
-      int K = J;
-      for (; K + 1 < NB; K += 2) {
-        const f32x4 a0 = ws_load(ws, NB, K, I, lane), b0 = ws_load(ws, NB, K, J, lane);
-        const f32x4 a1 = ws_load(ws, NB, K + 1, I, lane), b1 = ws_load(ws, NB, K + 1, J, lane);
-        k0 = mma_tn(a0, b0, k0);
-        k1 = mma_tn(a1, b1, k1);
-      }
-      if (K < NB) k0 = mma_tn(ws_load(ws, NB, K, I, lane), ws_load(ws, NB, K, J, lane), k0);
-      const f32x4 kinv = k0 + k1;
-      // Gram of xs rows (contraction over d in chunks of 16)
-      f32x4 gr = {0.f, 0.f, 0.f, 0.f};
-      for (int dd = 0; dd < DP; dd += 16) {
-        const f32x4 qi = *(const f32x4*)&xs[(16 * I + c) * DP + dd + 4 * g];
-        const f32x4 qj = *(const f32x4*)&xs[(16 * J + c) * DP + dd + 4 * g];
-        gr = mma_tn(qi, qj, gr);
-      }
-      const int col = 16 * J + c;
-      const float aj = alpha[col], nj = nrm[col];
-      f32x4 W;
-      float csum = 0.f;
+  const int ncol = (NB > kNW && NB - 1 - wave >= kNW) ? 2 : (wave < NB ? 1 : 0);
+  for (int ci = 0; ci < ncol; ++ci) {
+    const int J = __builtin_amdgcn_readfirstlane(ci == 0 ? wave : NB - 1 - wave);
+    f32x4 V[NB];
+    // forward: V = L^-1 e_J (block rows I >= J)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * I + 4 * g + r;
-        float G = (alpha[row] * aj - kinv[r]) * gs;
-        if (row >= N || col >= N) G = 0.f;
-        float dist = nrm[row] + nj - 2.f * gr[r];
-        dist = dist < 0.f ? 0.f : dist;
-        if (row == col) dist = 0.f;
-        const float E = __expf(-0.5f * dist);
-        ds2 += (I == J ? 1.f : 2.f) * G * E;
-        if (row == col) dnz += G;
-        float w = G * s2 * E;
-        if (row == col) w = 0.f;
-        W[r] = w;
-        csum += w;
-      }
-      // w1: row sums (rows of block I) and, off the diagonal, column sums (rows of J)
+    for (int I = 0; I < NB; ++I) {
+      const int I16 = opaque_s(16 * I);   // per-step LDS offsets stay in place
+      if (I == J) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float rs = row16_sum(W[r]);
-        if (c == 0) lds_add(&w1[16 * I + 4 * g + r], rs);
-      }
-      if (I != J) lds_add(&w1[col], csum);
-      // Wx_J += W^T xs_I ; Wx_I += W xs_J (I != J)
-      *(f32x4*)&sc[lane * 4] = W;  // for the transpose below
-      for (int dd = 0; dd < DP; dd += 16) {
-        f32x4 pi;
+        for (int r = 0; r < 4; ++r) V[I][r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
+      } else if (I > J) {
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pi[r] = xs[(16 * I + 4 * g + r) * DP + dd + c];
-        const f32x4 o = mma_tn(W, pi, f32x4{0.f, 0.f, 0.f, 0.f});  // rows j, dims dd + c
-#pragma unroll
-        for (int r = 0; r < 4; ++r) lds_add(&Wx[(16 * J + 4 * g + r) * DP + dd + c], o[r]);
+        for (int K = 0; K < I; ++K) {
+          if (K >= J) {
+            const f32x4 la = load_L_rows<FULL>(Lb, N, I, K, c, g);
+            if (K & 1) s1 = mfma4(la, V[K], s1);
+            else s0 = mfma4(la, V[K], s0);
+          }
+        }
+        const f32x4 di = *(const f32x4*)&dinv[I16 * 16 + c * 16 + 4 * g];
+        const f32x4 z0 = {0.f, 0.f, 0.f, 0.f};
+        V[I] = -mfma4(di, s0 + s1, z0);
       }
-      if (I != J) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-        f32x4 wt;  // acc layout of W^T: W^T[4g + r][c] = W[c][4g + r]
+    }
+    // per-column operands: xs_J as Gram B operand and as the row-side B operand
+    f32x4 xj[DQ], pj[DQ], wxj[DQ];
+#pragma unroll
+    for (int q = 0; q < DQ; ++q) {
+      xj[q] = *(const f32x4*)&xs[xs_at<DP>(16 * J + c, 16 * q + 4 * g)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pj[q][r] = xs[xs_at<DP>(16 * J + 4 * g + r, 16 * q + c)];
+      wxj[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int col = 16 * J + c;
+    const float aj = alpha[col], nj = nrm[col];
+    float w1c = 0.f;
+    // backward: U = L^-T V, I = NB-1 .. J, each final tile consumed at once
+#pragma unroll
+    for (int I = NB - 1; I >= 0; --I) {
+      if (I >= J) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int I16 = opaque_s(16 * I);
+        f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int K = I + 1; K < NB; ++K) {
+          const f32x4 la = load_L_cols<FULL>(Lb, N, K, I, c, g);
+          if (K & 1) s1 = mfma4(la, V[K], s1);
+          else s0 = mfma4(la, V[K], s0);
+        }
+        const f32x4 t = V[I] - s0 - s1;
+        f32x4 dt;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
+        const f32x4 z0 = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 U = mfma4(dt, t, z0);
+        V[I] = U;
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- consume K^-1_IJ = U (rows 16I + 4g + r, column col)
+        f32x4 gr = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < DQ; ++q)
+          gr = mfma4(*(const f32x4*)&xs[xs_at2<DP>(I16, c, 16 * q + 4 * g)], xj[q], gr);
+        f32x4 W;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int a = c, bb = 4 * g + r;  // element W[a][bb]
-          wt[r] = sc[(16 * (a >> 2) + bb) * 4 + (a & 3)];
+          const int row = I16 + 4 * g + r;
+          const int lrow = row;
+          float G = (alpha[lrow] * aj - U[r]) * gs;
+          if (!FULL && (row >= N || col >= N)) G = 0.f;
+          float d2 = __builtin_fmaxf(nrm[lrow] + nj - 2.f * gr[r], 0.f);
+          if (row == col) d2 = 0.f;
+          const float E = __builtin_amdgcn_exp2f(d2 * nhalf_log2e);
+          ds2 = __builtin_fmaf((I == J ? 1.f : 2.f) * G, E, ds2);
+          if (row == col) dnz += G;
+          W[r] = (row == col) ? 0.f : G * s2 * E;
         }
-        for (int dd = 0; dd < DP; dd += 16) {
-          f32x4 pj;
+        // column side: rows of J
+        w1c += (W[0] + W[1]) + (W[2] + W[3]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) pj[r] = xs[(16 * J + 4 * g + r) * DP + dd + c];
-          const f32x4 o = mma_tn(wt, pj, f32x4{0.f, 0.f, 0.f, 0.f});  // rows i
+        for (int q = 0; q < DQ; ++q) {
+          f32x4 p;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) lds_add(&Wx[(16 * I + 4 * g + r) * DP + dd + c], o[r]);
+          for (int r = 0; r < 4; ++r) p[r] = xs[xs_at2<DP>(I16, 4 * g + r, 16 * q + c)];
+          wxj[q] = mfma4(W, p, wxj[q]);
+        }
+        // row side: rows of I (off-diagonal tiles only)
+        if (I > J) {
+          *(f32x4*)&tsc[lane * 4] = W;
+          wave_lds_sync();
+          f32x4 wt;   // acc layout of W^T: reg r = W[c][4g + r]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int e = 4 * g + r;
+            wt[r] = tsc[((c >> 2) * 16 + e) * 4 + (c & 3)];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float rs = row16_sum(W[r]);
+            if (c == 0) lds_add(&w1[I16 + 4 * g + r], rs);
+          }
+#pragma unroll
+          for (int q = 0; q < DQ; ++q) {
+            const f32x4 z0 = {0.f, 0.f, 0.f, 0.f};
+            const f32x4 o = mfma4(wt, pj[q], z0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) lds_add(&wx[(I16 + 4 * g + r) * DP + 16 * q + c], o[r]);
+          }
+          wave_lds_sync();   // tsc is rewritten by the next tile
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
+    w1c += __shfl_xor(w1c, 16, 64);
+    w1c += __shfl_xor(w1c, 32, 64);
+    if (g == 0) lds_add(&w1[col], w1c);
+#pragma unroll
+    for (int q = 0; q < DQ; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lds_add(&wx[(16 * J + 4 * g + r) * DP + 16 * q + c], wxj[q][r]);
   }
   ds2 = wave_sum(ds2);
   dnz = wave_sum(dnz);
   if (lane == 0) {
-    red[wave] = ds2;
-    red[kNW + wave] = dnz;
+    red[DP + wave] = ds2;
+    red[DP + kNW + wave] = dnz;
   }
+  for (int q = tid; q < DP; q += kT) red[DP + 3 * kNW + q] = 0.f;
   __syncthreads();
 
-  // ---- 3. per-row outputs and the lengthscale / constant sums
+  // ---- per-row outputs and the lengthscale / constant sums
   const float invN = 1.f / (float)N;
   float asum = 0.f;
   for (int n = tid; n < N; n += kT) {
     const float an = alpha[n];
     asum += an;
-    if (dy != nullptr) dy[(size_t)b * N + n] = -gw * an * invN;
+    if (a.dy != nullptr) a.dy[(size_t)b * N + n] = -gw * an * invN;
   }
-  // thread (row n) accumulates xs_nd (xs_nd w1_n - Wx_nd) per d into part[d] via atomics
-  for (int q = tid; q < DP; q += kT) part[q] = 0.f;
-  __syncthreads();
-  for (int n = tid; n < N; n += kT) {
-    const float wn = w1[n];
-    for (int d = 0; d < D; ++d) {
-      const float x = xs[n * DP + d];
-      const float e = x * wn - Wx[n * DP + d];  // = -dxs / 2
-      const float l = hyp[3 + (n_ls == 1 ? 0 : d)];
-      if (dX != nullptr) dX[((size_t)b * N + n) * D + d] = -2.f * e / l;
-      lds_add(&part[d], x * e);
+  float* part = red + DP + 3 * kNW;
+  for (int e = tid; e < N * DP; e += kT) {
+    const int n = e / DP, d = e - n * DP;
+    if (d < D) {
+      const float x = xs[xs_at<DP>(n, d)];
+      const float ee = x * w1[n] - wx[n * DP + d];  // = -dxs / 2
+      if (a.dX != nullptr) a.dX[((size_t)b * N + n) * D + d] = -2.f * ee / hyp[3 + (n_ls == 1 ? 0 : d)];
+      lds_add(&part[d], x * ee);
     }
   }
   asum = wave_sum(asum);
-  if (lane == 0) red[2 * kNW + wave] = asum;
+  if (lane == 0) red[DP + 2 * kNW + wave] = asum;
   __syncthreads();
   if (tid == 0) {
-    float* o = dhyp + (size_t)b * (3 + n_ls);
+    float* o = a.dhyp + (size_t)b * (3 + n_ls);
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     for (int w = 0; w < kNW; ++w) {
-      a0 += red[w];
-      a1 += red[kNW + w];
-      a2 += red[2 * kNW + w];
+      a0 += red[DP + w];
+      a1 += red[DP + kNW + w];
+      a2 += red[DP + 2 * kNW + w];
     }
     o[0] = a0;
     o[1] = a1;
@@ -337,36 +430,44 @@ gpk_exact_grad_kernel(const float* __restrict__ X, const float* __restrict__ Lg,
   }
 }
 
+template <int NB, int DQ, bool FULL>
+int launch_grad(const GpkExactGradArgs& a, hipStream_t stream) {
+  const GradLds lay = grad_lds_layout(NB, 16 * DQ);
+  const size_t lds = (size_t)lay.total * sizeof(float);
+  if (lds > 160 * 1024) return -8;
+  static std::once_flag once;
+  std::call_once(once, [&] {
+    (void)hipFuncSetAttribute((const void*)gpk_exact_grad_kernel<NB, DQ, FULL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipGetLastError();
+  });
+  hipLaunchKernelGGL((gpk_exact_grad_kernel<NB, DQ, FULL>), dim3(a.B), dim3(kT), lds, stream, a);
+  return (int)hipGetLastError();
+}
+
 template <int NB>
 int launch_grad_nb(const GpkExactGradArgs& a, hipStream_t stream) {
-  const int DP = (a.D + 15) / 16 * 16;
-  if (DP > 64) return -7;
-  const size_t lds = sizeof(float) * ((size_t)NB * 256 + 2 * (size_t)NB * 16 * DP + 3 * NB * 16 + kNW * 256 + kT + 3 * kNW);
-  if (lds > 160 * 1024) return -7;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)gpk_exact_grad_kernel<NB>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((gpk_exact_grad_kernel<NB>), dim3(a.B), dim3(kT), lds, stream, a.X, a.L, a.z,
-                     a.hyp, a.n_ls, a.N, a.D, DP, a.gout, a.ws, a.dX, a.dy, a.dhyp);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : (int)e;
+  const bool full = a.N == 16 * NB;
+  if (a.D <= 16) return full ? launch_grad<NB, 1, true>(a, stream) : launch_grad<NB, 1, false>(a, stream);
+  if (a.D <= 32) return full ? launch_grad<NB, 2, true>(a, stream) : launch_grad<NB, 2, false>(a, stream);
+  return full ? launch_grad<NB, 4, true>(a, stream) : launch_grad<NB, 4, false>(a, stream);
 }
 
 }  // namespace
 
 size_t gpk_exact_grad_ws_floats(int B, int N) {
-  const size_t NB = (size_t)(N + 15) / 16;
-  return (size_t)B * NB * NB * 256;
+  (void)B;
+  (void)N;
+  return 0;   // the adjoint keeps L^-1 in registers: no workspace
 }
 
 int gpk_launch_exact_grad(const GpkExactGradArgs& a, hipStream_t stream) {
-  const int NB = (a.N + 15) / 16;
-  switch (NB) {
+  switch ((a.N + 15) / 16) {
 #define GPK_CASE(nb) case nb: return launch_grad_nb<nb>(a, stream);
     GPK_CASE(1) GPK_CASE(2) GPK_CASE(3) GPK_CASE(4) GPK_CASE(5) GPK_CASE(6)
     GPK_CASE(7) GPK_CASE(8) GPK_CASE(9) GPK_CASE(10) GPK_CASE(11) GPK_CASE(12)
     GPK_CASE(13) GPK_CASE(14) GPK_CASE(15) GPK_CASE(16)
 #undef GPK_CASE
-    default: return -6;
+    default: return -7;
   }
 }
