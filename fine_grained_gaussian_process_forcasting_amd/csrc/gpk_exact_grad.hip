@@ -14,18 +14,19 @@
 // linear_operator inv_quad_logdet + psd_safe_cholesky backward) when train.py:166
 // calls loss.backward(); oracle: oracle/gp_oracle.py::exact_mll_grads.
 //
-// Design: one workgroup of 8 waves per window, inputs are the forward's
-// L and z (nothing is refactored, no workspace). Block column J of K^-1 (lower part,
-// rows I >= J) is produced by ONE wave with its tiles held in registers (acc layout):
-//   forward   V = L^-1 e_J       V_I = -Linv_II sum_{K=J}^{I-1} L_IK V_K   (rows I >= J)
-//   backward  U = L^-T V         U_I =  Linv_II^T (V_I - sum_{K>I} L_KI^T U_K), I = NB-1..J
-// (fp32 MFMA; L tiles are read straight from L2 as MFMA A operands, the 16 diagonal-block
-// inverses Linv_II live in LDS), and every tile U_I = K^-1_IJ is consumed as soon as it
-// is final: the RBF tile is recomputed (fp32-MFMA Gram of the LDS-staged xs), and
-//   column side (rows of J, in registers):  w1_J += colsum W_IJ,  Wx_J += W_IJ^T xs_I
-//   row side (rows of I > J, LDS adds):     w1_I += rowsum W_IJ,  Wx_I += W_IJ xs_J
-// Only the lower half of K^-1 is formed (N^3/3 flops for both solves). Columns are
-// dealt to waves in mirrored pairs (w, NB-1-w) to balance the (NB-J)^2 work.
+// Three launches, inputs are the forward's L and z (nothing is refactored):
+//   gpk_grad_solve_kernel  one workgroup (16 waves) per window: alpha = L^-T z, dy, and the
+//       lower block tiles of K^-1: wave J solves block column J with its tiles in registers
+//         forward   V_I = -Linv_II sum_{K=J}^{I-1} L_IK V_K       (I > J, V_J = Linv_JJ)
+//         backward  U_I =  Linv_II^T (V_I - sum_{K>I} L_KI^T U_K)  (I = NB-1 .. J)
+//       fp32 MFMA; all waves step together and each step's block row / column of L is
+//       staged once in LDS by the workgroup, fetched two steps ahead (double buffer);
+//       the diagonal-block inverses Linv_II live in LDS. U_I = K^-1_IJ -> workspace.
+//   gpk_grad_gram_kernel   one wave per (window, block row I), no atomics: for every J the
+//       tile K^-1_JI (stored, or the transpose of the stored K^-1_IJ), the RBF tile
+//       recomputed from xs (fp32-MFMA Gram), G, W and Wx_I += W_JI^T xs_J (MFMA), w1_I;
+//       then dX of rows I and the block row's partials of ds2, dnoise, dl.
+//   gpk_grad_fin_kernel    fixed-order sums of the partials -> dhyp (deterministic).
 #include "gpk_common.h"
 #include "gpk_internal.h"
 
@@ -33,44 +34,29 @@
 
 namespace {
 
-constexpr int kNW = 8;           // waves per workgroup (one window)
-constexpr int kT = 64 * kNW;
+constexpr int kSW = 16;          // waves of the solve kernel (one block column each)
+constexpr int kST = 64 * kSW;
+constexpr int kMaxD = 64;
 
-struct GradLds {
-  int xs, wx, dinv, w1, alpha, sv, nrm, tsc, red, total;   // float offsets
+// ---- workspace layout (floats, per window) -------------------------------------------
+struct GradWs {
+  int NB, NT, kinv, alpha, mean, asum, part, per;
 };
-
-// xs row stride: padded by 4 floats for DP <= 32; at DP = 64 (LDS-bound) unpadded with
-// the 16-B column groups XOR-swizzled by row instead (xs_at)
-__host__ __device__ constexpr int grad_xs_stride(int DP) { return DP == 64 ? DP : DP + 4; }
-
-template <int DP>
-GPK_DEVICE int xs_at(int n, int d) {
-  if constexpr (DP == 64) return n * DP + (d ^ ((n & 15) << 2));
-  else return n * (DP + 4) + d;
+__host__ __device__ inline GradWs grad_ws(int N) {
+  GradWs w;
+  w.NB = (N + 15) / 16;
+  w.NT = w.NB * (w.NB + 1) / 2;
+  w.kinv = 0;                           // NT tiles x 256: lower tiles (I >= J), row-major
+                                        // tile order, each in acc layout (lane-major float4)
+  w.alpha = w.kinv + w.NT * 256;        // NP
+  w.mean = w.alpha + 16 * w.NB;         // kMaxD: column means of x / l
+  w.asum = w.mean + kMaxD;              // 4: sum(alpha)
+  w.part = w.asum + 4;                  // NB x (2 + kMaxD): ds2, dnoise, dl[d] per block row
+  w.per = w.part + w.NB * (2 + kMaxD);
+  w.per = (w.per + 63) & ~63;
+  return w;
 }
-// same, for row n = i16 + m with i16 a multiple of 16 and m < 16
-template <int DP>
-GPK_DEVICE int xs_at2(int i16, int m, int d) {
-  if constexpr (DP == 64) return (i16 + m) * DP + (d ^ (m << 2));
-  else return (i16 + m) * (DP + 4) + d;
-}
-
-__host__ __device__ inline GradLds grad_lds_layout(int NB, int DP) {
-  GradLds o;
-  const int NP = 16 * NB, XS = grad_xs_stride(DP);
-  o.xs = 0;                         // NP x XS   centred x / l (zero padded)
-  o.wx = o.xs + NP * XS;            // NP x DP   Wx (prologue: staged diagonal blocks of L)
-  o.dinv = o.wx + NP * DP;          // NB x 16 x 16, row-major Linv_II
-  o.w1 = o.dinv + NB * 256;         // NP
-  o.alpha = o.w1 + NP;              // NP
-  o.sv = o.alpha + NP;              // NP   back-substitution right-hand side
-  o.nrm = o.sv + NP;                // NP   ||xs_n||^2
-  o.tsc = o.nrm + NP;               // kNW x 256 per-wave transpose scratch
-  o.red = o.tsc + kNW * 256;        // 256 reductions
-  o.total = o.red + 256;
-  return o;
-}
+GPK_DEVICE int tile_index(int I, int J) { return I * (I + 1) / 2 + J; }
 
 GPK_DEVICE f32x4 mfma4(const f32x4 a, const f32x4 b, f32x4 d) {
   d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], d, 0, 0, 0);
@@ -80,8 +66,11 @@ GPK_DEVICE f32x4 mfma4(const f32x4 a, const f32x4 b, f32x4 d) {
   return d;
 }
 
-GPK_DEVICE void lds_add(float* p, float v) {
-  (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+// Uniform value the compiler must treat as unknown at this point: keeps per-tile
+// addresses from being hoisted out of their step (live addresses would spill).
+GPK_DEVICE int opaque_s(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
 }
 
 // Sum over the 16 lanes of each row (lanes sharing g), DPP only.
@@ -93,81 +82,48 @@ GPK_DEVICE float row16_sum(float v) {
   return v;
 }
 
-// Uniform value the compiler must treat as unknown at this point: keeps per-tile
-// addresses from being hoisted out of the column loop (hundreds of live 64-bit
-// addresses would spill).
-GPK_DEVICE int opaque_s(int v) {
-  asm volatile("" : "+s"(v));
-  return v;
+// ======================================================================================
+// 1. solve: alpha, dy and the lower tiles of K^-1
+// ======================================================================================
+struct SolveLds {
+  int dinv, stg, sv, alpha, red, total;
+};
+__host__ __device__ inline SolveLds solve_lds(int NB) {
+  SolveLds o;
+  const int TS = (NB > 1 ? NB - 1 : 1) * 256;
+  const int stg = 2 * TS > NB * 256 ? 2 * TS : NB * 256;   // (prologue: diagonal blocks of L)
+  o.dinv = 0;                     // NB x 16 x 16 row-major Linv_II
+  o.stg = o.dinv + NB * 256;
+  o.sv = o.stg + stg;             // NP
+  o.alpha = o.sv + 16 * NB;       // NP
+  o.red = o.alpha + 16 * NB;      // kST column-sum partials + 64
+  o.total = o.red + kST + 64;
+  return o;
 }
 
-// A operand L_IK (lane (c, g), step r: L[16I + c][16K + 4g + r]); padding = identity.
-// FULL: one 16-B load at (scalar tile base) + (per-lane offset c N + 4g).
-template <bool FULL>
-GPK_DEVICE f32x4 load_L_rows(const float* Lb, int N, int I, int K, int c, int g) {
-  if (FULL) {
-    const float* t = Lb + opaque_s(16 * I * N + 16 * K);
-    return *(const f32x4*)&t[c * N + 4 * g];
-  }
-  // (masks from laundered block offsets: hoisted per-site lane masks would spill SGPRs)
-  const int i16 = opaque_s(16 * I), k16 = opaque_s(16 * K);
-  const int row = i16 + c, col = k16 + 4 * g;
-  f32x4 v;
-  const float* t = Lb + i16 * N;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    v[r] = (row < N && col + r < N) ? t[c * N + col + r] : (row == col + r ? 1.f : 0.f);
-  return v;
-}
-
-// A operand L_KI^T (lane (c, g), step r: L[16K + 4g + r][16I + c])
-template <bool FULL>
-GPK_DEVICE f32x4 load_L_cols(const float* Lb, int N, int K, int I, int c, int g) {
-  f32x4 v;
-  if (FULL) {
-    const float* t = Lb + opaque_s(16 * K * N + 16 * I) + 4 * g * N + c;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = t[r * N];
-    return v;
-  }
-  const int i16 = opaque_s(16 * I), k16 = opaque_s(16 * K);
-  const int col = i16 + c;
-  const float* t = Lb + k16 * N;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = k16 + 4 * g + r;
-    v[r] = (row < N && col < N) ? t[(4 * g + r) * N + col] : (row == col ? 1.f : 0.f);
-  }
-  return v;
-}
-
-template <int NB, int DQ, bool FULL>
-__global__ void __launch_bounds__(kT, 1) gpk_exact_grad_kernel(GpkExactGradArgs a) {
+template <int NB, bool FULL>
+__global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int DP = 16 * DQ, NP = 16 * NB;
-  const GradLds lay = grad_lds_layout(NB, DP);
-  float* xs = smem + lay.xs;
-  float* wx = smem + lay.wx;
+  constexpr int NP = 16 * NB;
+  constexpr int TS = (NB > 1 ? NB - 1 : 1) * 256;
+  const SolveLds lay = solve_lds(NB);
   float* dinv = smem + lay.dinv;
-  float* w1 = smem + lay.w1;
-  float* alpha = smem + lay.alpha;
+  float* stg = smem + lay.stg;
   float* sv = smem + lay.sv;
-  float* nrm = smem + lay.nrm;
+  float* alpha = smem + lay.alpha;
   float* red = smem + lay.red;
-
   const int N = FULL ? NP : a.N;
   const int D = a.D;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
   const int b = blockIdx.x;
   const float* Lb = a.L + (size_t)b * N * N;
+  const GradWs ws = grad_ws(N);
+  float* wsb = a.ws + (size_t)b * ws.per;
   const float* hyp = a.hyp;
   const int n_ls = a.n_ls;
-  const float s2 = hyp[0];
-  const float gw = a.gout[b];
-  const float gs = gw / (2.f * (float)N);
 
-  // ---- prologue: stage the diagonal blocks of L, xs = x / l, z
+  // ---- prologue: diagonal blocks of L (staged in stg), z, column sums of x / l
   {
     const int bi = tid >> 4, m = tid & 15;
     if (bi < NB) {
@@ -177,30 +133,25 @@ __global__ void __launch_bounds__(kT, 1) gpk_exact_grad_kernel(GpkExactGradArgs 
         const int col = 16 * bi + k;
         float v = (row == col) ? 1.f : 0.f;
         if (k <= m && row < N) v = Lb[(size_t)row * N + col];
-        wx[bi * 256 + m * 16 + k] = v;
+        stg[bi * 256 + m * 16 + k] = v;
       }
     }
   }
-  for (int e = tid; e < NP * DP; e += kT) {
-    const int n = e / DP, d = e - n * DP;
-    float v = 0.f;
-    if (n < N && d < D) v = a.X[((size_t)b * N + n) * D + d] / hyp[3 + (n_ls == 1 ? 0 : d)];
-    xs[xs_at<DP>(n, d)] = v;
-  }
-  for (int n = tid; n < NP; n += kT) {
-    sv[n] = n < N ? a.z[(size_t)b * N + n] : 0.f;
-    w1[n] = 0.f;
+  for (int n = tid; n < NP; n += kST) sv[n] = n < N ? a.z[(size_t)b * N + n] : 0.f;
+  {
+    const int d = tid & 63, part = tid >> 6;
+    float s = 0.f;
+    if (d < D) {
+      const float inv_l = 1.f / hyp[3 + (n_ls == 1 ? 0 : d)];
+      for (int n = part; n < N; n += kST / 64) s += a.X[((size_t)b * N + n) * D + d] * inv_l;
+    }
+    red[tid] = s;
   }
   lds_barrier();
-  {  // column sums of xs (partials) and the diagonal-block inverses
-    constexpr int P = kT / DP;
-    const int d = tid % DP, part = tid / DP;
-    float s = 0.f;
-    for (int n = part; n < N; n += P) s += xs[xs_at<DP>(n, d)];
-    smem[lay.tsc + tid] = s;
+  {
     const int bi = tid >> 4, cc = tid & 15;
     if (bi < NB) {
-      const float* Lt = wx + bi * 256;
+      const float* Lt = stg + bi * 256;
       float x[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -212,26 +163,13 @@ __global__ void __launch_bounds__(kT, 1) gpk_exact_grad_kernel(GpkExactGradArgs 
 #pragma unroll
       for (int m = 0; m < 16; ++m) dinv[bi * 256 + m * 16 + cc] = x[m];
     }
+    if (tid < kMaxD) {
+      float s = 0.f;
+      for (int p = 0; p < kST / 64; ++p) s += red[p * 64 + tid];
+      wsb[ws.mean + tid] = s / (float)N;
+    }
   }
   lds_barrier();
-  if (tid < DP) {
-    float s = 0.f;
-    for (int p = 0; p < kT / DP; ++p) s += smem[lay.tsc + p * DP + tid];
-    red[tid] = s / (float)N;
-  }
-  for (int e = tid; e < NP * DP; e += kT) wx[e] = 0.f;
-  lds_barrier();
-  for (int e = tid; e < N * DP; e += kT) {
-    const int n = e / DP, d = e - n * DP;
-    if (d < D) xs[xs_at<DP>(n, d)] -= red[d];
-  }
-  lds_barrier();
-  for (int n = tid; n < NP; n += kT) {
-    float s = 0.f;
-#pragma unroll 8
-    for (int d = 0; d < DP; ++d) s = __builtin_fmaf(xs[xs_at<DP>(n, d)], xs[xs_at<DP>(n, d)], s);
-    nrm[n] = s;
-  }
   // alpha = L^-T z: blocked back substitution (alpha_I = Linv_II^T s_I, then s_i -= L_Ii^T alpha_I)
   for (int I = NB - 1; I >= 0; --I) {
     if (tid < 16) {
@@ -252,222 +190,359 @@ __global__ void __launch_bounds__(kT, 1) gpk_exact_grad_kernel(GpkExactGradArgs 
     }
     lds_barrier();
   }
+  {
+    const float gw = a.gout[b];
+    const float invN = 1.f / (float)N;
+    float asum = 0.f;
+    for (int n = tid; n < NP; n += kST) {
+      const float an = alpha[n];
+      wsb[ws.alpha + n] = an;
+      if (n < N) {
+        asum += an;
+        if (a.dy != nullptr) a.dy[(size_t)b * N + n] = -gw * an * invN;
+      }
+    }
+    asum = wave_sum(asum);
+    if (lane == 0) red[wave] = asum;
+    lds_barrier();
+    if (tid == 0) {
+      float s = 0.f;
+      for (int w = 0; w < kSW; ++w) s += red[w];
+      wsb[ws.asum] = s;
+    }
+  }
 
-  // ---- block columns of K^-1 (lower part) and their consumers
-  constexpr float nhalf_log2e = -0.72134752044448170f;
-  float* tsc = smem + lay.tsc + wave * 256;
-  float ds2 = 0.f, dnz = 0.f;
-  const int ncol = (NB > kNW && NB - 1 - wave >= kNW) ? 2 : (wave < NB ? 1 : 0);
-  for (int ci = 0; ci < ncol; ++ci) {
-    const int J = __builtin_amdgcn_readfirstlane(ci == 0 ? wave : NB - 1 - wave);
-    f32x4 V[NB];
-    // forward: V = L^-1 e_J (block rows I >= J)
+  // ---- block columns of K^-1 (lower part): wave J owns column J; all waves step
+  //      together through 2 NB steps with the step's L tiles staged in LDS
+  const int J = wave;
+  const bool live = J < NB;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  auto fetch_row = [&](const int I) -> f32x4 {    // tiles (I, K < I), row-major
+    if (tid >= I * 64) return z4;
+    const int K = tid >> 6, q = tid & 63, m = q >> 2, cg = (q & 3) * 4;
+    const int row = 16 * I + m, col0 = 16 * K + cg;
+    if (FULL) return *(const f32x4*)&Lb[(size_t)row * N + col0];
+    f32x4 v;
 #pragma unroll
-    for (int I = 0; I < NB; ++I) {
-      const int I16 = opaque_s(16 * I);   // per-step LDS offsets stay in place
+    for (int j = 0; j < 4; ++j) v[j] = (row < N && col0 + j < N) ? Lb[(size_t)row * N + col0 + j] : 0.f;
+    return v;
+  };
+  auto put_row = [&](float* buf, const int I, const f32x4 v) {
+    if (tid >= I * 64) return;
+    const int K = tid >> 6, q = tid & 63, m = q >> 2, cg = (q & 3) * 4;
+    *(f32x4*)&buf[K * 256 + m * 16 + cg] = v;
+  };
+  auto fetch_col = [&](const int I) -> f32x4 {    // tiles (K > I, I), read by rows
+    if (tid >= (NB - 1 - I) * 64) return z4;
+    const int sl = tid >> 6, q = tid & 63, k = q >> 2, cg = (q & 3) * 4;
+    const int row = 16 * (I + 1 + sl) + k, col0 = 16 * I + cg;
+    if (FULL) return *(const f32x4*)&Lb[(size_t)row * N + col0];
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (row < N && col0 + j < N) ? Lb[(size_t)row * N + col0 + j] : 0.f;
+    return v;
+  };
+  auto put_col = [&](float* buf, const int I, const f32x4 v) {   // stored transposed
+    if (tid >= (NB - 1 - I) * 64) return;
+    const int sl = tid >> 6, q = tid & 63, k = q >> 2, cg = (q & 3) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) buf[sl * 256 + (cg + j) * 16 + k] = v[j];
+  };
+  f32x4 X[NB];
+  // Step s reads buffer s & 1: phase 1 step I (s = I) block row I, phase 2 step I
+  // (s = 2NB-1-I) block column I. The tiles of step s+2 are fetched during step s and
+  // written into buffer s & 1 after the step's barrier (everyone is done reading it).
+  if (NB > 1) put_row(stg + TS, 1, fetch_row(1));
+  lds_barrier();
+#pragma unroll
+  for (int I = 0; I < NB; ++I) {
+    const f32x4 nxt = (I + 2 < NB) ? fetch_row(I + 2) : ((I + 2 == NB + 1 && NB >= 2) ? fetch_col(NB - 2) : z4);
+    const float* buf = stg + (I & 1) * TS;
+    const int I16 = opaque_s(16 * I);
+    if (live) {
       if (I == J) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) V[I][r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
+        for (int r = 0; r < 4; ++r) X[I][r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
       } else if (I > J) {
-        __builtin_amdgcn_sched_barrier(0);
-        f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+        f32x4 s0 = z4, s1 = z4;
 #pragma unroll
         for (int K = 0; K < I; ++K) {
           if (K >= J) {
-            const f32x4 la = load_L_rows<FULL>(Lb, N, I, K, c, g);
-            if (K & 1) s1 = mfma4(la, V[K], s1);
-            else s0 = mfma4(la, V[K], s0);
+            const f32x4 la = *(const f32x4*)&buf[K * 256 + c * 16 + 4 * g];
+            if (K & 1) s1 = mfma4(la, X[K], s1);
+            else s0 = mfma4(la, X[K], s0);
           }
         }
         const f32x4 di = *(const f32x4*)&dinv[I16 * 16 + c * 16 + 4 * g];
-        const f32x4 z0 = {0.f, 0.f, 0.f, 0.f};
-        V[I] = -mfma4(di, s0 + s1, z0);
+        X[I] = -mfma4(di, s0 + s1, z4);
       }
     }
-    // per-column operands: xs_J as Gram B operand and as the row-side B operand
-    f32x4 xj[DQ], pj[DQ], wxj[DQ];
+    lds_barrier();
+    if (I + 2 < NB) put_row(stg + (I & 1) * TS, I + 2, nxt);
+    else if (I + 2 == NB + 1 && NB >= 2) put_col(stg + (I & 1) * TS, NB - 2, nxt);   // step 2NB-1-(NB-2)
+  }
+  lds_barrier();
+#pragma unroll
+  for (int I = NB - 1; I >= 0; --I) {
+    const int st = 2 * NB - 1 - I;
+    const f32x4 nxt = (I > 1) ? fetch_col(I - 2) : z4;
+    const float* buf = stg + (st & 1) * TS;
+    const int I16 = opaque_s(16 * I);
+    if (live && I >= J) {
+      f32x4 s0 = z4, s1 = z4;
+#pragma unroll
+      for (int K = I + 1; K < NB; ++K) {
+        const f32x4 la = *(const f32x4*)&buf[(K - I - 1) * 256 + c * 16 + 4 * g];
+        if (K & 1) s1 = mfma4(la, X[K], s1);
+        else s0 = mfma4(la, X[K], s0);
+      }
+      const f32x4 t = X[I] - s0 - s1;
+      f32x4 dt;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
+      const f32x4 U = mfma4(dt, t, z4);
+      X[I] = U;
+      *(f32x4*)&wsb[ws.kinv + (size_t)tile_index(I, J) * 256 + lane * 4] = U;
+    }
+    lds_barrier();
+    if (I > 1) put_col(stg + (st & 1) * TS, I - 2, nxt);
+  }
+}
+
+// ======================================================================================
+// 2. contractions per (window, block row I): W, w1, Wx, dX and the partials
+// ======================================================================================
+template <int DQ, bool FULL>
+__global__ void __launch_bounds__(256) gpk_grad_gram_kernel(GpkExactGradArgs a) {
+  const int N = a.N, D = a.D;
+  const GradWs ws = grad_ws(N);
+  const int NB = ws.NB;
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15, g = lane >> 4;
+  const int rows_per = (NB + 3) / 4;
+  const int b = blockIdx.x / rows_per;
+  const int I = (blockIdx.x - b * rows_per) * 4 + (threadIdx.x >> 6);
+  if (I >= NB) return;   // wave-uniform exit: no barriers in this kernel
+  const float* Xb = a.X + (size_t)b * N * D;
+  const float* wsb = a.ws + (size_t)b * ws.per;
+  const float* hyp = a.hyp;
+  const bool ard = a.n_ls > 1;
+  const float s2 = hyp[0];
+  const float gw = a.gout[b];
+  const float gs = gw / (2.f * (float)N);
+  constexpr float nhalf_log2e = -0.72134752044448170f;
+
+  // per-lane scale / centre of the dims this lane touches: 16q + 4g + r (Gram operands)
+  // and 16q + c (P operands); zero for d >= D
+  f32x4 ila[DQ], mua[DQ];
+  float ilp[DQ], mup[DQ];
+#pragma unroll
+  for (int q = 0; q < DQ; ++q) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int d = 16 * q + 4 * g + r;
+      ila[q][r] = d < D ? 1.f / hyp[3 + (ard ? d : 0)] : 0.f;
+      mua[q][r] = d < D ? wsb[ws.mean + d] : 0.f;
+    }
+    const int d = 16 * q + c;
+    ilp[q] = d < D ? 1.f / hyp[3 + (ard ? d : 0)] : 0.f;
+    mup[q] = d < D ? wsb[ws.mean + d] : 0.f;
+  }
+  const bool vec4 = (D & 3) == 0;
+  // xs[n][16q + 4g .. +3] (Gram operand layout)
+  auto xs4 = [&](int n, int q) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (!FULL && n >= N) return v;
+    const int d0 = 16 * q + 4 * g;
+    if (vec4 && d0 + 3 < D) {
+      v = *(const f32x4*)&Xb[(size_t)n * D + d0];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = d0 + r < D ? Xb[(size_t)n * D + d0 + r] : 0.f;
+    }
+    return v * ila[q] - mua[q];
+  };
+  // xs[n][16q + c] (P operand layout)
+  auto xs1 = [&](int n, int q) -> float {
+    const int d = 16 * q + c;
+    if ((!FULL && n >= N) || d >= D) return 0.f;
+    return Xb[(size_t)n * D + d] * ilp[q] - mup[q];
+  };
+
+  f32x4 bi[DQ];
+  float ni = 0.f;
+#pragma unroll
+  for (int q = 0; q < DQ; ++q) {
+    bi[q] = xs4(16 * I + c, q);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ni = __builtin_fmaf(bi[q][r], bi[q][r], ni);
+  }
+  ni += __shfl_xor(ni, 16, 64);
+  ni += __shfl_xor(ni, 32, 64);
+  const int col = 16 * I + c;
+  const float ai = wsb[ws.alpha + col];
+  f32x4 wx[DQ];
+#pragma unroll
+  for (int q = 0; q < DQ; ++q) wx[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float w1p = 0.f, ds2 = 0.f, dnz = 0.f;
+
+  for (int J = 0; J < NB; ++J) {
+    f32x4 aj[DQ], pj[DQ];
 #pragma unroll
     for (int q = 0; q < DQ; ++q) {
-      xj[q] = *(const f32x4*)&xs[xs_at<DP>(16 * J + c, 16 * q + 4 * g)];
+      aj[q] = xs4(16 * J + c, q);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pj[q][r] = xs[xs_at<DP>(16 * J + 4 * g + r, 16 * q + c)];
-      wxj[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) pj[q][r] = xs1(16 * J + 4 * g + r, q);
     }
-    const int col = 16 * J + c;
-    const float aj = alpha[col], nj = nrm[col];
-    float w1c = 0.f;
-    // backward: U = L^-T V, I = NB-1 .. J, each final tile consumed at once
+    // K^-1_JI in acc layout (rows j, cols i): stored when J >= I, else the transpose of K^-1_IJ
+    f32x4 T;
+    if (J >= I) {
+      T = *(const f32x4*)&wsb[ws.kinv + (size_t)tile_index(J, I) * 256 + lane * 4];
+    } else {
+      const float* t = wsb + ws.kinv + (size_t)tile_index(I, J) * 256;
 #pragma unroll
-    for (int I = NB - 1; I >= 0; --I) {
-      if (I >= J) {
-        __builtin_amdgcn_sched_barrier(0);
-        const int I16 = opaque_s(16 * I);
-        f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) T[r] = t[((c >> 2) * 16 + 4 * g + r) * 4 + (c & 3)];
+    }
+    const f32x4 al = *(const f32x4*)&wsb[ws.alpha + 16 * J + 4 * g];
+    f32x4 gr = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int K = I + 1; K < NB; ++K) {
-          const f32x4 la = load_L_cols<FULL>(Lb, N, K, I, c, g);
-          if (K & 1) s1 = mfma4(la, V[K], s1);
-          else s0 = mfma4(la, V[K], s0);
-        }
-        const f32x4 t = V[I] - s0 - s1;
-        f32x4 dt;
+    for (int q = 0; q < DQ; ++q) gr = mfma4(aj[q], bi[q], gr);
+    f32x4 W;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
-        const f32x4 z0 = {0.f, 0.f, 0.f, 0.f};
-        const f32x4 U = mfma4(dt, t, z0);
-        V[I] = U;
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- consume K^-1_IJ = U (rows 16I + 4g + r, column col)
-        f32x4 gr = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) {
+      float nj = 0.f;
 #pragma unroll
-        for (int q = 0; q < DQ; ++q)
-          gr = mfma4(*(const f32x4*)&xs[xs_at2<DP>(I16, c, 16 * q + 4 * g)], xj[q], gr);
-        f32x4 W;
+      for (int q = 0; q < DQ; ++q) nj = __builtin_fmaf(pj[q][r], pj[q][r], nj);
+      nj = row16_sum(nj);                   // ||xs_j||^2 of row 16J + 4g + r
+      const int row = 16 * J + 4 * g + r;
+      float G = (al[r] * ai - T[r]) * gs;
+      if (!FULL && (row >= N || col >= N)) G = 0.f;
+      float d2 = __builtin_fmaxf(nj + ni - 2.f * gr[r], 0.f);
+      if (row == col) d2 = 0.f;
+      const float E = __builtin_amdgcn_exp2f(d2 * nhalf_log2e);
+      ds2 = __builtin_fmaf(G, E, ds2);
+      if (row == col) dnz += G;
+      W[r] = (row == col) ? 0.f : G * s2 * E;
+    }
+    w1p += (W[0] + W[1]) + (W[2] + W[3]);
+    // Wx_I += W_JI^T xs_J  (rows i, dims)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = I16 + 4 * g + r;
-          const int lrow = row;
-          float G = (alpha[lrow] * aj - U[r]) * gs;
-          if (!FULL && (row >= N || col >= N)) G = 0.f;
-          float d2 = __builtin_fmaxf(nrm[lrow] + nj - 2.f * gr[r], 0.f);
-          if (row == col) d2 = 0.f;
-          const float E = __builtin_amdgcn_exp2f(d2 * nhalf_log2e);
-          ds2 = __builtin_fmaf((I == J ? 1.f : 2.f) * G, E, ds2);
-          if (row == col) dnz += G;
-          W[r] = (row == col) ? 0.f : G * s2 * E;
-        }
-        // column side: rows of J
-        w1c += (W[0] + W[1]) + (W[2] + W[3]);
+    for (int q = 0; q < DQ; ++q) wx[q] = mfma4(W, pj[q], wx[q]);
+  }
+  // w1 of row 16I + c (column sums of the W_JI tiles)
+  w1p += __shfl_xor(w1p, 16, 64);
+  w1p += __shfl_xor(w1p, 32, 64);
+  // rows of the Wx accumulator are 16I + 4g + r; their w1 lives in lane 4g + r
+  float w1r[4];
 #pragma unroll
-        for (int q = 0; q < DQ; ++q) {
-          f32x4 p;
+  for (int r = 0; r < 4; ++r) w1r[r] = __shfl(w1p, 4 * g + r, 64);
+  float* part = a.ws + (size_t)b * ws.per + ws.part + I * (2 + kMaxD);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) p[r] = xs[xs_at2<DP>(I16, 4 * g + r, 16 * q + c)];
-          wxj[q] = mfma4(W, p, wxj[q]);
-        }
-        // row side: rows of I (off-diagonal tiles only)
-        if (I > J) {
-          *(f32x4*)&tsc[lane * 4] = W;
-          wave_lds_sync();
-          f32x4 wt;   // acc layout of W^T: reg r = W[c][4g + r]
+  for (int q = 0; q < DQ; ++q) {
+    const int d = 16 * q + c;
+    float lp = 0.f;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int e = 4 * g + r;
-            wt[r] = tsc[((c >> 2) * 16 + e) * 4 + (c & 3)];
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float rs = row16_sum(W[r]);
-            if (c == 0) lds_add(&w1[I16 + 4 * g + r], rs);
-          }
-#pragma unroll
-          for (int q = 0; q < DQ; ++q) {
-            const f32x4 z0 = {0.f, 0.f, 0.f, 0.f};
-            const f32x4 o = mfma4(wt, pj[q], z0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) lds_add(&wx[(I16 + 4 * g + r) * DP + 16 * q + c], o[r]);
-          }
-          wave_lds_sync();   // tsc is rewritten by the next tile
-        }
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * I + 4 * g + r;
+      const float x = xs1(row, q);
+      const float e = x * w1r[r] - wx[q][r];   // = -dxs / 2
+      if ((FULL || row < N) && d < D) {
+        if (a.dX != nullptr) a.dX[((size_t)b * N + row) * D + d] = -2.f * e * ilp[q];
+        lp = __builtin_fmaf(x, e, lp);
       }
     }
-    w1c += __shfl_xor(w1c, 16, 64);
-    w1c += __shfl_xor(w1c, 32, 64);
-    if (g == 0) lds_add(&w1[col], w1c);
-#pragma unroll
-    for (int q = 0; q < DQ; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) lds_add(&wx[(16 * J + 4 * g + r) * DP + 16 * q + c], wxj[q][r]);
+    lp += __shfl_xor(lp, 16, 64);
+    lp += __shfl_xor(lp, 32, 64);
+    if (g == 0) part[2 + d] = lp;          // (d >= D: 0)
   }
   ds2 = wave_sum(ds2);
   dnz = wave_sum(dnz);
   if (lane == 0) {
-    red[DP + wave] = ds2;
-    red[DP + kNW + wave] = dnz;
-  }
-  for (int q = tid; q < DP; q += kT) red[DP + 3 * kNW + q] = 0.f;
-  __syncthreads();
-
-  // ---- per-row outputs and the lengthscale / constant sums
-  const float invN = 1.f / (float)N;
-  float asum = 0.f;
-  for (int n = tid; n < N; n += kT) {
-    const float an = alpha[n];
-    asum += an;
-    if (a.dy != nullptr) a.dy[(size_t)b * N + n] = -gw * an * invN;
-  }
-  float* part = red + DP + 3 * kNW;
-  for (int e = tid; e < N * DP; e += kT) {
-    const int n = e / DP, d = e - n * DP;
-    if (d < D) {
-      const float x = xs[xs_at<DP>(n, d)];
-      const float ee = x * w1[n] - wx[n * DP + d];  // = -dxs / 2
-      if (a.dX != nullptr) a.dX[((size_t)b * N + n) * D + d] = -2.f * ee / hyp[3 + (n_ls == 1 ? 0 : d)];
-      lds_add(&part[d], x * ee);
-    }
-  }
-  asum = wave_sum(asum);
-  if (lane == 0) red[DP + 2 * kNW + wave] = asum;
-  __syncthreads();
-  if (tid == 0) {
-    float* o = a.dhyp + (size_t)b * (3 + n_ls);
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    for (int w = 0; w < kNW; ++w) {
-      a0 += red[DP + w];
-      a1 += red[DP + kNW + w];
-      a2 += red[DP + 2 * kNW + w];
-    }
-    o[0] = a0;
-    o[1] = a1;
-    o[2] = gw * a2 * invN;
-    if (n_ls == 1) {
-      float s = 0.f;
-      for (int d = 0; d < D; ++d) s += part[d];
-      o[3] = 2.f * s / hyp[3];
-    } else {
-      for (int d = 0; d < D; ++d) o[3 + d] = 2.f * part[d] / hyp[3 + d];
-    }
+    part[0] = ds2;
+    part[1] = dnz;
   }
 }
 
-template <int NB, int DQ, bool FULL>
-int launch_grad(const GpkExactGradArgs& a, hipStream_t stream) {
-  const GradLds lay = grad_lds_layout(NB, 16 * DQ);
-  const size_t lds = (size_t)lay.total * sizeof(float);
-  if (lds > 160 * 1024) return -8;
-  static std::once_flag once;
-  std::call_once(once, [&] {
-    (void)hipFuncSetAttribute((const void*)gpk_exact_grad_kernel<NB, DQ, FULL>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipGetLastError();
-  });
-  hipLaunchKernelGGL((gpk_exact_grad_kernel<NB, DQ, FULL>), dim3(a.B), dim3(kT), lds, stream, a);
-  return (int)hipGetLastError();
+// ======================================================================================
+// 3. fixed-order sums of the block-row partials -> dhyp
+// ======================================================================================
+__global__ void __launch_bounds__(128) gpk_grad_fin_kernel(GpkExactGradArgs a, int DP) {
+  const int N = a.N, D = a.D;
+  const GradWs ws = grad_ws(N);
+  const int b = blockIdx.x, t = threadIdx.x;
+  const float* wsb = a.ws + (size_t)b * ws.per;
+  const float* part = wsb + ws.part;
+  float* o = a.dhyp + (size_t)b * (3 + a.n_ls);
+  const float* hyp = a.hyp;
+  // thread t < 64: dl_t (t < D); 64: ds2, 65: dnoise, 66: dc
+  const int f = t < 64 ? (t < D ? 2 + t : -1) : (t == 64 ? 0 : (t == 65 ? 1 : -1));
+  float s = 0.f;
+  if (f >= 0)
+    for (int I = 0; I < ws.NB; ++I) s += part[I * (2 + kMaxD) + f];
+  if (t == 64) o[0] = s;
+  if (t == 65) o[1] = s;
+  if (t == 66) o[2] = a.gout[b] * wsb[ws.asum] / (float)N;
+  if (t < 64) {
+    if (a.n_ls == 1) {
+      const float tot = wave_sum(s);   // fixed-order butterfly over the dims
+      if (t == 0) o[3] = 2.f * tot / hyp[3];
+    } else if (t < D) {
+      o[3 + t] = 2.f * s / hyp[3 + t];
+    }
+  }
+  (void)DP;
 }
 
 template <int NB>
-int launch_grad_nb(const GpkExactGradArgs& a, hipStream_t stream) {
-  const bool full = a.N == 16 * NB;
-  if (a.D <= 16) return full ? launch_grad<NB, 1, true>(a, stream) : launch_grad<NB, 1, false>(a, stream);
-  if (a.D <= 32) return full ? launch_grad<NB, 2, true>(a, stream) : launch_grad<NB, 2, false>(a, stream);
-  return full ? launch_grad<NB, 4, true>(a, stream) : launch_grad<NB, 4, false>(a, stream);
+int launch_solve(const GpkExactGradArgs& a, hipStream_t stream) {
+  const size_t lds = (size_t)solve_lds(NB).total * sizeof(float);
+  if (lds > 160 * 1024) return -7;
+  static std::once_flag once;
+  std::call_once(once, [&] {
+    (void)hipFuncSetAttribute((const void*)gpk_grad_solve_kernel<NB, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gpk_grad_solve_kernel<NB, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipGetLastError();
+  });
+  if (a.N == 16 * NB)
+    hipLaunchKernelGGL((gpk_grad_solve_kernel<NB, true>), dim3(a.B), dim3(kST), lds, stream, a);
+  else
+    hipLaunchKernelGGL((gpk_grad_solve_kernel<NB, false>), dim3(a.B), dim3(kST), lds, stream, a);
+  return (int)hipGetLastError();
+}
+
+template <int DQ>
+int launch_gram(const GpkExactGradArgs& a, hipStream_t stream) {
+  const int NB = (a.N + 15) / 16;
+  const long long grid = (long long)a.B * ((NB + 3) / 4);
+  if (grid > 0x7fffffff) return -6;
+  if (a.N == 16 * NB)
+    hipLaunchKernelGGL((gpk_grad_gram_kernel<DQ, true>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((gpk_grad_gram_kernel<DQ, false>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
 
 size_t gpk_exact_grad_ws_floats(int B, int N) {
-  (void)B;
-  (void)N;
-  return 0;   // the adjoint keeps L^-1 in registers: no workspace
+  return (size_t)B * grad_ws(N).per;
 }
 
 int gpk_launch_exact_grad(const GpkExactGradArgs& a, hipStream_t stream) {
+  int rc;
   switch ((a.N + 15) / 16) {
-#define GPK_CASE(nb) case nb: return launch_grad_nb<nb>(a, stream);
+#define GPK_CASE(nb) case nb: rc = launch_solve<nb>(a, stream); break;
     GPK_CASE(1) GPK_CASE(2) GPK_CASE(3) GPK_CASE(4) GPK_CASE(5) GPK_CASE(6)
     GPK_CASE(7) GPK_CASE(8) GPK_CASE(9) GPK_CASE(10) GPK_CASE(11) GPK_CASE(12)
     GPK_CASE(13) GPK_CASE(14) GPK_CASE(15) GPK_CASE(16)
 #undef GPK_CASE
     default: return -7;
   }
+  if (rc != 0) return rc;
+  rc = a.D <= 16 ? launch_gram<1>(a, stream) : (a.D <= 32 ? launch_gram<2>(a, stream) : launch_gram<4>(a, stream));
+  if (rc != 0) return rc;
+  hipLaunchKernelGGL(gpk_grad_fin_kernel, dim3(a.B), dim3(128), 0, stream, a, 0);
+  return (int)hipGetLastError();
 }

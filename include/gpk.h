@@ -74,8 +74,8 @@ int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp,
  * psd_safe_cholesky backward, kernels/rbf_kernel.py backward); SURVEY.md §8f row 1.
  *
  * L : (B, N, N) float, z : (B, N) float (gpk_exact_mll_f32 outputs)   gout : (B,) float
- * workspace : gpk_exact_grad_workspace_bytes(B, N) bytes of device memory (currently 0:
- *             NULL is accepted; kept in the ABI so a future variant may ask for scratch)
+ * workspace : gpk_exact_grad_workspace_bytes(B, N) bytes of device memory (the lower block
+ *             tiles of K_hat^{-1} per window, ~145 KB at N = 256, plus small vectors)
  * dX : (B, N, D) float out or NULL (D <= 64)   dy : (B, N) float out or NULL
  * dhyp : (B, 3 + n_lengthscale) float out (per window; the caller sums over b)
  */

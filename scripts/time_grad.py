@@ -1,32 +1,30 @@
-"""Time the exact-GP forward (L + z kept) and the analytic backward at B=512 N=256 D=32."""
-import math, os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch
-from fine_grained_gaussian_process_forcasting_amd import ops
+"""Kernel time of the exact backward (and forward) at B=512 N=256 D=32 with HIP events;
+GPK_LIB selects an A/B build.   python scripts/time_grad.py [B] [N] [D]"""
+import math
+import os
+import sys
 
-B, N, D = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (512, 256, 32)))
-dev = torch.device("cuda:0")
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fine_grained_gaussian_process_forcasting_amd import ops  # noqa: E402
+
+B, N, D = (int(v) for v in (sys.argv[1:] + ["512", "256", "32"])[:3])
+dev = torch.device("cuda", 0)
 g = torch.Generator().manual_seed(0)
 X = (torch.randn(B, N, D, generator=g) / math.sqrt(D)).to(dev)
 y = torch.randn(B, N, generator=g).to(dev)
-LN2 = math.log(2)
-hyp = ops.pack_exact_hyper(LN2, LN2 + 1e-4, 0.0, LN2, dev)
+h = ops.pack_exact_hyper(math.log(2), math.log(2) + 1e-4, 0.0, math.log(2), dev)
+f = ops.exact_mll(X, y, None, None, None, None, hyper=h, want_L=True, want_z=True)
 gout = torch.ones(B, device=dev)
-fw = ops.exact_mll(X, y, None, None, None, None, hyper=hyp, want_L=True, want_z=True)
 for _ in range(3):
-    ops.exact_mll_grad(X, fw.L, fw.z, hyp, gout)
+    ops.exact_mll_grad(X, f.L, f.z, h, gout)
 torch.cuda.synchronize()
-s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-reps = 10
-s.record()
-for _ in range(reps):
-    fw = ops.exact_mll(X, y, None, None, None, None, hyper=hyp, want_L=True, want_z=True)
-e.record(); torch.cuda.synchronize()
-tf = s.elapsed_time(e) / reps
-s.record()
-for _ in range(reps):
-    ops.exact_mll_grad(X, fw.L, fw.z, hyp, gout)
-e.record(); torch.cuda.synchronize()
-tb = s.elapsed_time(e) / reps
-print(f"B={B} N={N} D={D}: forward(L,z) {tf*1e3:.1f} us, backward {tb*1e3:.1f} us "
-      f"({B / ((tf + tb) * 1e-3):.3e} windows/s fwd+bwd)")
+ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+for a, b in ev:
+    a.record()
+    ops.exact_mll_grad(X, f.L, f.z, h, gout)
+    b.record()
+torch.cuda.synchronize()
+ms = sorted(a.elapsed_time(b) for a, b in ev)
+print(f"{os.environ.get('GPK_LIB', 'default')}: grad median {ms[5]:.4f} ms min {ms[0]:.4f}", flush=True)

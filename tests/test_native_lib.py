@@ -96,7 +96,8 @@ def test_grad_entry_validation_without_device():
     from fine_grained_gaussian_process_forcasting_amd import _native
     lib = _native.lib()
     one = ctypes.c_void_p(16)  # never dereferenced: validation returns first
-    assert lib.gpk_exact_grad_workspace_bytes(3, 256) == 0   # L^-1 stays in registers
+    # K^-1 lower tiles (136 x 1 KiB) + alpha, means, partials per window, 64-float aligned
+    assert lib.gpk_exact_grad_workspace_bytes(3, 256) == 3 * 36224 * 4
     assert lib.gpk_exact_grad_workspace_bytes(3, 257) == 0
     args = [one, one, one, one, 1, 2, 16, 4, one, one, None, None, one, None]
     bad = list(args); bad[0] = None
