@@ -125,16 +125,22 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
 
   // ---- prologue: diagonal blocks of L (staged in stg), z, column sums of x / l
   {
-    const int bi = tid >> 4, m = tid & 15;
+    const int bi = tid >> 6, m = (tid >> 2) & 15, kq = (tid & 3) * 4;   // one float4 per thread
     if (bi < NB) {
-      const int row = 16 * bi + m;
+      const int row = 16 * bi + m, col0 = 16 * bi + kq;
+      f32x4 v;
+      if (FULL) {
+        v = *(const f32x4*)&Lb[(size_t)row * N + col0];
+      } else {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int col = 16 * bi + k;
-        float v = (row == col) ? 1.f : 0.f;
-        if (k <= m && row < N) v = Lb[(size_t)row * N + col];
-        stg[bi * 256 + m * 16 + k] = v;
+        for (int j = 0; j < 4; ++j) v[j] = (row < N && col0 + j < N) ? Lb[(size_t)row * N + col0 + j] : 0.f;
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (kq + j > m) v[j] = 0.f;
+        if (kq + j == m && row >= N) v[j] = 1.f;   // identity padding
+      }
+      *(f32x4*)&stg[bi * 256 + m * 16 + kq] = v;
     }
   }
   for (int n = tid; n < NP; n += kST) sv[n] = n < N ? a.z[(size_t)b * N + n] : 0.f;
@@ -170,52 +176,14 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
     }
   }
   lds_barrier();
-  // alpha = L^-T z: blocked back substitution (alpha_I = Linv_II^T s_I, then s_i -= L_Ii^T alpha_I)
-  for (int I = NB - 1; I >= 0; --I) {
-    if (tid < 16) {
-      float t = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) t = __builtin_fmaf(dinv[I * 256 + k * 16 + tid], sv[16 * I + k], t);
-      alpha[16 * I + tid] = t;
-    }
-    lds_barrier();
-    if (tid < 16 * I) {
-      float t = sv[tid];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int row = 16 * I + k;
-        if (FULL || row < N) t = __builtin_fmaf(-Lb[(size_t)row * N + tid], alpha[row], t);
-      }
-      sv[tid] = t;
-    }
-    lds_barrier();
-  }
-  {
-    const float gw = a.gout[b];
-    const float invN = 1.f / (float)N;
-    float asum = 0.f;
-    for (int n = tid; n < NP; n += kST) {
-      const float an = alpha[n];
-      wsb[ws.alpha + n] = an;
-      if (n < N) {
-        asum += an;
-        if (a.dy != nullptr) a.dy[(size_t)b * N + n] = -gw * an * invN;
-      }
-    }
-    asum = wave_sum(asum);
-    if (lane == 0) red[wave] = asum;
-    lds_barrier();
-    if (tid == 0) {
-      float s = 0.f;
-      for (int w = 0; w < kSW; ++w) s += red[w];
-      wsb[ws.asum] = s;
-    }
-  }
-
   // ---- block columns of K^-1 (lower part): wave J owns column J; all waves step
   //      together through 2 NB steps with the step's L tiles staged in LDS
   const int J = wave;
   const bool live = J < NB;
+  constexpr int AW = NB < kSW ? NB : kSW - 1;   // the wave that also solves alpha
+  const float gw = a.gout[b];
+  const float invN = 1.f / (float)N;
+  float asum = 0.f;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   auto fetch_row = [&](const int I) -> f32x4 {    // tiles (I, K < I), row-major
     if (tid >= I * 64) return z4;
@@ -304,97 +272,107 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
       X[I] = U;
       *(f32x4*)&wsb[ws.kinv + (size_t)tile_index(I, J) * 256 + lane * 4] = U;
     }
+    // alpha = L^-T z by the same back substitution (right-hand side z in column 0 of the
+    // tiles), run by wave AW: an idle wave when NB < 16, else wave 15 once its own
+    // column (one tile, step NB-1) is done
+    if (wave == AW) {
+      if (I == NB - 1) {
+#pragma unroll
+        for (int K = 0; K < NB; ++K)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) X[K][r] = c == 0 ? sv[16 * K + 4 * g + r] : 0.f;
+      }
+      f32x4 s0 = z4, s1 = z4;
+#pragma unroll
+      for (int K = I + 1; K < NB; ++K) {
+        const f32x4 la = *(const f32x4*)&buf[(K - I - 1) * 256 + c * 16 + 4 * g];
+        if (K & 1) s1 = mfma4(la, X[K], s1);
+        else s0 = mfma4(la, X[K], s0);
+      }
+      const f32x4 t = X[I] - s0 - s1;
+      f32x4 dt;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
+      X[I] = mfma4(dt, t, z4);
+      if (c == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = 16 * I + 4 * g + r;
+          const float an = X[I][r];
+          wsb[ws.alpha + n] = an;
+          if (FULL || n < N) {
+            asum += an;
+            if (a.dy != nullptr) a.dy[(size_t)b * N + n] = -gw * an * invN;
+          }
+        }
+      }
+    }
     lds_barrier();
     if (I > 1) put_col(stg + (st & 1) * TS, I - 2, nxt);
+  }
+  if (wave == AW) {
+    asum = wave_sum(asum);
+    if (lane == 0) wsb[ws.asum] = asum;
   }
 }
 
 // ======================================================================================
-// 2. contractions per (window, block row I): W, w1, Wx, dX and the partials
+// 2. contractions per (window, block row I): W, w1, Wx, dX and the partials.
+//    One workgroup (16 waves) per window: xs = x / l - mean, ||xs||^2 and alpha are
+//    staged in LDS once; wave I owns block row I and visits every block column J.
 // ======================================================================================
+constexpr int kGW = 16;
+
 template <int DQ, bool FULL>
-__global__ void __launch_bounds__(256) gpk_grad_gram_kernel(GpkExactGradArgs a) {
+__global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : 8) gpk_grad_gram_kernel(GpkExactGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int DP = 16 * DQ, XS = DP + 4;
   const int N = a.N, D = a.D;
   const GradWs ws = grad_ws(N);
-  const int NB = ws.NB;
-  const int lane = threadIdx.x & 63;
+  const int NB = ws.NB, NP = 16 * NB;
+  const int tid = threadIdx.x, lane = tid & 63, I = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
-  const int rows_per = (NB + 3) / 4;
-  const int b = blockIdx.x / rows_per;
-  const int I = (blockIdx.x - b * rows_per) * 4 + (threadIdx.x >> 6);
-  if (I >= NB) return;   // wave-uniform exit: no barriers in this kernel
+  const int b = blockIdx.x;
   const float* Xb = a.X + (size_t)b * N * D;
   const float* wsb = a.ws + (size_t)b * ws.per;
   const float* hyp = a.hyp;
   const bool ard = a.n_ls > 1;
+  float* xs = smem;                  // NP x XS
+  float* nrm = xs + NP * XS;         // NP
+  float* al = nrm + NP;              // NP
+  for (int e = tid; e < NP * DP; e += 64 * kGW) {
+    const int n = e / DP, d = e - n * DP;
+    float v = 0.f;
+    if ((FULL || n < N) && d < D) v = Xb[(size_t)n * D + d] / hyp[3 + (ard ? d : 0)] - wsb[ws.mean + d];
+    xs[n * XS + d] = v;
+  }
+  for (int n = tid; n < NP; n += 64 * kGW) al[n] = wsb[ws.alpha + n];
+  lds_barrier();
+  for (int n = tid; n < NP; n += 64 * kGW) {
+    float t = 0.f;
+#pragma unroll
+    for (int d = 0; d < DP; ++d) t = __builtin_fmaf(xs[n * XS + d], xs[n * XS + d], t);
+    nrm[n] = t;
+  }
+  lds_barrier();
+  if (I >= NB) return;   // wave-uniform; no barriers below
   const float s2 = hyp[0];
   const float gw = a.gout[b];
   const float gs = gw / (2.f * (float)N);
   constexpr float nhalf_log2e = -0.72134752044448170f;
 
-  // per-lane scale / centre of the dims this lane touches: 16q + 4g + r (Gram operands)
-  // and 16q + c (P operands); zero for d >= D
-  f32x4 ila[DQ], mua[DQ];
-  float ilp[DQ], mup[DQ];
-#pragma unroll
-  for (int q = 0; q < DQ; ++q) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int d = 16 * q + 4 * g + r;
-      ila[q][r] = d < D ? 1.f / hyp[3 + (ard ? d : 0)] : 0.f;
-      mua[q][r] = d < D ? wsb[ws.mean + d] : 0.f;
-    }
-    const int d = 16 * q + c;
-    ilp[q] = d < D ? 1.f / hyp[3 + (ard ? d : 0)] : 0.f;
-    mup[q] = d < D ? wsb[ws.mean + d] : 0.f;
-  }
-  const bool vec4 = (D & 3) == 0;
-  // xs[n][16q + 4g .. +3] (Gram operand layout)
-  auto xs4 = [&](int n, int q) -> f32x4 {
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (!FULL && n >= N) return v;
-    const int d0 = 16 * q + 4 * g;
-    if (vec4 && d0 + 3 < D) {
-      v = *(const f32x4*)&Xb[(size_t)n * D + d0];
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = d0 + r < D ? Xb[(size_t)n * D + d0 + r] : 0.f;
-    }
-    return v * ila[q] - mua[q];
-  };
-  // xs[n][16q + c] (P operand layout)
-  auto xs1 = [&](int n, int q) -> float {
-    const int d = 16 * q + c;
-    if ((!FULL && n >= N) || d >= D) return 0.f;
-    return Xb[(size_t)n * D + d] * ilp[q] - mup[q];
-  };
-
+  // Gram B operand for the columns i = 16I + c: xs[i][16q + 4g .. +3]
   f32x4 bi[DQ];
-  float ni = 0.f;
 #pragma unroll
-  for (int q = 0; q < DQ; ++q) {
-    bi[q] = xs4(16 * I + c, q);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ni = __builtin_fmaf(bi[q][r], bi[q][r], ni);
-  }
-  ni += __shfl_xor(ni, 16, 64);
-  ni += __shfl_xor(ni, 32, 64);
+  for (int q = 0; q < DQ; ++q) bi[q] = *(const f32x4*)&xs[(16 * I + c) * XS + 16 * q + 4 * g];
   const int col = 16 * I + c;
-  const float ai = wsb[ws.alpha + col];
+  const float ni = nrm[col], ai = al[col];
   f32x4 wx[DQ];
 #pragma unroll
   for (int q = 0; q < DQ; ++q) wx[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   float w1p = 0.f, ds2 = 0.f, dnz = 0.f;
-
-  for (int J = 0; J < NB; ++J) {
-    f32x4 aj[DQ], pj[DQ];
-#pragma unroll
-    for (int q = 0; q < DQ; ++q) {
-      aj[q] = xs4(16 * J + c, q);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pj[q][r] = xs1(16 * J + 4 * g + r, q);
-    }
-    // K^-1_JI in acc layout (rows j, cols i): stored when J >= I, else the transpose of K^-1_IJ
+  // K^-1_JI in acc layout (rows j, cols i): stored when J >= I, else the transpose of K^-1_IJ
+  auto load_T = [&](int J) -> f32x4 {
     f32x4 T;
     if (J >= I) {
       T = *(const f32x4*)&wsb[ws.kinv + (size_t)tile_index(J, I) * 256 + lane * 4];
@@ -403,21 +381,29 @@ __global__ void __launch_bounds__(256) gpk_grad_gram_kernel(GpkExactGradArgs a) 
 #pragma unroll
       for (int r = 0; r < 4; ++r) T[r] = t[((c >> 2) * 16 + 4 * g + r) * 4 + (c & 3)];
     }
-    const f32x4 al = *(const f32x4*)&wsb[ws.alpha + 16 * J + 4 * g];
-    f32x4 gr = {0.f, 0.f, 0.f, 0.f};
+    return T;
+  };
+  f32x4 Tn = load_T(0);
+  for (int J = 0; J < NB; ++J) {
+    const f32x4 T = Tn;
+    if (J + 1 < NB) Tn = load_T(J + 1);      // one tile ahead: the L2 latency overlaps this one
+    const int j0 = 16 * J;
+    f32x4 gr = {0.f, 0.f, 0.f, 0.f}, pj[DQ];
 #pragma unroll
-    for (int q = 0; q < DQ; ++q) gr = mfma4(aj[q], bi[q], gr);
+    for (int q = 0; q < DQ; ++q) {
+      gr = mfma4(*(const f32x4*)&xs[(j0 + c) * XS + 16 * q + 4 * g], bi[q], gr);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pj[q][r] = xs[(j0 + 4 * g + r) * XS + 16 * q + c];
+    }
+    const f32x4 aj = *(const f32x4*)&al[j0 + 4 * g];
+    const f32x4 nj = *(const f32x4*)&nrm[j0 + 4 * g];
     f32x4 W;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float nj = 0.f;
-#pragma unroll
-      for (int q = 0; q < DQ; ++q) nj = __builtin_fmaf(pj[q][r], pj[q][r], nj);
-      nj = row16_sum(nj);                   // ||xs_j||^2 of row 16J + 4g + r
-      const int row = 16 * J + 4 * g + r;
-      float G = (al[r] * ai - T[r]) * gs;
+      const int row = j0 + 4 * g + r;
+      float G = (aj[r] * ai - T[r]) * gs;
       if (!FULL && (row >= N || col >= N)) G = 0.f;
-      float d2 = __builtin_fmaxf(nj + ni - 2.f * gr[r], 0.f);
+      float d2 = __builtin_fmaxf(nj[r] + ni - 2.f * gr[r], 0.f);
       if (row == col) d2 = 0.f;
       const float E = __builtin_amdgcn_exp2f(d2 * nhalf_log2e);
       ds2 = __builtin_fmaf(G, E, ds2);
@@ -440,14 +426,15 @@ __global__ void __launch_bounds__(256) gpk_grad_gram_kernel(GpkExactGradArgs a) 
 #pragma unroll
   for (int q = 0; q < DQ; ++q) {
     const int d = 16 * q + c;
+    const float ilq = d < D ? 1.f / hyp[3 + (ard ? d : 0)] : 0.f;
     float lp = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * I + 4 * g + r;
-      const float x = xs1(row, q);
+      const float x = xs[row * XS + d];
       const float e = x * w1r[r] - wx[q][r];   // = -dxs / 2
       if ((FULL || row < N) && d < D) {
-        if (a.dX != nullptr) a.dX[((size_t)b * N + row) * D + d] = -2.f * e * ilp[q];
+        if (a.dX != nullptr) a.dX[((size_t)b * N + row) * D + d] = -2.f * e * ilq;
         lp = __builtin_fmaf(x, e, lp);
       }
     }
@@ -515,12 +502,19 @@ int launch_solve(const GpkExactGradArgs& a, hipStream_t stream) {
 template <int DQ>
 int launch_gram(const GpkExactGradArgs& a, hipStream_t stream) {
   const int NB = (a.N + 15) / 16;
-  const long long grid = (long long)a.B * ((NB + 3) / 4);
-  if (grid > 0x7fffffff) return -6;
+  const size_t lds = sizeof(float) * (size_t)(16 * NB) * (16 * DQ + 4 + 2);
+  static std::once_flag once;
+  std::call_once(once, [&] {
+    (void)hipFuncSetAttribute((const void*)gpk_grad_gram_kernel<DQ, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)gpk_grad_gram_kernel<DQ, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();
+  });
   if (a.N == 16 * NB)
-    hipLaunchKernelGGL((gpk_grad_gram_kernel<DQ, true>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((gpk_grad_gram_kernel<DQ, true>), dim3(a.B), dim3(64 * kGW), lds, stream, a);
   else
-    hipLaunchKernelGGL((gpk_grad_gram_kernel<DQ, false>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((gpk_grad_gram_kernel<DQ, false>), dim3(a.B), dim3(64 * kGW), lds, stream, a);
   return (int)hipGetLastError();
 }
 
