@@ -32,6 +32,13 @@
 
 #include <mutex>
 
+// Timing experiments only (A/B builds of the solve kernel; results are wrong when set):
+// bit 1 skips the phase-1 tile math, 2 the phase-2 tile math, 4 the L staging, 8 the
+// K^-1 tile stores, 16 the alpha wave, 32 the phase-2 staging stores.
+#ifndef GPK_GRAD_SKIP
+#define GPK_GRAD_SKIP 0
+#endif
+
 namespace {
 
 constexpr int kSW = 16;          // waves of the solve kernel (one block column each)
@@ -186,7 +193,7 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
   float asum = 0.f;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   auto fetch_row = [&](const int I) -> f32x4 {    // tiles (I, K < I), row-major
-    if (tid >= I * 64) return z4;
+    if (tid >= I * 64 || (GPK_GRAD_SKIP & 4)) return z4;
     const int K = tid >> 6, q = tid & 63, m = q >> 2, cg = (q & 3) * 4;
     const int row = 16 * I + m, col0 = 16 * K + cg;
     if (FULL) return *(const f32x4*)&Lb[(size_t)row * N + col0];
@@ -201,7 +208,7 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
     *(f32x4*)&buf[K * 256 + m * 16 + cg] = v;
   };
   auto fetch_col = [&](const int I) -> f32x4 {    // tiles (K > I, I), read by rows
-    if (tid >= (NB - 1 - I) * 64) return z4;
+    if (tid >= (NB - 1 - I) * 64 || (GPK_GRAD_SKIP & 4)) return z4;
     const int sl = tid >> 6, q = tid & 63, k = q >> 2, cg = (q & 3) * 4;
     const int row = 16 * (I + 1 + sl) + k, col0 = 16 * I + cg;
     if (FULL) return *(const f32x4*)&Lb[(size_t)row * N + col0];
@@ -227,22 +234,21 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
     const f32x4 nxt = (I + 2 < NB) ? fetch_row(I + 2) : ((I + 2 == NB + 1 && NB >= 2) ? fetch_col(NB - 2) : z4);
     const float* buf = stg + (I & 1) * TS;
     const int I16 = opaque_s(16 * I);
-    if (live) {
+    if (live && !(GPK_GRAD_SKIP & 1)) {
       if (I == J) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) X[I][r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
       } else if (I > J) {
-        f32x4 s0 = z4, s1 = z4;
+        f32x4 s[4] = {z4, z4, z4, z4};   // 4 independent MFMA chains
 #pragma unroll
         for (int K = 0; K < I; ++K) {
           if (K >= J) {
             const f32x4 la = *(const f32x4*)&buf[K * 256 + c * 16 + 4 * g];
-            if (K & 1) s1 = mfma4(la, X[K], s1);
-            else s0 = mfma4(la, X[K], s0);
+            s[K & 3] = mfma4(la, X[K], s[K & 3]);
           }
         }
         const f32x4 di = *(const f32x4*)&dinv[I16 * 16 + c * 16 + 4 * g];
-        X[I] = -mfma4(di, s0 + s1, z4);
+        X[I] = -mfma4(di, (s[0] + s[1]) + (s[2] + s[3]), z4);
       }
     }
     lds_barrier();
@@ -256,40 +262,38 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
     const f32x4 nxt = (I > 1) ? fetch_col(I - 2) : z4;
     const float* buf = stg + (st & 1) * TS;
     const int I16 = opaque_s(16 * I);
-    if (live && I >= J) {
-      f32x4 s0 = z4, s1 = z4;
+    if (live && I >= J && !(GPK_GRAD_SKIP & 2)) {
+      f32x4 s[4] = {z4, z4, z4, z4};   // 4 independent MFMA chains
 #pragma unroll
       for (int K = I + 1; K < NB; ++K) {
         const f32x4 la = *(const f32x4*)&buf[(K - I - 1) * 256 + c * 16 + 4 * g];
-        if (K & 1) s1 = mfma4(la, X[K], s1);
-        else s0 = mfma4(la, X[K], s0);
+        s[K & 3] = mfma4(la, X[K], s[K & 3]);
       }
-      const f32x4 t = X[I] - s0 - s1;
+      const f32x4 t = X[I] - ((s[0] + s[1]) + (s[2] + s[3]));
       f32x4 dt;
 #pragma unroll
       for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
       const f32x4 U = mfma4(dt, t, z4);
       X[I] = U;
-      *(f32x4*)&wsb[ws.kinv + (size_t)tile_index(I, J) * 256 + lane * 4] = U;
+      if (!(GPK_GRAD_SKIP & 8)) *(f32x4*)&wsb[ws.kinv + (size_t)tile_index(I, J) * 256 + lane * 4] = U;
     }
     // alpha = L^-T z by the same back substitution (right-hand side z in column 0 of the
     // tiles), run by wave AW: an idle wave when NB < 16, else wave 15 once its own
     // column (one tile, step NB-1) is done
-    if (wave == AW) {
+    if (wave == AW && !(GPK_GRAD_SKIP & 18)) {
       if (I == NB - 1) {
 #pragma unroll
         for (int K = 0; K < NB; ++K)
 #pragma unroll
           for (int r = 0; r < 4; ++r) X[K][r] = c == 0 ? sv[16 * K + 4 * g + r] : 0.f;
       }
-      f32x4 s0 = z4, s1 = z4;
+      f32x4 s[4] = {z4, z4, z4, z4};   // 4 independent MFMA chains
 #pragma unroll
       for (int K = I + 1; K < NB; ++K) {
         const f32x4 la = *(const f32x4*)&buf[(K - I - 1) * 256 + c * 16 + 4 * g];
-        if (K & 1) s1 = mfma4(la, X[K], s1);
-        else s0 = mfma4(la, X[K], s0);
+        s[K & 3] = mfma4(la, X[K], s[K & 3]);
       }
-      const f32x4 t = X[I] - s0 - s1;
+      const f32x4 t = X[I] - ((s[0] + s[1]) + (s[2] + s[3]));
       f32x4 dt;
 #pragma unroll
       for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
@@ -308,7 +312,7 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
       }
     }
     lds_barrier();
-    if (I > 1) put_col(stg + (st & 1) * TS, I - 2, nxt);
+    if (I > 1 && !(GPK_GRAD_SKIP & 32)) put_col(stg + (st & 1) * TS, I - 2, nxt);
   }
   if (wave == AW) {
     asum = wave_sum(asum);
