@@ -30,6 +30,13 @@
 
 #include <mutex>
 
+// Timing experiments only (A/B builds of the adjoint; results are wrong when set): bit 1
+// skips A = L^-1 K_ZX, 2 dK = L^-T dA, 4 the dA / K_ZX workspace stores, 8 the Q / Q^T zs /
+// QX section, 16 the q column sums, 32 the dX loop.
+#ifndef GPK_VAR_SKIP
+#define GPK_VAR_SKIP 0
+#endif
+
 namespace {
 
 constexpr float kLog2PiF = 1.8378770664093453f;
@@ -42,6 +49,14 @@ GPK_DEVICE f64x4 mfma64(double a, double b, f64x4 c) {
 }
 GPK_DEVICE f32x4 mfma32(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// Sum over the 16 lanes of a row (lanes sharing g), DPP only.
+GPK_DEVICE float row16_sum_f(float v) {
+#define GPK_DPP_ADD(ctrl) \
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false));
+  GPK_DPP_ADD(0xB1) GPK_DPP_ADD(0x4E) GPK_DPP_ADD(0x141) GPK_DPP_ADD(0x140)
+#undef GPK_DPP_ADD
+  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -722,7 +737,13 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     build_kzx<MB, TW>(zs, xs, zn, xn, M, nvalid, Dq, ds, s2, Kl);
     lds_barrier();
     f64x4 acc[G::RT][G::CT];
-    gemm_linv_k<MB>(Linv, Kl, M, acc);
+    if (!(GPK_VAR_SKIP & 1)) gemm_linv_k<MB>(Linv, Kl, M, acc);
+    else {
+#pragma unroll
+      for (int j = 0; j < G::RT; ++j)
+#pragma unroll
+        for (int q = 0; q < G::CT; ++q) acc[j][q] = f64x4{0.1, 0.1, 0.1, 0.1};
+    }
     // variance -> clamp mask (no gradient below the clamp)
 #pragma unroll
     for (int q = 0; q < G::CT; ++q) {
@@ -764,7 +785,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
           const float gm = gmc[col], gv = gvc[col];
           const float da = gm * vm[row] + 2.f * gv * sm1[row] * a32;
           dAl[row * TW + col] = da;
-          if (row < M && col < nvalid) wsdA[(size_t)row * BN + col0 + col] = da;
+          if (row < M && col < nvalid && !(GPK_VAR_SKIP & 4)) wsdA[(size_t)row * BN + col0 + col] = da;
           pm = __builtin_fmaf(gm, a32, pm);
           ps = __builtin_fmaf(gv, a32 * a32, ps);
         }
@@ -780,7 +801,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       }
     }
     // K_ZX -> workspace (row-major M x BN, coalesced along points)
-    for (int e = tid; e < M * TW; e += blockDim.x) {
+    for (int e = tid; e < M * TW && !(GPK_VAR_SKIP & 4); e += blockDim.x) {
       const int p = e / TW, col = e - p * TW;
       if (col < nvalid) wsK[(size_t)p * BN + col0 + col] = Kl[p * TW + col];
     }
@@ -813,7 +834,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         }
       };
       load_blk(first, an);
-      for (int kb = first; kb < MB; ++kb) {
+      for (int kb = first; kb < MB && !(GPK_VAR_SKIP & 2); ++kb) {
         double a[G::RT][4];
 #pragma unroll
         for (int j = 0; j < G::RT; ++j)
@@ -849,7 +870,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 #pragma unroll
     for (int j = 0; j < G::RT; ++j) {
       const int rt = wr + G::WR * j;
-      if (rt >= MB) continue;
+      if (rt >= MB || (GPK_VAR_SKIP & 8)) continue;
 #pragma unroll
       for (int q = 0; q < G::CT; ++q) {
         const int col = 16 * (wc * G::CT + q) + c;
@@ -899,20 +920,20 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 #pragma unroll
     for (int u = 0; u < MAXQT; ++u) {
       const int tq = wave + 4 * u;
-      if (tq < MB * NDT) {
+      if (tq < MB * NDT && !(GPK_VAR_SKIP & 8)) {
         const int pt = tq / NDT, dt = tq - pt * NDT;
         for (int k = 0; k < TW / 4; ++k)
           qx[u] = mfma32(dAl[(4 * k + g) * QST + 16 * pt + c], xs[(4 * k + g) * ds + 16 * dt + c], qx[u]);
       }
     }
-    for (int p = tid; p < MP; p += blockDim.x) {
+    for (int p = tid; p < MP && !(GPK_VAR_SKIP & 16); p += blockDim.x) {
       float v = 0.f;
       for (int i = 0; i < TW; ++i) v += dAl[i * QST + p];
       qacc[p] += v;
     }
     lds_barrier();  // Q^T zs partials and r complete
     // dX per point; sum_i r_i xs_i^2 per d (thread tid always sees d = tid % Dq)
-    for (int e = tid; e < TW * Dq; e += blockDim.x) {
+    for (int e = tid; e < TW * Dq && !(GPK_VAR_SKIP & 32); e += blockDim.x) {
       const int col = e / Dq, d = e - col * Dq;
       float v = 0.f;
       for (int q = 0; q < G::WR; ++q) v += Kl[(q * TW + col) * Dq + d];
@@ -1179,6 +1200,538 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
 }
 
 // ---------------------------------------------------------------------------
+// Register-resident variants for M <= 64, D <= 32 (BASELINE cfg 5: M = 64, D = 32).
+// With at most 4 row tiles every wave owns ALL rows of its points, so the waves of a
+// workgroup never exchange data: each wave walks its own 32-point chunks (2 column
+// tiles) and keeps K_ZX, A = L^{-1} K_ZX, dA, dK and Q in MFMA registers. The f32 Gram
+// feeds the zs rows in the order pi(x) = (x >> 2) + 4 (x & 3), so its accumulator holds
+// row g + 4r in register r -- the f64 MFMA layout -- and K_ZX tiles are directly the B
+// operands of the f64 products. L^{-1} (fp64, row stride 66: conflict-free reads) and zs
+// live in LDS, shared by the 4 waves; only the adjoint's Q^T needs a per-wave LDS
+// transpose (one tile at a time).
+// ---------------------------------------------------------------------------
+constexpr int RLS = 66;        // L^{-1} row stride (doubles)
+
+template <int DQ>
+struct RegLds {
+  static constexpr int ZS = DQ + 1;
+  static constexpr int zs = 0;                      // 64 x ZS
+  static constexpr int zn = zs + 64 * ZS;           // 64
+  static constexpr int vm = zn + 64;                // 64
+  static constexpr int sm1 = vm + 64;               // 64
+  static constexpr int cm = sm1 + 64;               // DQ
+  static constexpr int li = ((cm + DQ + 3) / 4) * 4;          // 64 x RLS doubles (16-B aligned)
+  static constexpr int fwd_total = li + 2 * 64 * RLS;
+  // adjoint only: per-wave transpose scratch, per-wave row accumulators, reductions
+  static constexpr int scr = fwd_total;             // 4 x 320
+  static constexpr int rows = scr + 4 * 320;        // 4 waves x 3 x 64 (dvm, dsm, q)
+  static constexpr int qxr = rows + 4 * 3 * 64;     // 64 x DQ  (workgroup QX)
+  static constexpr int misc = qxr + 64 * DQ;        // 4 x (2 DQ + 3)
+  static constexpr int adj_total = misc + 4 * (2 * DQ + 3);
+};
+
+// stage zs, norms, q(u) moments (stage_inducing) and L^{-1} (zero padded to 64 x 64)
+template <int DQ>
+GPK_DEVICE void stage_reg(const float* Z, const float* ls, const float* vmean, const float* vstd,
+                          const double* Linv, int M, int D, float* sm) {
+  using L = RegLds<DQ>;
+  stage_inducing(Z, ls, vmean, vstd, M, D, 64, DQ, L::ZS, sm + L::zs, sm + L::zn, sm + L::cm,
+                 sm + L::vm, sm + L::sm1);
+  double* li = (double*)(sm + L::li);
+  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
+    const int r = e >> 6, c = e & 63;
+    li[r * RLS + c] = (r < M && c < M) ? Linv[(size_t)r * M + c] : 0.0;
+  }
+  lds_barrier();
+}
+
+GPK_DEVICE int pi_row(int x) { return (x >> 2) + 4 * (x & 3); }
+
+// Per-chunk LDS base the compiler must treat as new on every iteration: the staged
+// operands (L^{-1}, zs, norms) would otherwise be hoisted out of the chunk loop as
+// loop-invariant loads and pinned in (hundreds of) registers.
+GPK_DEVICE const float* fresh_lds(const float* p) {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return p + z;
+}
+
+// Points i0 + 16q + c of window b: Gram B operands xb[q][s] = xs[i][4s + g], squared
+// norms (full, every lane), and optionally x . w (full).
+template <int DQ>
+struct RegPoints {
+  float xb[2][DQ / 4];
+  float xn[2];
+  float lin[2];
+};
+
+template <int DQ, bool LIN>
+GPK_DEVICE void load_points(const float* X, int N, int D, int b, int i0, const float (&il)[DQ / 4],
+                            const float (&cmv)[DQ / 4], const float (&wv)[DQ / 4], RegPoints<DQ>& P) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = i0 + 16 * q + c;
+    const bool ok = i < N;
+    const float* xr = X + ((size_t)b * N + (ok ? i : 0)) * D;
+    float nn = 0.f, lw = 0.f;
+#pragma unroll
+    for (int s = 0; s < DQ / 4; ++s) {
+      const int d = 4 * s + g;
+      const float raw = (ok && d < D) ? xr[d] : 0.f;
+      const float v = (d < D) ? raw * il[s] - cmv[s] : 0.f;
+      P.xb[q][s] = ok ? v : 0.f;
+      nn = __builtin_fmaf(P.xb[q][s], P.xb[q][s], nn);
+      if (LIN) lw = __builtin_fmaf(raw, wv[s], lw);
+    }
+    nn += __shfl_xor(nn, 16, 64);
+    nn += __shfl_xor(nn, 32, 64);
+    P.xn[q] = nn;
+    if (LIN) {
+      lw += __shfl_xor(lw, 16, 64);
+      lw += __shfl_xor(lw, 32, 64);
+      P.lin[q] = lw;
+    }
+  }
+}
+
+// K_ZX tiles (register r <-> row 16 rt + g + 4r, column 16q + c), zero outside M x N
+template <int DQ>
+GPK_DEVICE void build_k_reg(const float* sm, const RegPoints<DQ>& P, int M, int N, int i0, float s2,
+                            f32x4 (&K)[4][2]) {
+  using L = RegLds<DQ>;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const float* zs = sm + L::zs;
+  const float* zn = sm + L::zn;
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt) {
+    float za[DQ / 4];
+#pragma unroll
+    for (int s = 0; s < DQ / 4; ++s) za[s] = zs[(16 * rt + pi_row(c)) * L::ZS + 4 * s + g];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < DQ / 4; ++s) acc = mfma32(za[s], P.xb[q][s], acc);
+      const bool ok = i0 + 16 * q + c < N;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = 16 * rt + g + 4 * r;
+        const float d2 = __builtin_fmaxf(zn[p] + P.xn[q] - 2.f * acc[r], 0.f);
+        K[rt][q][r] = (ok && p < M) ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * d2) : 0.f;
+      }
+    }
+  }
+}
+
+// A = L^{-1} K (fp64 MFMA, k-order m = 16 kb + g + 4u; L^{-1} lower: kb <= rt), one row
+// tile at a time, cast to fp32 as the reference does (A.float()): the f64 accumulators of
+// only one row tile are live at a time.
+template <int DQ>
+GPK_DEVICE void linv_times_k(const float* sm, const f32x4 (&K)[4][2], f32x4 (&A)[4][2]) {
+  using L = RegLds<DQ>;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const double* li = (const double*)(sm + L::li);
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt) {
+    f64x4 acc[2] = {f64x4{0.0, 0.0, 0.0, 0.0}, f64x4{0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+    for (int kb = 0; kb <= rt; ++kb)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double la = li[(16 * rt + c) * RLS + 16 * kb + g + 4 * u];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc[q] = mfma64(la, (double)K[kb][q][u], acc[q]);
+      }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) A[rt][q][r] = (float)acc[q][r];
+  }
+}
+
+// per-lane constants of the dims this lane touches as a Gram operand: 4s + g
+template <int DQ>
+GPK_DEVICE void dim_consts(const float* sm, const float* ls, const float* w, int D, float (&il)[DQ / 4],
+                           float (&cmv)[DQ / 4], float (&wv)[DQ / 4]) {
+  using L = RegLds<DQ>;
+  const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int s = 0; s < DQ / 4; ++s) {
+    const int d = 4 * s + g;
+    il[s] = d < D ? 1.f / ls[d] : 0.f;
+    cmv[s] = sm[L::cm + d];
+    wv[s] = (d < D && w != nullptr) ? w[d] : 0.f;
+  }
+}
+
+template <int DQ>
+__global__ void __launch_bounds__(256)
+gpk_var_fwd_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                     const double* __restrict__ Linv, const float* __restrict__ vmean,
+                     const float* __restrict__ vstd, const float* __restrict__ hyp, int B, int N,
+                     int M, int D, float* __restrict__ mean_out, float* __restrict__ var_out,
+                     int* __restrict__ flags) {
+  using L = RegLds<DQ>;
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const float s2 = hyp[0], jit = hyp[2], b0 = hyp[3];
+  const float* w = hyp + 4;
+  const float* ls = hyp + 4 + D;
+  stage_reg<DQ>(Z, ls, vmean, vstd, Linv, M, D, vsm);
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = threadIdx.x >> 6;
+  float il[DQ / 4], cmv[DQ / 4], wv[DQ / 4];
+  dim_consts<DQ>(vsm, ls, w, D, il, cmv, wv);
+  const int nch = (N + 31) / 32;
+  const long long total = (long long)B * nch;
+  int clamped = 0;
+  for (long long t = (long long)blockIdx.x * 4 + wave; t < total; t += (long long)gridDim.x * 4) {
+    const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
+    const float* sm = fresh_lds(vsm);
+    const float* vm = sm + L::vm;
+    const float* sm1 = sm + L::sm1;
+    RegPoints<DQ> P;
+    load_points<DQ, true>(X, N, D, b, i0, il, cmv, wv, P);
+    f32x4 K[4][2];
+    build_k_reg<DQ>(sm, P, M, N, i0, s2, K);
+    f32x4 A[4][2];
+    linv_times_k<DQ>(sm, K, A);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float mp = 0.f, vp = 0.f;
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * rt + g + 4 * r;
+          const float a32 = A[rt][q][r];   // A is cast to fp32 (reference)
+          mp = __builtin_fmaf(a32, vm[p], mp);
+          vp = __builtin_fmaf(a32 * a32, sm1[p], vp);
+        }
+      mp += __shfl_xor(mp, 16, 64);
+      mp += __shfl_xor(mp, 32, 64);
+      vp += __shfl_xor(vp, 16, 64);
+      vp += __shfl_xor(vp, 32, 64);
+      const int i = i0 + 16 * q + c;
+      if (g == q && i < N) {
+        float var_i = s2 + jit + vp;
+        if (var_i < 1e-6f) { var_i = 1e-6f; clamped = 1; }   // MVN.variance clamp (fp32)
+        mean_out[(size_t)b * N + i] = mp + (P.lin[q] + b0);
+        var_out[(size_t)b * N + i] = var_i;
+      }
+    }
+  }
+  if (flags != nullptr && clamped)
+    (void)__hip_atomic_fetch_or(flags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int DQ>
+__global__ void __launch_bounds__(256, 2)
+gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                     const double* __restrict__ Linv, const float* __restrict__ vmean,
+                     const float* __restrict__ vstd, const float* __restrict__ hyp,
+                     const float* __restrict__ gmean, const float* __restrict__ gvar, int B, int N,
+                     int M, int D, long long BN, float* __restrict__ wsdA, float* __restrict__ wsK,
+                     float* __restrict__ wspart, float* __restrict__ dX) {
+  using L = RegLds<DQ>;
+  constexpr int NDT = DQ / 16;
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const float s2 = hyp[0], jit = hyp[2];
+  const float* w = hyp + 4;
+  const float* ls = hyp + 4 + D;
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int wave = tid >> 6;
+  stage_reg<DQ>(Z, ls, vmean, vstd, Linv, M, D, vsm);
+  float* rows = vsm + L::rows + wave * 3 * 64;    // this wave's dvm | dsm | q accumulators
+  for (int e = lane; e < 3 * 64; e += 64) rows[e] = 0.f;
+  float* scr = vsm + L::scr + wave * 320;
+  float il[DQ / 4], cmv[DQ / 4], wv[DQ / 4];
+  dim_consts<DQ>(vsm, ls, nullptr, D, il, cmv, wv);
+  // constants of the dims 16 dt + c (QX / dX operands)
+  float ilc[NDT], cmc[NDT], wc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    const int d = 16 * dt + c;
+    ilc[dt] = d < D ? 1.f / ls[d] : 0.f;
+    cmc[dt] = vsm[L::cm + d];
+    wc[dt] = d < D ? w[d] : 0.f;
+  }
+  f32x4 qx[4][NDT];
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) qx[rt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rx2[NDT] = {}, gx[NDT] = {};
+  float sumQ = 0.f, sumgv = 0.f, sumgm = 0.f;
+
+  const int nch = (N + 31) / 32;
+  const long long total = (long long)B * nch;
+  for (long long t = (long long)blockIdx.x * 4 + wave; t < total; t += (long long)gridDim.x * 4) {
+    const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
+    const size_t col0 = (size_t)b * N;
+    const float* sm = fresh_lds(vsm);
+    const float* zs = sm + L::zs;
+    const float* vm = sm + L::vm;
+    const float* sm1 = sm + L::sm1;
+    const double* li = (const double*)(sm + L::li);
+    RegPoints<DQ> P;
+    load_points<DQ, false>(X, N, D, b, i0, il, cmv, wv, P);
+    f32x4 K[4][2];
+    build_k_reg<DQ>(sm, P, M, N, i0, s2, K);
+    f32x4 A[4][2];
+    linv_times_k<DQ>(sm, K, A);
+    // variance -> clamp mask; point gradients
+    float gmq[2], gvq[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float vp = 0.f;
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float a32 = A[rt][q][r];
+          vp = __builtin_fmaf(a32 * a32, sm1[16 * rt + g + 4 * r], vp);
+        }
+      vp += __shfl_xor(vp, 16, 64);
+      vp += __shfl_xor(vp, 32, 64);
+      const int i = i0 + 16 * q + c;
+      const bool ok = i < N;
+      gmq[q] = ok ? gmean[col0 + i] : 0.f;
+      gvq[q] = ok ? gvar[col0 + i] : 0.f;
+      if (s2 + jit + vp < 1e-6f) gvq[q] = 0.f;   // clamp_min(1e-6): gradient masked
+      if (g == 0) {
+        sumgv += gvq[q];
+        sumgm += gmq[q];
+      }
+    }
+    // dA (fp32, in A's registers) and the dvmean / dvstd row partials
+    f32x4 (&dA)[4][2] = A;
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = 16 * rt + g + 4 * r;
+        const float vmp = vm[p], smp = sm1[p];
+        float pm = 0.f, ps = 0.f;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float a32 = A[rt][q][r];
+          dA[rt][q][r] = gmq[q] * vmp + 2.f * gvq[q] * smp * a32;
+          pm = __builtin_fmaf(gmq[q], a32, pm);
+          ps = __builtin_fmaf(gvq[q], a32 * a32, ps);
+        }
+        pm = row16_sum_f(pm);
+        ps = row16_sum_f(ps);
+        if (c == 0) {
+          rows[p] += pm;
+          rows[64 + p] += ps;
+        }
+      }
+    // dA and K_ZX -> workspace (for dL^{-1} = sum dA K^T)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = i0 + 16 * q + c;
+      if (i < N) {
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int p = 16 * rt + g + 4 * r;
+            if (p < M) {
+              wsdA[(size_t)p * BN + col0 + i] = dA[rt][q][r];
+              wsK[(size_t)p * BN + col0 + i] = K[rt][q][r];
+            }
+          }
+      }
+    }
+    // dK = L^{-T} dA (fp64; L^{-T} upper: kb >= rt), then Q = dK o K_ZX (in K's registers)
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      f64x4 acc[2] = {f64x4{0.0, 0.0, 0.0, 0.0}, f64x4{0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+      for (int kb = rt; kb < 4; ++kb)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double la = li[(16 * kb + g + 4 * u) * RLS + 16 * rt + c];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) acc[q] = mfma64(la, (double)dA[kb][q][u], acc[q]);
+        }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) K[rt][q][r] = (float)acc[q][r] * K[rt][q][r];
+    }
+    // r_i = sum_p Q_pi (every lane c of a column), q_p row partials, sum Q
+    float rq[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float v = 0.f;
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) v += (K[rt][q][0] + K[rt][q][1]) + (K[rt][q][2] + K[rt][q][3]);
+      sumQ += v;
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      rq[q] = v;
+    }
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = row16_sum_f(K[rt][0][r] + K[rt][1][r]);
+        if (c == 0) rows[128 + 16 * rt + g + 4 * r] += v;
+      }
+    // (Q^T zs)_i: f32 MFMA with k = p (rows g + 4r of each row tile)
+    f32x4 xz[2][NDT];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) xz[q][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const float zb = zs[(16 * rt + g + 4 * r) * L::ZS + 16 * dt + c];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) xz[q][dt] = mfma32(K[rt][q][r], zb, xz[q][dt]);
+        }
+    // QX_p += sum_i Q_pi xs_i: Q tiles transposed through LDS (k = point 4s + g)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float xb2[4][NDT];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int i = i0 + 16 * q + 4 * s + g;
+        const bool ok = i < N;
+        const float* xr = X + (col0 + (ok ? i : 0)) * D;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int d = 16 * dt + c;
+          xb2[s][dt] = (ok && d < D) ? xr[d] * ilc[dt] - cmc[dt] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = K[rt][q][r];
+        wave_lds_sync();
+        float aq[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) aq[s] = scr[((c & 3) * 16 + 4 * s + g) * 5 + (c >> 2)];
+        wave_lds_sync();   // the next tile overwrites scr
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) qx[rt][dt] = mfma32(aq[s], xb2[s][dt], qx[rt][dt]);
+      }
+    }
+    // dX_i = ((Q^T zs)_i - xs_i r_i) / l + gmean_i w; sum_i r_i xs_i^2, sum_i gmean_i xs_i
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pc = 4 * g + r;                  // point (within the tile) of register r
+        const float rr = __shfl(rq[q], pc, 64);
+        const float gm = __shfl(gmq[q], pc, 64);
+        const int i = i0 + 16 * q + pc;
+        if (i < N) {
+          const float* xr = X + (col0 + i) * D;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const int d = 16 * dt + c;
+            if (d < D) {
+              const float xv = xr[d] * ilc[dt] - cmc[dt];
+              dX[(col0 + i) * D + d] = (xz[q][dt][r] - xv * rr) * ilc[dt] + gm * wc[dt];
+              rx2[dt] = __builtin_fmaf(rr * xv, xv, rx2[dt]);
+              gx[dt] = __builtin_fmaf(gm, xv, gx[dt]);
+            }
+          }
+        }
+      }
+  }
+
+  // ---- workgroup partials, summed over the waves in a fixed order:
+  //   [QX (M x D) | q (M) | dvm (M) | dsm (M) | rx2 (D) | sumQ | sumgv | gx (D) | sumgm]
+  float* qxr = vsm + L::qxr;
+  float* misc = vsm + L::misc + wave * (2 * DQ + 3);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    float v = rx2[dt], u = gx[dt];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    u += __shfl_xor(u, 16, 64);
+    u += __shfl_xor(u, 32, 64);
+    if (g == 0) {
+      misc[16 * dt + c] = v;
+      misc[DQ + 16 * dt + c] = u;
+    }
+  }
+  sumQ = wave_sum(sumQ);
+  sumgv = wave_sum(sumgv);
+  sumgm = wave_sum(sumgm);
+  if (lane == 0) {
+    misc[2 * DQ] = sumQ;
+    misc[2 * DQ + 1] = sumgv;
+    misc[2 * DQ + 2] = sumgm;
+  }
+  for (int wv2 = 0; wv2 < 4; ++wv2) {
+    lds_barrier();
+    if (wave == wv2) {
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int e = (16 * rt + 4 * g + r) * DQ + 16 * dt + c;
+            qxr[e] = (wv2 == 0 ? 0.f : qxr[e]) + qx[rt][dt][r];
+          }
+    }
+  }
+  lds_barrier();
+  const int P = M * D + 3 * M + 2 * D + 3;
+  float* po = wspart + (size_t)blockIdx.x * P;
+  for (int e = tid; e < M * D; e += blockDim.x) {
+    const int p = e / D, d = e - p * D;
+    po[e] = qxr[p * DQ + d];
+  }
+  const float* rw = vsm + L::rows;
+  for (int m = tid; m < M; m += blockDim.x) {
+    float a = 0.f, s = 0.f, qq = 0.f;
+    for (int u = 0; u < 4; ++u) {
+      a += rw[u * 192 + m];
+      s += rw[u * 192 + 64 + m];
+      qq += rw[u * 192 + 128 + m];
+    }
+    po[M * D + m] = qq;
+    po[M * D + M + m] = a;
+    po[M * D + 2 * M + m] = s;
+  }
+  const float* ms = vsm + L::misc;
+  for (int d = tid; d < D; d += blockDim.x) {
+    float v = 0.f, u = 0.f;
+    for (int k = 0; k < 4; ++k) {
+      v += ms[k * (2 * DQ + 3) + d];
+      u += ms[k * (2 * DQ + 3) + DQ + d];
+    }
+    po[M * D + 3 * M + d] = v;
+    po[M * D + 3 * M + D + 2 + d] = u;
+  }
+  if (tid == 0) {
+    float a = 0.f, v = 0.f, u = 0.f;
+    for (int k = 0; k < 4; ++k) {
+      a += ms[k * (2 * DQ + 3) + 2 * DQ];
+      v += ms[k * (2 * DQ + 3) + 2 * DQ + 1];
+      u += ms[k * (2 * DQ + 3) + 2 * DQ + 2];
+    }
+    po[M * D + 3 * M + D] = a;
+    po[M * D + 3 * M + D + 1] = v;
+    po[M * D + 3 * M + 2 * D + 2] = u;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 template <int MB>
@@ -1247,12 +1800,31 @@ struct AdjPlan {
   size_t fin_lds;
 };
 
+// register-resident path (M <= 64, D <= 32): 32-point chunks, one per wave, 4 waves per
+// workgroup, 2 workgroups per CU
+#ifndef GPK_VAR_REG
+#define GPK_VAR_REG 1   // 0: A/B builds without the register-resident path
+#endif
+GPK_HOST_DEVICE_INLINE bool var_reg_path(int M, int D) { return GPK_VAR_REG && M <= 64 && D <= 32; }
+
+AdjPlan adj_plan_common(AdjPlan p, int B, int N, int M, int D);
+
 template <int MB>
 AdjPlan adj_plan(int B, int N, int M, int D) {
   using G = VarGeo<MB>;
   AdjPlan p{};
+  if (var_reg_path(M, D)) {
+    const long long nch = (long long)B * ((N + 31) / 32);
+    p.nchunks = (int)nch;
+    p.nwg = (int)((nch + 3) / 4 < 512 ? (nch + 3) / 4 : 512);
+    return adj_plan_common(p, B, N, M, D);
+  }
   p.nchunks = B * ((N + G::TW - 1) / G::TW);
   p.nwg = chunk_grid(p.nchunks, 2);
+  return adj_plan_common(p, B, N, M, D);
+}
+
+AdjPlan adj_plan_common(AdjPlan p, int B, int N, int M, int D) {
   p.P = M * D + 3 * M + 2 * D + 3;
   p.fin_lds = (size_t)M * D * sizeof(float);
   p.BN = (long long)B * N;
@@ -1276,26 +1848,66 @@ AdjPlan adj_plan(int B, int N, int M, int D) {
   return p;
 }
 
+template <int DQ>
+int launch_var_fwd_r(const GpkVarArgs& a, int* flags, hipStream_t stream) {
+  const size_t lds = (size_t)RegLds<DQ>::fwd_total * sizeof(float);
+  set_lds_once<gpk_var_fwd_r_kernel<DQ>>();
+  const long long nch = (long long)a.B * ((a.N + 31) / 32);
+  const long long nwg = (nch + 3) / 4 < 768 ? (nch + 3) / 4 : 768;
+  hipLaunchKernelGGL((gpk_var_fwd_r_kernel<DQ>), dim3((unsigned)nwg), dim3(256), lds, stream, a.X, a.Z,
+                     a.Linv, a.vmean, a.vstd, a.hyp, a.B, a.N, a.M, a.D, a.mean, a.var, flags);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  if (a.ell != nullptr) {
+    hipLaunchKernelGGL(gpk_var_ell_kernel, dim3(a.B), dim3(256), 0, stream, a.mean, a.var, a.y,
+                       a.hyp, a.N, a.ell);
+    e = hipGetLastError();
+  }
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t stream);
+
 template <int MB, int DQ>
 int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
+  const AdjPlan p = adj_plan<MB>(a.B, a.N, a.M, a.D);
+  char* ws = (char*)a.ws;
+  float* wsdA = (float*)(ws + p.off_dA);
+  float* wsK = (float*)(ws + p.off_K);
+  float* wspart = (float*)(ws + p.off_part);
+  if (var_reg_path(a.M, a.D)) {
+    constexpr int RQ = DQ <= 16 ? 16 : 32;
+    const size_t lds = (size_t)RegLds<RQ>::adj_total * sizeof(float);
+    set_lds_once<gpk_var_adj_r_kernel<RQ>>();
+    hipLaunchKernelGGL((gpk_var_adj_r_kernel<RQ>), dim3(p.nwg), dim3(256), lds, stream, a.X, a.Z,
+                       a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.B, a.N, a.M, a.D, p.BN,
+                       wsdA, wsK, wspart, a.dX);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    return launch_var_adj_tail(a, p, stream);
+  }
   const size_t lds = var_adj_lds<MB, DQ>();
   if (lds > 160 * 1024) return -12;
   set_lds_once<gpk_var_adj_kernel<MB, DQ>>();
-  const AdjPlan p = adj_plan<MB>(a.B, a.N, a.M, a.D);
+  hipLaunchKernelGGL((gpk_var_adj_kernel<MB, DQ>), dim3(p.nwg), dim3(256), lds, stream, a.X, a.Z,
+                     a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.N, a.M, a.D, p.nchunks,
+                     p.BN, wsdA, wsK, wspart, a.dX);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  return launch_var_adj_tail(a, p, stream);
+}
+
+// dL^{-1} GEMM, the fixed-order reductions and the outputs (both adjoint paths)
+int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t stream) {
   char* ws = (char*)a.ws;
   float* wsdA = (float*)(ws + p.off_dA);
   float* wsK = (float*)(ws + p.off_K);
   float* wspart = (float*)(ws + p.off_part);
   double* tot = (double*)(ws + p.off_tot);
   double* dl = (double*)(ws + p.off_dl);
-  hipLaunchKernelGGL((gpk_var_adj_kernel<MB, DQ>), dim3(p.nwg), dim3(256), lds, stream, a.X, a.Z,
-                     a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.N, a.M, a.D, p.nchunks,
-                     p.BN, wsdA, wsK, wspart, a.dX);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(gpk_dlinv_kernel, dim3(p.ntiles * p.nsplit), dim3(256), 0, stream, wsdA, wsK,
                      a.M, p.BN, p.ntiles, p.cols_per_split, dl);
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const long long nred = (p.P + 31) / 32 + ((long long)a.M * a.M + 31) / 32;
   hipLaunchKernelGGL(gpk_var_red_kernel, dim3((unsigned)nred), dim3(256), 0, stream,
@@ -1349,6 +1961,8 @@ int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream) {
     const hipError_t e = hipMemsetAsync(flags, 0, sizeof(int), stream);
     if (e != hipSuccess) return (int)e;
   }
+  if (var_reg_path(a.M, a.D)) return a.D <= 16 ? launch_var_fwd_r<16>(a, flags, stream)
+                                               : launch_var_fwd_r<32>(a, flags, stream);
 #define GPK_CALL_FWD(mb) return launch_var_fwd<mb>(a, flags, stream);
   GPK_MB_SWITCH((a.M + 15) / 16, GPK_CALL_FWD)
 #undef GPK_CALL_FWD
