@@ -67,6 +67,13 @@ def var_flops_per_window(N, M, D):  # SURVEY.md §8d cfg 5: (fp32, fp64)
     return 3 * D * M * N + 5 * M * N + 2 * D * N + 8 * N, M * M * N
 
 
+def var_adj_flops_per_window(N, M, D):
+    """Adjoint of the same window: fp32 = K_ZX recompute (3DMN + 5MN),
+    Q^T zs and Q X (2 x 2MND), elementwise dA / Q / dX (~10MN + 6DN); fp64 = A = L^-1 K_ZX,
+    dK = L^-T dA and the window's share of dL^-1 = sum dA K^T (3 x M^2 N, triangular)."""
+    return 3 * D * M * N + 5 * M * N + 4 * M * N * D + 10 * M * N + 6 * D * N, 3 * M * M * N
+
+
 def make_inputs(B, N, D, device, seed):
     g = torch.Generator().manual_seed(seed)
     X = (torch.randn(B, N, D, generator=g) / math.sqrt(D)).to(device)
@@ -210,6 +217,8 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
         ms = dict(zip(["kzz", "fwd", "bwd"], t.tolist()))
     f32, f64 = var_flops_per_window(N, M, D)
     roof_s = f64 / FP64_PEAK + f32 / FP32_PEAK          # per window, fp64 + fp32 roofs added
+    a32, a64 = var_adj_flops_per_window(N, M, D)
+    adj_roof_s = a64 / FP64_PEAK + a32 / FP32_PEAK
     t_fwd_s = ms["fwd"] * 1e-3
     achieved = (f32 + f64) * B / t_fwd_s
     return {
@@ -224,6 +233,11 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
                      "flops_per_window": {"fp32": f32, "fp64": f64},
                      "hbm_frac": var_bytes_per_window(N, D) * B / t_fwd_s / HBM_PEAK,
                      "traffic": load_traffic(f"var_B{B}_N{N}_M{M}_D{D}")},
+        "backward_roofline": {"kernel": "gpk_variational_adjoint_f32 (all launches)", "bound": "mfma",
+                              "achieved": sum(var_adj_flops_per_window(N, M, D)) * B / (ms["bwd"] * 1e-3) / 1e12,
+                              "peak": sum(var_adj_flops_per_window(N, M, D)) / adj_roof_s / 1e12,
+                              "unit": "TFLOP/s", "frac": adj_roof_s * B / (ms["bwd"] * 1e-3),
+                              "flops_per_window": dict(zip(("fp32", "fp64"), var_adj_flops_per_window(N, M, D)))},
         "mean_ell": float(out.ell.double().mean()),
         "info": int(kz.info.item()),
     }

@@ -67,7 +67,7 @@ def main():
         if k.startswith("gpk_exact_kernel"):
             summary["exact_B512_N256_D32"] = {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
                                               "source": "profiles/r02_pmc.json " + k}
-        if k.startswith("gpk_var_fwd_kernel<4>"):
+        if k.startswith("gpk_var_fwd_r_kernel<32>") or k.startswith("gpk_var_fwd_kernel<4>"):
             summary["var_B1024_N256_M64_D32"] = {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
                                                  "fetch_raw_bytes": v["fetch_kib"] * 1024,
                                                  "source": "profiles/r02_pmc.json " + k}
