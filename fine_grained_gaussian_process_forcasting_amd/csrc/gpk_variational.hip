@@ -144,8 +144,10 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
   double* P = (double*)vsm;            // Mp x 4  panel columns (phase 1) / L panel (phase 2)
   double* lb = P + Mp * 4;             // Mp x 4  l rows (phase 1) / X_k as 4 x Mp (phase 2)
   double* xr = lb + Mp * 4;            // 4 x Mp  published X rows (phase 2)
+  // phase 2 double-buffers P / lb / xr by step parity (second copies after xr), which
+  // makes the end-of-step barrier unnecessary
   const int D4 = (D + 3) & ~3;
-  float* zt = (float*)(xr + Mp * 4);   // M x D4  Z / l, centred (zero padded)
+  float* zt = (float*)(xr + Mp * 4 + 3 * Mp * 4);   // M x D4  Z / l, centred (zero padded)
   float* zn = zt + M * D4;             // M
   float* cm = zn + M;                  // D
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
@@ -157,7 +159,7 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
     const int m = e / D4, d = e - m * D4;
     zt[e] = d < D ? Z[m * D + d] / ls[d] : 0.f;
   }
-  for (int e = tid; e < Mp * 4; e += KT) { lb[e] = 0.0; P[e] = 0.0; xr[e] = 0.0; }
+  for (int e = tid; e < 6 * Mp * 4; e += KT) P[e] = 0.0;   // both parities of P / lb / xr
   lds_barrier();
   for (int d = tid; d < D; d += KT) {
     float sm = 0.f;
@@ -311,8 +313,15 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
     };
     double pn[4];
     if (tid < Mp) load_panel(0, pn);
+    double* const P0 = P;
+    double* const lb0 = lb;
+    double* const xr0 = xr;
     for (int s = 0; s < (Mp >> 2); ++s) {
       const int j0 = 4 * s, it0 = s >> 2, sub = s & 3;
+      const int par = s & 1;
+      double* P = P0 + par * (3 * Mp * 4);
+      double* lb = lb0 + par * (3 * Mp * 4);
+      double* xr = xr0 + par * (3 * Mp * 4);
 #pragma unroll
       for (int q = 0; q < NS; ++q) asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
       if (j0 + tid < Mp) {
@@ -370,8 +379,9 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
           acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc[q], 0, 0, 0);
         }
       }
-      lds_barrier();
+      // (no end-of-step barrier: step s+1 writes the other parity's P / xr / lb)
     }
+    lds_barrier();
   }
   for (int e = tid; e < M * M; e += KT) {
     const int i = e / M, j = e - i * M;
@@ -1944,7 +1954,7 @@ int launch_kzz(const GpkKzzArgs& a, size_t lds, hipStream_t stream) {
 
 int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
   const int Mp = (a.M + 15) & ~15;
-  const size_t lds = (size_t)(3 * Mp * 4) * sizeof(double) +
+  const size_t lds = (size_t)(6 * Mp * 4) * sizeof(double) +
                      (size_t)(a.M * ((a.D + 3) & ~3) + a.M + a.D) * sizeof(float);
   if (lds > 160 * 1024) return -4;
   const int T16 = Mp >> 4;
