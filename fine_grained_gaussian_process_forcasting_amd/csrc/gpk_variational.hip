@@ -76,6 +76,22 @@ GPK_DEVICE float row16_sum_f(float v) {
 // step (X -= L[:, panel] X_panel, again one MFMA per tile) -> L^{-1}.
 // ---------------------------------------------------------------------------
 constexpr int KT = 512;   // 8 waves
+// Z row stride (floats): D rounded up to the 16 dims one MFMA k-group reads, + 4, so a
+// row spans an odd number of 16-byte slots and the b128 reads of 16 rows are conflict-free
+__host__ __device__ inline int kzz_zstride(int D) { return ((D + 15) & ~15) + 4; }
+#ifndef GPK_KZZ_SKIP
+#define GPK_KZZ_SKIP 0   // timing-only A/B switches (results invalid when set)
+#endif
+#ifndef GPK_KZZ_STAMPS
+#define GPK_KZZ_STAMPS 0   // debug: phase clocks into Linv[0][1..] (results invalid when set)
+#endif
+#if GPK_KZZ_STAMPS
+#define KZ_STAMP(k) kst[k] = __builtin_amdgcn_s_memtime()
+#define KZ_ACC(k, t0) kst[k] += __builtin_amdgcn_s_memtime() - (t0)
+#else
+#define KZ_STAMP(k)
+#define KZ_ACC(k, t0)
+#endif
 
 GPK_DEVICE double rsq64(double x) {   // 1/sqrt(x), x > 0: hardware estimate + 2 Newton steps
   double y = __builtin_amdgcn_rsq(x);
@@ -146,35 +162,41 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
   double* xr = lb + Mp * 4;            // 4 x Mp  published X rows (phase 2)
   // phase 2 double-buffers P / lb / xr by step parity (second copies after xr), which
   // makes the end-of-step barrier unnecessary
-  const int D4 = (D + 3) & ~3;
-  float* zt = (float*)(xr + Mp * 4 + 3 * Mp * 4);   // M x D4  Z / l, centred (zero padded)
-  float* zn = zt + M * D4;             // M
+  const int D16 = (D + 15) & ~15;
+  const int ZS = kzz_zstride(D);
+  float* zt = (float*)(xr + Mp * 4 + 3 * Mp * 4);   // M x ZS  Z / l, centred (zero padded)
+  float* zn = zt + M * ZS;             // M
   float* cm = zn + M;                  // D
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float s2 = hyp[0];
   const float* ls = hyp + 1;
+#if GPK_KZZ_STAMPS
+  unsigned long long kst[12] = {0};
+#endif
+  KZ_STAMP(0);
 
-  for (int e = tid; e < M * D4; e += KT) {
-    const int m = e / D4, d = e - m * D4;
+  for (int e = tid; e < M * ZS; e += KT) {
+    const int m = e / ZS, d = e - m * ZS;
     zt[e] = d < D ? Z[m * D + d] / ls[d] : 0.f;
   }
   for (int e = tid; e < 6 * Mp * 4; e += KT) P[e] = 0.0;   // both parities of P / lb / xr
   lds_barrier();
-  for (int d = tid; d < D; d += KT) {
+  for (int d = wave; d < D; d += KT / 64) {   // column means: one wave per column
     float sm = 0.f;
-    for (int m = 0; m < M; ++m) sm += zt[m * D4 + d];
-    cm[d] = sm / (float)M;
+    for (int m = lane; m < M; m += 64) sm += zt[m * ZS + d];
+    sm = wave_sum(sm);
+    if (lane == 0) cm[d] = sm / (float)M;
   }
   lds_barrier();
-  for (int e = tid; e < M * D4; e += KT) {
-    const int d = e % D4;
+  for (int e = tid; e < M * ZS; e += KT) {
+    const int d = e % ZS;
     if (d < D) zt[e] -= cm[d];
   }
   lds_barrier();
   for (int m = tid; m < M; m += KT) {
     float sm = 0.f;
-    for (int d = 0; d < D; ++d) sm = __builtin_fmaf(zt[m * D4 + d], zt[m * D4 + d], sm);
+    for (int d = 0; d < D; ++d) sm = __builtin_fmaf(zt[m * ZS + d], zt[m * ZS + d], sm);
     zn[m] = sm;
   }
   lds_barrier();
@@ -192,6 +214,7 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
   }
   f64x4 acc[NS];
   int status = 0;
+  KZ_STAMP(1);
   for (int attempt = 0; attempt <= max_tries; ++attempt) {
     double ladder = 0.0;  // GPyTorch adds (jitter_new - jitter_prev) cumulatively
     {
@@ -203,26 +226,33 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
         p10 *= 10.0;
       }
     }
-    // K_ZZ tiles (fp32 arithmetic as the reference's kernel, + jitter, -> fp64 + ladder)
+    // K_ZZ tiles (fp32 arithmetic as the reference's kernel, + jitter, -> fp64 + ladder).
+    // The Gram runs on fp32 MFMA with the A rows fed in the order pi(x) = (x >> 2) + 4 (x & 3),
+    // so the fp32 accumulator (reg r <-> row 4g + r) lands in the fp64 tile layout (row g + 4r).
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
       asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
       const int j = 16 * jts[q] + c;
+      f32x4 gram = {0.f, 0.f, 0.f, 0.f};
+      if (its[q] < T16) {
+        const int ia = 16 * its[q] + (c >> 2) + 4 * (c & 3);
+        const float* za = zt + (ia < M ? ia : 0) * ZS + 4 * g;
+        const float* zb = zt + (j < M ? j : 0) * ZS + 4 * g;
+        for (int d0 = 0; d0 < D16; d0 += 16) {
+          const float4 av = *(const float4*)(za + d0);
+          const float4 bv = *(const float4*)(zb + d0);
+          gram = mfma32(av.x, bv.x, gram);
+          gram = mfma32(av.y, bv.y, gram);
+          gram = mfma32(av.z, bv.z, gram);
+          gram = mfma32(av.w, bv.w, gram);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 16 * its[q] + g + 4 * r;
         double v = (i == j) ? 1.0 : 0.0;
         if (its[q] < T16 && i < M && j < M) {
-          float dot = 0.f;
-          for (int d = 0; d < D4; d += 4) {
-            const float4 zi = *(const float4*)&zt[i * D4 + d];
-            const float4 zj = *(const float4*)&zt[j * D4 + d];
-            dot = __builtin_fmaf(zi.x, zj.x, dot);
-            dot = __builtin_fmaf(zi.y, zj.y, dot);
-            dot = __builtin_fmaf(zi.z, zj.z, dot);
-            dot = __builtin_fmaf(zi.w, zj.w, dot);
-          }
-          float dist = zn[i] + zn[j] - 2.f * dot;
+          float dist = zn[i] + zn[j] - 2.f * gram[r];
           dist = dist < 0.f ? 0.f : dist;
           float kv = s2 * __expf(-0.5f * dist);
           if (i == j) kv = kv + jitter_var;
@@ -233,8 +263,12 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
       }
     }
     int failed = 0;
+    KZ_STAMP(2);
     for (int s = 0; s < (Mp >> 2); ++s) {
       const int j0 = 4 * s, jt0 = s >> 2, sub = s & 3;
+#if GPK_KZZ_STAMPS
+      unsigned long long ta = __builtin_amdgcn_s_memtime();
+#endif
       // opaque tile coordinates: the compiler must not hoist every tile's derived LDS
       // addresses out of the step loop (they would cost more registers than the tiles)
 #pragma unroll
@@ -251,13 +285,25 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
         }
       }
       lds_barrier();
+      KZ_ACC(6, ta);
+#if GPK_KZZ_STAMPS
+      ta = __builtin_amdgcn_s_memtime();
+#endif
       double dd[4][4], l4[4][4], l4i[4][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int t = 0; t < 4; ++t) dd[r][t] = P[(j0 + r) * 4 + t];
       int bad = 0;
+#if GPK_KZZ_SKIP & 1
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) l4i[r][t] = (r == t) ? 0.5 : 0.0;
+      if (dd[0][0] == -12345.0) {
+#else
       if (!chol4(dd, l4, l4i, bad)) {   // uniform: every thread factors the same LDS block
+#endif
         failed = j0 + bad + 1;
         break;
       }
@@ -274,16 +320,25 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
           if (i < M && j0 + t < M && j0 + t <= i) L[(size_t)i * M + j0 + t] = v;
         }
       }
+      KZ_ACC(7, ta);
+#if GPK_KZZ_STAMPS
+      ta = __builtin_amdgcn_s_memtime();
+#endif
       lds_barrier();
+      KZ_ACC(8, ta);
+#if GPK_KZZ_STAMPS
+      ta = __builtin_amdgcn_s_memtime();
+#endif
       // rank-4 update of every tile with columns beyond the panel: one f64 MFMA each
 #pragma unroll
       for (int q = 0; q < NS; ++q) {
-        if (its[q] < T16 && 16 * jts[q] + 15 >= j0 + 4) {
+        if (its[q] < T16 && 16 * jts[q] + 15 >= j0 + 4 && !(GPK_KZZ_SKIP & 2)) {
           const double av = lb[(16 * its[q] + c) * 4 + g];
           const double bv = lb[(16 * jts[q] + c) * 4 + g];
           acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc[q], 0, 0, 0);
         }
       }
+      KZ_ACC(9, ta);
     }
     if (!failed) {
       status = attempt > 0 ? -attempt : 0;
@@ -292,9 +347,10 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
     status = failed;
     lds_barrier();
   }
+  KZ_STAMP(3);
   __threadfence_block();
   __syncthreads();   // L (global) complete and visible before the inverse phase reads it
-  if (status <= 0) {
+  if (status <= 0 && !(GPK_KZZ_SKIP & 4)) {
 #pragma unroll
     for (int q = 0; q < NS; ++q)
 #pragma unroll
@@ -373,7 +429,7 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
       // X[i] -= L[i][j0..j0+3] X_k for tiles below the pivot rows and left of j0+4
 #pragma unroll
       for (int q = 0; q < NS; ++q) {
-        if (its[q] < T16 && 16 * its[q] + 15 >= j0 + 4 && 16 * jts[q] <= j0 + 3) {
+        if (its[q] < T16 && 16 * its[q] + 15 >= j0 + 4 && 16 * jts[q] <= j0 + 3 && !(GPK_KZZ_SKIP & 8)) {
           const double av = P[(16 * its[q] + c) * 4 + g];
           const double bv = lb[g * Mp + 16 * jts[q] + c];
           acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc[q], 0, 0, 0);
@@ -383,11 +439,21 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
     }
     lds_barrier();
   }
-  for (int e = tid; e < M * M; e += KT) {
-    const int i = e / M, j = e - i * M;
-    if (j > i) { L[e] = 0.0; Linv[e] = 0.0; }
+  KZ_STAMP(4);
+  for (int i = wave; i < M; i += KT / 64) {   // strict upper triangles: one row per wave
+    for (int j = i + 1 + lane; j < M; j += 64) {
+      L[(size_t)i * M + j] = 0.0;
+      Linv[(size_t)i * M + j] = 0.0;
+    }
   }
   if (tid == 0) info[0] = status;
+#if GPK_KZZ_STAMPS
+  KZ_STAMP(5);
+  if (tid == 0) {
+    for (int k = 1; k < 6; ++k) Linv[k] = (double)(kst[k] - kst[k - 1]);
+    for (int k = 6; k < 10; ++k) Linv[k] = (double)kst[k];
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1955,7 +2021,7 @@ int launch_kzz(const GpkKzzArgs& a, size_t lds, hipStream_t stream) {
 int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
   const int Mp = (a.M + 15) & ~15;
   const size_t lds = (size_t)(6 * Mp * 4) * sizeof(double) +
-                     (size_t)(a.M * ((a.D + 3) & ~3) + a.M + a.D) * sizeof(float);
+                     (size_t)(a.M * kzz_zstride(a.D) + a.M + a.D) * sizeof(float);
   if (lds > 160 * 1024) return -4;
   const int T16 = Mp >> 4;
   const int ns = (T16 * (T16 + 1) / 2 + 7) / 8;   // tiles per wave
