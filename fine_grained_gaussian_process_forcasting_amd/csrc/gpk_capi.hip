@@ -173,7 +173,7 @@ int gpk_window_gather_f32(const float* table, long long n_rows, int F, const lon
 }
 
 // Diagnostic (not part of the product ABI): same as gpk_exact_mll_f32 for N in
-// (240, 256], plus per-workgroup phase clocks (32 x u64 per window) in `stamps`.
+// (240, 256], plus per-workgroup phase clocks and a per-step timeline (32 + 1024 x u64 per window) in `stamps`.
 int gpk_debug_exact_stamps(const float* X, const float* y, const float* hyp, int n_lengthscale,
                            int B, int N, int D, double jitter, int max_tries, float* L, float* z,
                            float* mll, int* info, unsigned long long* stamps, void* stream) {

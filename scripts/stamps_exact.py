@@ -13,7 +13,8 @@ LN2 = math.log(2)
 hyp = ops.pack_exact_hyper(LN2, LN2 + 1e-4, 0.0, LN2, dev)
 L = torch.empty(B, N, N, device=dev); mll = torch.empty(B, device=dev)
 info = torch.empty(B, dtype=torch.int32, device=dev)
-st = torch.zeros(B, 32, dtype=torch.int64, device=dev)
+STRIDE = 32 + 16 * 8 * 8
+st = torch.zeros(B, STRIDE, dtype=torch.int64, device=dev)
 lib = _native.lib()
 for it in range(5):
     rc = lib.gpk_debug_exact_stamps(X.data_ptr(), y.data_ptr(), hyp.data_ptr(), 1, B, N, D, 1e-6, 3,
@@ -21,7 +22,8 @@ for it in range(5):
                                     torch.cuda.current_stream().cuda_stream)
     assert rc == 0
 torch.cuda.synchronize()
-s = st.cpu().numpy().astype(np.float64)
+s_all = st.cpu().numpy()
+s = s_all[:, :32].astype(np.float64)
 names = ["prologue", "RBF rows 0-1"]
 tot = s[:, 8]
 print(f"B={B} total cycles: mean {tot.mean():.0f} min {tot.min():.0f} max {tot.max():.0f}")
@@ -48,3 +50,22 @@ for bb in range(B):
 same = sum(1 for v in groups.values() if len(v) == 2 and v[0] == v[1])
 print(f"CUs hosting 2 WGs: {sum(1 for v in groups.values() if len(v) == 2)}; diag waves on the same SIMD: {same}; groups={len(groups)}")
 print("sample hw_id:", [hex(int(x)) for x in hw[:8]])
+
+# per-step timeline (absolute s_memtime, made relative to each window's earliest event)
+tl = s_all[:, 32:].reshape(B, 16, 8, 8).astype(np.int64)
+valid = tl > 0
+base = np.where(valid, tl, np.iinfo(np.int64).max).reshape(B, -1).min(1)
+rel = np.where(valid, tl - base[:, None, None, None], -1).astype(np.float64)
+rel[~valid] = np.nan
+m = np.nanmean(rel, axis=0)  # (16 steps, 8 waves, 8 events)
+print("per-step timeline (cycles from the window's first timeline event, mean over windows)")
+print(" k | diag: fac0  fac1  LAin  LAdone | workers (mean over waves): start  trail  zRHS   rbf   wait  trsm  barr | max-wave barr")
+for k in range(16):
+    d = m[k, 7]
+    w = np.nanmean(m[k, :7], axis=0)
+    wb = np.nanmax(m[k, :7, 6])
+    print(f"{k:2d} | {d[0]:6.0f} {d[1]:6.0f} {d[2]:6.0f} {d[3]:6.0f} | " + " ".join(f"{v:6.0f}" for v in w[:7]) + f" | {wb:6.0f}")
+print("per-wave trailing+rbf+trsm busy cycles at k=1..3:")
+for k in (1, 2, 3, 8):
+    busy = (m[k, :7, 1] - m[k, :7, 0]) + (m[k, :7, 3] - m[k, :7, 2]) + (m[k, :7, 5] - m[k, :7, 4])
+    print(k, " ".join(f"{v:5.0f}" for v in busy), " wait:", " ".join(f"{v:5.0f}" for v in (m[k, :7, 4] - m[k, :7, 3])))
