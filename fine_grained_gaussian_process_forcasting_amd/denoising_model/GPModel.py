@@ -20,6 +20,7 @@ as GPyTorch accepts; targets follow (B, N) / (N,).
 from __future__ import annotations
 
 import warnings
+import weakref
 
 import torch
 import torch.nn as nn
@@ -40,6 +41,19 @@ def _as_batch(x: torch.Tensor) -> torch.Tensor:
     raise ValueError(f"inputs must be (N,), (N, D) or (B, N, D), got {tuple(x.shape)}")
 
 
+class _PredictionCacheHandle:
+    """Lets ops_autograd.invalidate_caches() drop a model's prediction cache (HIP graph
+    replays change parameters without bumping the version counters it is keyed on)."""
+
+    def __init__(self, model):
+        self._model = weakref.ref(model)
+
+    def clear(self):
+        m = self._model()
+        if m is not None:
+            m._prediction_cache = None
+
+
 def _version_key(*ts):
     return tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in ts)
 
@@ -53,6 +67,9 @@ class ExactGPModel(nn.Module):
         self.mean_module = ConstantMean()
         self.covar_module = ScaleKernel(RBFKernel())
         self._prediction_cache = None
+        self._cache_handle = _PredictionCacheHandle(self)
+        from ..ops_autograd import register_cache
+        register_cache(self._cache_handle)
 
     def set_train_data(self, inputs=None, targets=None, strict=True):
         if inputs is not None:

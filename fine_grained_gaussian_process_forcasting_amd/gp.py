@@ -168,6 +168,14 @@ class LinearMean(nn.Module):
 # ---------------------------------------------------------------------------
 # distributions (upstream distributions/multivariate_normal.py)
 # ---------------------------------------------------------------------------
+def warn_if_clamped(flag: torch.Tensor, min_var: float) -> None:
+    """GPyTorch's NumericalWarning when the variational kernel clamped a variance."""
+    if int(flag.item()) & 1:
+        warnings.warn(f"Negative variance values detected. This is likely due to numerical "
+                      f"instabilities. Rounding negative variances up to {min_var}.",
+                      NumericalWarning)
+
+
 class MultivariateNormal:
     """Diagonal-query MVN of the hot path.
 
@@ -212,10 +220,10 @@ class MultivariateNormal:
         if self._clamp_flag is not None and self._added_noise is None:
             # the kernel already clamped (fp32 min_variance); it tells us whether it did:
             # one host read of the flag, as GPyTorch's own .lt(min_var).any() sync
-            if int(self._clamp_flag.item()) & 1:
-                warnings.warn(f"Negative variance values detected. This is likely due to numerical "
-                              f"instabilities. Rounding negative variances up to {min_var}.",
-                              NumericalWarning)
+            # (recorded instead while a HIP graph is captured, ops.DeferredChecks)
+            from .ops import record_or_run
+            flag = self._clamp_flag
+            record_or_run("clamp", (flag, min_var), lambda: warn_if_clamped(flag, min_var))
             return var
         if bool((var < min_var).any()):
             warnings.warn(f"Negative variance values detected. This is likely due to numerical "

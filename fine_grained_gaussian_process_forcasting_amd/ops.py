@@ -32,7 +32,8 @@ def _stream_ptr(device: torch.device) -> int:
 def _scalar_tensor(v, device) -> torch.Tensor:
     if isinstance(v, torch.Tensor):
         return v.detach().reshape(-1).to(device=device, dtype=torch.float32)
-    return torch.tensor([float(v)], device=device, dtype=torch.float32)
+    # a fill kernel, not a host->device copy: graph-capture safe
+    return torch.full((1,), float(v), device=device, dtype=torch.float32)
 
 
 def pack_exact_hyper(outputscale, noise, mean_constant, lengthscale, device) -> torch.Tensor:
@@ -163,6 +164,43 @@ def exact_posterior(X: torch.Tensor, L: torch.Tensor, z: torch.Tensor, hyper: to
 INFO_TIMEOUT = 1 << 20   # gpk_exact.hip kInfoTimeout: a bounded LDS spin-wait expired
 
 
+class DeferredChecks:
+    """Host-side verdicts recorded while a HIP graph is being captured.
+
+    A captured step cannot read device memory on the host (the capture would break),
+    so psd_safe_cholesky's info check and the variance-clamp flag are RECORDED instead:
+    the recorded tensors live in the graph's memory pool and are rewritten by every
+    replay, so ``check()`` after a replay raises / warns exactly as the eager call
+    would have for that replay's data (graphs.GraphedStep calls it).
+    """
+
+    def __init__(self):
+        self.items = []
+
+    def check(self) -> None:
+        for kind, args in self.items:
+            if kind == "cholesky":
+                info, jitter, what, max_tries = args
+                check_cholesky_info(info, jitter, (), what, max_tries)
+            else:
+                from .gp import warn_if_clamped
+                warn_if_clamped(*args)
+
+
+_RECORDERS: list = []
+
+
+def record_or_run(kind: str, args: tuple, run) -> None:
+    """Run a host-side check now, or record it when the current stream is capturing."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        if not _RECORDERS:
+            raise RuntimeError("gpk: a HIP graph capture reached a host-side numerical check; "
+                               "capture through graphs.GraphedStep, which defers the checks")
+        _RECORDERS[-1].items.append((kind, args))
+        return
+    run()
+
+
 def check_cholesky_info(info: torch.Tensor, jitter: float, inputs=(), what: str = "cholesky",
                         max_tries: int = 3) -> None:
     """GPyTorch's psd_safe_cholesky bookkeeping, from the per-window info codes.
@@ -171,7 +209,11 @@ def check_cholesky_info(info: torch.Tensor, jitter: float, inputs=(), what: str 
     same NumericalWarning text per ladder step and raises NanError / NotPSDError.
     When any window is still not PD, psd_safe_cholesky has walked the whole ladder
     (``max_tries`` warnings) before raising, whatever the other windows needed.
+    Under HIP graph capture the check is recorded (DeferredChecks) instead.
     """
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        record_or_run("cholesky", (info, jitter, what, max_tries), None)
+        return
     info_h = info.detach().to("cpu")
     if not bool((info_h != 0).any()):
         return

@@ -12,6 +12,7 @@ calls that used it. Nothing here runs on the CPU.
 from __future__ import annotations
 
 import math
+import weakref
 from typing import Optional
 
 import torch
@@ -20,6 +21,20 @@ from . import library  # noqa: F401  (registers the gpk:: ops)
 from . import ops
 
 LOG_2PI = math.log(2.0 * math.pi)
+
+# Every factor / prediction cache of the package (objects with .clear()). Their keys
+# are tensor version counters, which a HIP graph replay does not bump, so
+# graphs.GraphedStep clears them all after each replay.
+_CACHES: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def register_cache(obj) -> None:
+    _CACHES.add(obj)
+
+
+def invalidate_caches() -> None:
+    for c in list(_CACHES):
+        c.clear()
 
 
 def exact_log_prob(X, y, lengthscale, outputscale, constant, noise) -> torch.Tensor:
@@ -49,6 +64,7 @@ class KzzCache:
 
     def __init__(self):
         self._entry = None
+        register_cache(self)
 
     def clear(self):
         self._entry = None

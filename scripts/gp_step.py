@@ -14,6 +14,8 @@ path. Batches come from the GPU-resident window sampler (data.batch_sampled_data
 synthetic traffic-like frame): no per-step host->device copy.
 
 GP share = t(step with gp=True) - t(step with the GP blur off, same backbone work).
+Both eager (the reference's loop) and HIP-graph-captured (graphs.GraphedStep: one graph
+launch per step) timings are reported.
 
     python scripts/gp_step.py [cfg3|cfg1] [steps]
 """
@@ -34,6 +36,7 @@ from fine_grained_gaussian_process_forcasting_amd import settings  # noqa: E402
 from fine_grained_gaussian_process_forcasting_amd.data import batch_sampled_data  # noqa: E402
 from fine_grained_gaussian_process_forcasting_amd.denoising_model.denoise_model_2 import denoise_model_2  # noqa: E402
 from fine_grained_gaussian_process_forcasting_amd.mlls import DeepApproximateMLL, VariationalELBO  # noqa: E402
+from fine_grained_gaussian_process_forcasting_amd.graphs import GraphedStep  # noqa: E402
 
 
 class Backbone(nn.Module):
@@ -100,31 +103,40 @@ def run(cfg, steps):
     train, _, _ = batch_sampled_data(frame, 0.8, (b * (steps + 4), b), T, n_enc, pred_len, coldef, b, device=dev)
     batches = list(train)
     res = {}
-    for gp in (True, False):
-        model = Model(nin, d, pred_len, gp).to(dev)
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.98), eps=1e-9)
+    for mode in ("eager", "graph"):
+        r = {}
+        for gp in (True, False):
+            model = Model(nin, d, pred_len, gp).to(dev)
+            # capturable=True in both modes, so the two time the same Adam arithmetic
+            opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.98), eps=1e-9,
+                                   capturable=True)
+            with settings.num_likelihood_samples(1):
+                if mode == "eager":
+                    def step(k):
+                        enc, dec, y = batches[k % len(batches)]
+                        loss = model(enc, dec, y)
+                        opt.zero_grad()
+                        loss.backward()
+                        opt.step()
+                        return loss
+                    for k in range(3):
+                        step(k)
+                else:
+                    gstep = GraphedStep(lambda enc, dec, y: model(enc, dec, y), opt, batches[0])
 
-        def step(k):
-            enc, dec, y = batches[k % len(batches)]
-            loss = model(enc, dec, y)
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-            return loss
-
-        with settings.num_likelihood_samples(1):
-            for k in range(3):
-                step(k)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for k in range(steps):
-                loss = step(k + 3)
-            torch.cuda.synchronize()
-            dt = (time.perf_counter() - t0) / steps
-        res["gp" if gp else "no_gp"] = {"ms_per_step": dt * 1e3, "windows_per_s": b / dt,
-                                        "loss": float(loss)}
-    res["gp_share_ms"] = res["gp"]["ms_per_step"] - res["no_gp"]["ms_per_step"]
-    res["gp_share_frac"] = res["gp_share_ms"] / res["gp"]["ms_per_step"]
+                    def step(k):
+                        return gstep(*batches[k % len(batches)])
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for k in range(steps):
+                    loss = step(k + 3)
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t0) / steps
+            r["gp" if gp else "no_gp"] = {"ms_per_step": dt * 1e3, "windows_per_s": b / dt,
+                                          "loss": float(loss)}
+        r["gp_share_ms"] = r["gp"]["ms_per_step"] - r["no_gp"]["ms_per_step"]
+        r["gp_share_frac"] = r["gp_share_ms"] / r["gp"]["ms_per_step"]
+        res[mode] = r
     res["config"] = {"cfg": cfg, "b": b, "enc": n_enc, "dec": pred_len, "d_model": d, "M": 256,
                      "backbone": "torch.nn.Transformer stand-in (d 32, 8 heads, d_ff 128, 1 layer)",
                      "anomaly_mode": False, "input": "GPU-resident window sampler"}
