@@ -37,7 +37,12 @@ class denoise_model_2(nn.Module):
     def add_gp_noise(self, x):
         b, s, _ = x.shape
         eps_gp, dist = self.deep_gp.predict(x)
-        eps_gp = self.proj_up(eps_gp.permute(1, 2, 0))
+        # proj_up(e) for in_features == 1 is e * W[:, 0] + bias: computed as a broadcast
+        # multiply-add (a GEMM with K = 1 whose weight gradient is a K = b*s reduction
+        # ran 0.17 ms per call in hipBLASLt at b = 256, s = 192; this is one fused
+        # elementwise kernel and a plain reduction in the backward)
+        e = eps_gp.permute(1, 2, 0)
+        eps_gp = torch.addcmul(self.proj_up.bias, e, self.proj_up.weight.reshape(-1))
         x_noisy = x + eps_gp
         return x_noisy, dist
 
