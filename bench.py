@@ -17,6 +17,8 @@ Side legs in the same JSON line (not the headline):
   backward     the exact path's analytic adjoint on the headline windows;
   posterior    the exact path's eval-mode posterior (mean + variance at N new points per
                window) from the headline windows' factor;
+  e2e_step     the cfg-3 forecast -> GP blur -> denoise train step, eager and HIP-graph
+               captured (scripts/gp_step.py, graphs.GraphedStep);
   cpu_baseline the reference's CPU arithmetic (GPyTorch's torch-CPU calls restated in
                oracle/) on the GPU box's host cores, all threads and 1 thread, plus the
                variational path; and the MLL relative error of the GPU kernel vs the
@@ -243,6 +245,22 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
     }
 
 
+def e2e_leg(steps=10):
+    """the cfg-3 forecast -> GP blur -> denoise train step (b=256, enc 192 /
+    dec 96, d 32, M 256), eager (the reference's loop) and HIP-graph captured
+    (graphs.GraphedStep), with and without the GP branch (scripts/gp_step.py)."""
+    import importlib.util
+    try:
+        spec = importlib.util.spec_from_file_location("gp_step", os.path.join(ROOT, "scripts", "gp_step.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        res = mod.run("cfg3", steps)
+        res["note"] = "windows/s = b / step time; GP share = step(gp) - step(no gp); not the headline"
+        return res
+    except Exception as e:  # a side leg never takes the headline line down
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -259,6 +277,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grad", action="store_true", help="skip the backward side measurement")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end train-step side leg")
     args = ap.parse_args()
 
     rank, local, world = env_rank_world()
@@ -388,6 +407,8 @@ def main():
                                  "note": "eval-mode exact posterior mean + variance; not the headline"}
         if var is not None:
             line["variational"] = var
+        if world == 1 and not args.no_e2e:
+            line["e2e_step"] = e2e_leg()
         if world == 1 and not args.no_cpu_baseline:
             # the box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool); os.cpu_count()
             # reports the whole machine
