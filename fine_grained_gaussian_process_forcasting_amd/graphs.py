@@ -10,9 +10,14 @@ host-side numerical verdicts (psd_safe_cholesky info codes, the variance-clamp f
 are recorded during capture (ops.DeferredChecks) and evaluated after each replay, so a
 replay warns / raises exactly as the eager step would for the same data.
 
-    step = GraphedStep(lambda enc, dec, y: model(enc, dec, y), optimizer, (enc0, dec0, y0))
+    step = GraphedStep(model, optimizer, (enc0, dec0, y0), loss_index=1)
     for enc, dec, y in batches:
-        loss = step(enc, dec, y)          # copies into the static inputs, replays
+        out, loss, mse = step(enc, dec, y)   # copies into the static inputs, replays
+
+``loss_fn`` returns the loss tensor, or a tuple whose ``loss_index``-th entry is the loss
+(``Forecast_denoising.forward`` returns ``(final_outputs, loss, mse_loss)``,
+forecast_denoising.py:105); the call returns the same structure, as graph-owned tensors
+rewritten by every replay.
 
 Requirements (checked): CUDA/ROCm tensors, an optimizer built with
 ``capturable=True`` (Adam/AdamW keep their step counters on the device), input shapes
@@ -32,8 +37,9 @@ from .ops_autograd import invalidate_caches
 
 
 class GraphedStep:
-    def __init__(self, loss_fn: Callable[..., torch.Tensor], optimizer: torch.optim.Optimizer,
-                 sample_inputs: Sequence[torch.Tensor], warmup: int = 3, check_every: int = 1):
+    def __init__(self, loss_fn: Callable[..., object], optimizer: torch.optim.Optimizer,
+                 sample_inputs: Sequence[torch.Tensor], warmup: int = 3, check_every: int = 1,
+                 loss_index: int = 0):
         if not torch.cuda.is_available():
             raise RuntimeError("GraphedStep needs a ROCm device (HIP graphs); there is no CPU path")
         for t in sample_inputs:
@@ -48,6 +54,7 @@ class GraphedStep:
         self.loss_fn = loss_fn
         self.optimizer = optimizer
         self.check_every = check_every
+        self.loss_index = loss_index
         self.static_inputs = [t.detach().clone() for t in sample_inputs]
         self._n = 0
 
@@ -66,21 +73,22 @@ class GraphedStep:
             # captured on the warm-up stream: the parameters' gradient-accumulation
             # nodes keep the stream they were created on
             with torch.cuda.graph(self.graph, stream=side):
-                self.static_loss = self.loss_fn(*self.static_inputs)
-                self.static_loss.backward()
+                self.static_outputs = self.loss_fn(*self.static_inputs)
+                self._loss(self.static_outputs).backward()
                 self.optimizer.step()
         finally:
             ops._RECORDERS.remove(self.checks)
         invalidate_caches()
 
-    def _eager_step(self) -> torch.Tensor:
-        self.optimizer.zero_grad(set_to_none=True)
-        loss = self.loss_fn(*self.static_inputs)
-        loss.backward()
-        self.optimizer.step()
-        return loss
+    def _loss(self, outputs) -> torch.Tensor:
+        return outputs[self.loss_index] if isinstance(outputs, (tuple, list)) else outputs
 
-    def __call__(self, *inputs: torch.Tensor) -> torch.Tensor:
+    def _eager_step(self) -> None:
+        self.optimizer.zero_grad(set_to_none=True)
+        self._loss(self.loss_fn(*self.static_inputs)).backward()
+        self.optimizer.step()
+
+    def __call__(self, *inputs: torch.Tensor):
         if len(inputs) != len(self.static_inputs):
             raise ValueError(f"expected {len(self.static_inputs)} inputs, got {len(inputs)}")
         for dst, src in zip(self.static_inputs, inputs):
@@ -93,4 +101,4 @@ class GraphedStep:
         self._n += 1
         if self._n % self.check_every == 0:
             self.checks.check()
-        return self.static_loss
+        return self.static_outputs

@@ -77,10 +77,16 @@ def test_graphed_train_step_matches_eager(cuda_device):
 
         for _ in range(3):                       # GraphedStep's warm-up steps
             eager(batches[0])
-        step = GraphedStep(lambda e, dd, y: mb(e, dd, y), ob, batches[0], warmup=3)
+        def fb(e, dd, y):              # (aux, loss) like Forecast_denoising's tuple return
+            loss = mb(e, dd, y)
+            return 2.0 * loss.detach(), loss
+
+        step = GraphedStep(fb, ob, batches[0], warmup=3, loss_index=1)
         for k in range(1, 6):
             la = eager(batches[k])
-            lb = float(step(*batches[k]).detach())
+            aux, lossb = step(*batches[k])
+            lb = float(lossb.detach())
+            assert float(aux) == 2.0 * lb
             assert math.isfinite(lb)
             assert abs(la - lb) <= 1e-5 * max(1.0, abs(la)), (k, la, lb)
         for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
