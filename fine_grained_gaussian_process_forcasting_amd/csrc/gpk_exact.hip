@@ -311,6 +311,15 @@ GPK_DEVICE f32x4 load_w(const float* wb, int c, int grp) {
   for (int r = 0; r < 4; ++r) q[r] = wb[(4 * grp + r) * 16 + c];
   return q;
 }
+// The same through volatile LDS reads (ordered after a flag read, see worker_step).
+GPK_DEVICE f32x4 load_w_v(const float* wb, int c, int grp) {
+  typedef __attribute__((address_space(3))) volatile float lds_vfloat;
+  const lds_vfloat* w = (const lds_vfloat*)wb;
+  f32x4 q;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) q[r] = w[(4 * grp + r) * 16 + c];
+  return q;
+}
 
 // d += R^T R for a rounded factor tile held as registers (hi, lo).
 GPK_DEVICE f32x4 mma_tn_split_regs(const half4_t h, const half4_t l, f32x4 d) {
@@ -344,17 +353,6 @@ GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) {   // d += V^T V of the round
   (void)round_split_f16(v, h, l);
   return mma_tn_split_regs(h, l, d);
 }
-// d += Q^T P with both operands already in registers (q, p as pan_load returns them)
-// (Qh Ph + Ql Pl on one K=32 MFMA, then Qh Pl and Ql Ph on two K=16 MFMAs that take
-// the halves of the same registers: no swapped copy of P, the same cycles)
-GPK_DEVICE f32x4 pan_mma_regs(const pan_op_t q, const pan_op_t p, f32x4 d) {
-  const half4_t qh = {q[0], q[1], q[2], q[3]}, ql = {q[4], q[5], q[6], q[7]};
-  const half4_t ph = {p[0], p[1], p[2], p[3]}, pl = {p[4], p[5], p[6], p[7]};
-  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q, p, d, 0, 0, 0);
-  d = __builtin_amdgcn_mfma_f32_16x16x16f16(qh, pl, d, 0, 0, 0);
-  d = __builtin_amdgcn_mfma_f32_16x16x16f16(ql, ph, d, 0, 0, 0);
-  return d;
-}
 #else
 typedef f32x4 pan_op_t;
 GPK_DEVICE pan_op_t pan_load(const float* tile, int lane) { return *(const f32x4*)&tile[4 * lane]; }
@@ -366,7 +364,6 @@ GPK_DEVICE f32x4 pan_store(float* tile, int lane, const f32x4 v) {
   return v;
 }
 GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) { return mma_tn(v, v, d); }
-GPK_DEVICE f32x4 pan_mma_regs(const pan_op_t q, const pan_op_t p, f32x4 d) { return mma_tn(q, p, d); }
 #endif
 
 // Factor one 16x16 diagonal tile T in ONE wave (the diagonal wave).
@@ -707,16 +704,28 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   GPK_WSTAMP(6, 2)  // right-hand side
   // TRSM of the row-K off-diagonal tiles (P(K) < t <= P(K) + NB - K - 1) and,
   // by the owner of RHS block row K, of the right-hand side: z_K
-  spin_until(x.vflag, kFlagFact, e0 + K);
+  // One LDS round trip in the usual case (the diagonal wave is ahead): the epoch flag, the
+  // failure word, R_KK^{-T} and 1/sigma are requested together. A wave's LDS reads are
+  // served in order, and the diagonal wave completes its R_KK^{-T} and failure-word writes
+  // before it releases the flag, so reads issued after a flag read that sees epoch K see
+  // them too (all volatile: the compiler keeps the order). Otherwise: wait, re-read.
+  const float* wbk = x.wbuf + (K & 1) * 256;
+  const int flag_now = x.vflag[kFlagFact];
+  int fail = x.vflag[kFlagFail + e0 / 32];
+  f32x4 q = load_w_v(wbk, c, grp);
+  // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
+  const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
+  if (flag_now < e0 + K) {
+    spin_until(x.vflag, kFlagFact, e0 + K);
+    fail = x.vflag[kFlagFail + e0 / 32];
+    q = load_w_v(wbk, c, grp);
+  }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
-  if (x.vflag[kFlagFail + e0 / 32] != 0) return 1;
+  if (fail != 0) return 1;
   constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
   constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
   constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
   {
-    const f32x4 q = load_w(x.wbuf + (K & 1) * 256, c, grp);
-    // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
-    const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
     if constexpr (THI >= TLO) {
       static_for_range<SLO, SHI>([&](auto I) {
         constexpr int s = decltype(I)::value;
