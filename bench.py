@@ -334,6 +334,26 @@ def main():
         elapsed, kern_ms = (float(v) for v in t.tolist())
     mean_mll = float(totals[-1].item()) / B_total
 
+    # BASELINE configs[1] (B=128, N=128, D=32): a side leg, same kernel, its own roofline
+    cfg2 = None
+    if rank == 0:
+        X2, y2 = make_inputs(128, 128, D, dev, seed=11)
+        for _ in range(3):
+            ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper)
+        t2 = EventTimer(20)
+        for _ in range(20):
+            with t2:
+                o2 = ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper)
+        torch.cuda.synchronize()
+        ms2 = t2.mean_ms()
+        b2, f2 = bytes_per_window(128, D), flops_per_window(128, D)
+        cfg2 = {"workload": "exact-GP windows B=128 N=128 D=32 (BASELINE configs[1]), L written",
+                "kernel_ms": ms2, "windows_per_s": 128 / (ms2 * 1e-3),
+                "hbm_frac": b2 * 128 / (ms2 * 1e-3) / HBM_PEAK,
+                "fp32_frac": f2 * 128 / (ms2 * 1e-3) / FP32_PEAK,
+                "note": "128 windows occupy half of the 256 CUs: latency-bound by one window's chain"}
+        assert bool((o2.info == 0).all())
+
     grad_ms = post_ms = None
     if not args.no_grad:
         fw = ops.exact_mll(X, y, None, None, None, None, hyper=hyper, want_L=True, want_z=True)
@@ -405,6 +425,8 @@ def main():
                                  "hbm_frac": pb * B / (post_ms * 1e-3) / HBM_PEAK,
                                  "fp32_frac": pf * B / (post_ms * 1e-3) / FP32_PEAK,
                                  "note": "eval-mode exact posterior mean + variance; not the headline"}
+        if cfg2 is not None:
+            line["cfg2"] = cfg2
         if var is not None:
             line["variational"] = var
         if world == 1 and not args.no_e2e:

@@ -192,3 +192,16 @@ def test_exact_accuracy_vs_fp32_lapack(cuda_device, N, D, ls, s2, noise, scale, 
         assert e <= max(4.0 * e32, 2e-6), (e, e32)
     em = np.max(np.abs(out.mll.cpu().double().numpy() - ref.mll) / np.abs(ref.mll))
     assert em <= 1e-4
+
+
+def test_exact_cfg2_full_batch(cuda_device):
+    """BASELINE config 2 shape (B=128, N=128, D=32, GPyTorch init hyper-parameters):
+    every window's factor and MLL vs the fp64 oracle (1e-4), info all zero."""
+    B, N, D = 128, 128, 32
+    X, y = _inputs(B, N, D, seed=2)
+    out = _run(cuda_device, X, y, LN2, LN2, 0.0, NOISE0)
+    ref = O.exact_mll(X.double().numpy(), y.double().numpy(), LN2, LN2, 0.0, NOISE0)
+    assert (out.info.cpu().numpy() == 0).all()
+    assert _rel_fro(out.L.cpu().double().numpy(), ref.L).max() <= 1e-4
+    mll = out.mll.cpu().double().numpy()
+    assert np.max(np.abs(mll - ref.mll) / np.abs(ref.mll)) <= 1e-4
