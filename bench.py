@@ -278,6 +278,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grad", action="store_true", help="skip the backward side measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end train-step side leg")
+    ap.add_argument("--no-cfg2", action="store_true", help="skip the B=128 N=128 side leg")
     args = ap.parse_args()
 
     rank, local, world = env_rank_world()
@@ -336,7 +337,7 @@ def main():
 
     # BASELINE configs[1] (B=128, N=128, D=32): a side leg, same kernel, its own roofline
     cfg2 = None
-    if rank == 0:
+    if rank == 0 and not args.no_cfg2:
         X2, y2 = make_inputs(128, 128, D, dev, seed=11)
         for _ in range(3):
             ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper)
