@@ -64,7 +64,7 @@ def main():
         json.dump(rows, fo, indent=1)
     summary = {}
     for k, v in rows.items():
-        if k.startswith("gpk_exact_kernel"):
+        if k.startswith("gpk_exact_kernel<16, 8, false, true>"):   # N=256 (not the cfg-2 leg)
             summary["exact_B512_N256_D32"] = {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
                                               "source": "profiles/r02_pmc.json " + k}
         if k.startswith("gpk_var_fwd_r_kernel<32>") or k.startswith("gpk_var_fwd_kernel<4>"):
