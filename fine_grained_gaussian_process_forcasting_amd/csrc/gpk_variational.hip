@@ -72,8 +72,7 @@ GPK_DEVICE float row16_sum_f(float v) {
 //            writes the final L entries;
 //   update   every tile right of the panel takes A -= l_rows l_cols^T: ONE f64 MFMA
 //            (rank 4 = the instruction's k) with both operands read from LDS.
-// Then the same tiles, reset to I, run the forward elimination of [L | I] 4 rows per
-// step (X -= L[:, panel] X_panel, again one MFMA per tile) -> L^{-1}.
+// L^{-1} is then formed by gpk_kzz_inv_kernel, one workgroup per 16-column block column.
 // ---------------------------------------------------------------------------
 constexpr int KT = 512;   // 8 waves
 // Z row stride (floats): D rounded up to the 16 dims one MFMA k-group reads, + 4, so a
@@ -348,103 +347,10 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
     lds_barrier();
   }
   KZ_STAMP(3);
-  __threadfence_block();
-  __syncthreads();   // L (global) complete and visible before the inverse phase reads it
-  if (status <= 0 && !(GPK_KZZ_SKIP & 4)) {
-#pragma unroll
-    for (int q = 0; q < NS; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        acc[q][r] = (its[q] == jts[q] && g + 4 * r == c) ? 1.0 : 0.0;
-    // L[i][j0..j0+3] (rows i >= j0; identity beyond M) of step s: loaded during step s-1
-    auto load_panel = [&](int j0n, double (&v)[4]) {
-      const int i = j0n + tid;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int cl = j0n + t;
-        double x = (i == cl) ? 1.0 : 0.0;
-        if (i < M && cl < M && cl <= i) x = L[(size_t)i * M + cl];
-        v[t] = x;
-      }
-    };
-    double pn[4];
-    if (tid < Mp) load_panel(0, pn);
-    double* const P0 = P;
-    double* const lb0 = lb;
-    double* const xr0 = xr;
-    for (int s = 0; s < (Mp >> 2); ++s) {
-      const int j0 = 4 * s, it0 = s >> 2, sub = s & 3;
-      const int par = s & 1;
-      double* P = P0 + par * (3 * Mp * 4);
-      double* lb = lb0 + par * (3 * Mp * 4);
-      double* xr = xr0 + par * (3 * Mp * 4);
-#pragma unroll
-      for (int q = 0; q < NS; ++q) asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
-      if (j0 + tid < Mp) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) P[(j0 + tid) * 4 + t] = pn[t];
-      }
-      if (j0 + 4 + tid < Mp) load_panel(j0 + 4, pn);
-      // publish X rows j0..j0+3 (tile row it0, register r = sub holds rows 4 sub + g)
-#pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        if (its[q] == it0) xr[g * Mp + 16 * jts[q] + c] = acc[q][sub];
-      }
-      lds_barrier();
-      // X_k = L4^{-1} X rows, one column per thread; final rows -> Linv
-      {
-        double l4[4][4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int t = 0; t < 4; ++t) l4[r][t] = P[(j0 + r) * 4 + t];
-        double rd[4], l4i[4][4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) rd[r] = rcp64(l4[r][r]);
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (r < cc) { l4i[r][cc] = 0.0; continue; }
-            double v = (r == cc) ? 1.0 : 0.0;
-#pragma unroll
-            for (int q = cc; q < r; ++q) v -= l4[r][q] * l4i[q][cc];
-            l4i[r][cc] = v * rd[r];
-          }
-        for (int col = tid; col < Mp; col += KT) {
-          double x[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) x[r] = xr[r * Mp + col];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            double v = 0.0;
-#pragma unroll
-            for (int q = 0; q <= r; ++q) v = __builtin_fma(l4i[r][q], x[q], v);
-            lb[r * Mp + col] = v;
-            if (j0 + r < M && col < M && col <= j0 + r) Linv[(size_t)(j0 + r) * M + col] = v;
-          }
-        }
-      }
-      lds_barrier();
-      // X[i] -= L[i][j0..j0+3] X_k for tiles below the pivot rows and left of j0+4
-#pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        if (its[q] < T16 && 16 * its[q] + 15 >= j0 + 4 && 16 * jts[q] <= j0 + 3 && !(GPK_KZZ_SKIP & 8)) {
-          const double av = P[(16 * its[q] + c) * 4 + g];
-          const double bv = lb[g * Mp + 16 * jts[q] + c];
-          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc[q], 0, 0, 0);
-        }
-      }
-      // (no end-of-step barrier: step s+1 writes the other parity's P / xr / lb)
-    }
-    lds_barrier();
-  }
+  // L^{-1} is formed by gpk_kzz_inv_kernel (one workgroup per block column), next launch
   KZ_STAMP(4);
-  for (int i = wave; i < M; i += KT / 64) {   // strict upper triangles: one row per wave
-    for (int j = i + 1 + lane; j < M; j += 64) {
-      L[(size_t)i * M + j] = 0.0;
-      Linv[(size_t)i * M + j] = 0.0;
-    }
+  for (int i = wave; i < M; i += KT / 64) {   // strict upper triangle of L: one row per wave
+    for (int j = i + 1 + lane; j < M; j += 64) L[(size_t)i * M + j] = 0.0;
   }
   if (tid == 0) info[0] = status;
 #if GPK_KZZ_STAMPS
@@ -454,6 +360,118 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
     for (int k = 6; k < 10; ++k) Linv[k] = (double)kst[k];
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// L^{-1} of the K_ZZ factor: one workgroup per 16-column block column jb (grid T16), so
+// the block columns run concurrently on different CUs (the serial [L | I] elimination
+// inside the one-workgroup factor kernel took as long as the factorisation). Block
+// forward substitution, right-looking, on fp64 MFMA:
+//   T_u = L_uu^{-1} (the diagonal blocks the column needs, formed in the workgroup),
+//   X_jb = T_jb;  for k = jb ..: S_u += -L_uk X_k (u > k), X_{k+1} = T_{k+1} S_{k+1}.
+// k-order of every MFMA: q = g + 4 kk, so a tile held in acc layout (reg r <-> row g + 4r)
+// is the B operand of k-step kk straight from register kk. S tiles dealt over the 4 waves
+// (u = wave mod 4); the L tiles of the next step are prefetched from L2 during this one.
+// ---------------------------------------------------------------------------
+constexpr int KIT = 256;
+__global__ void __launch_bounds__(KIT)
+gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ info,
+                   double* __restrict__ Linv) {
+  extern __shared__ __attribute__((aligned(16))) double dsm[];
+  const int Mp = (M + 15) & ~15, T16 = Mp >> 4;
+  const int jb = blockIdx.x;
+  const int nb = T16 - jb;            // block rows jb .. T16-1 of this block column
+  double* Tv = dsm;                   // nb x 256: T_{jb+u}, row-major [row][col]
+  double* Xs = Tv + nb * 256;         // nb x 256: X_{jb+u}, row-major
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (info[0] > 0) return;           // no factor (the op raises NotPSDError)
+  auto Lat = [&](int i, int j) -> double {   // L with identity padding beyond M
+    if (i < M && j < M) return L[(size_t)i * M + j];
+    return i == j ? 1.0 : 0.0;
+  };
+  for (int e = tid; e < 16 * jb * 16; e += KIT) {   // block rows above the diagonal: zero
+    const int i = e >> 4, j = 16 * jb + (e & 15);
+    if (i < M && j < M) Linv[(size_t)i * M + j] = 0.0;
+  }
+  // diagonal-block inverses: lane group g of wave w takes block u = 4 w + g (+ 16 ...),
+  // lane c its column c by forward substitution
+  for (int u = 4 * wave + g; u < nb; u += 16) {
+    const int b0 = 16 * (jb + u);
+    double lr[16][16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int q = 0; q <= r; ++q) lr[r][q] = Lat(b0 + r, b0 + q);
+    double x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      double v = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int q = 0; q < r; ++q) v = __builtin_fma(-lr[r][q], x[q], v);
+      x[r] = (r >= c) ? v * rcp64(lr[r][r]) : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Tv[u * 256 + r * 16 + c] = x[r];
+  }
+  lds_barrier();
+  for (int e = tid; e < 256; e += KIT) {      // X_jb = T_jb
+    Xs[e] = Tv[e];
+    const int i = 16 * jb + (e >> 4), j = 16 * jb + (e & 15);
+    if (i < M && j < M) Linv[(size_t)i * M + j] = Tv[e];
+  }
+  lds_barrier();
+  f64x4 S[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) S[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // A operands of step k: -L_{jb+u, jb+k}[c][g + 4kk] for the wave's tiles u = wave + 4t
+  double an[4][4];
+  auto load_a = [&](int k, double (&dst)[4][4]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int u = wave + 4 * t;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        dst[t][kk] = (u > k && u < nb) ? -Lat(16 * (jb + u) + c, 16 * (jb + k) + g + 4 * kk) : 0.0;
+    }
+  };
+  load_a(0, an);
+  for (int k = 0; k + 1 < nb; ++k) {
+    double a[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) a[t][kk] = an[t][kk];
+    if (k + 2 < nb) load_a(k + 1, an);
+    double xb[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) xb[kk] = Xs[k * 256 + (g + 4 * kk) * 16 + c];
+    const int tn = (k + 1) >> 2;          // slot of S_{k+1} in its owner wave
+    const bool own = wave == ((k + 1) & 3);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int u = wave + 4 * t;
+      if (u > k && u < nb) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) S[t] = mfma64(a[t][kk], xb[kk], S[t]);
+      }
+    }
+    if (own) {                            // X_{k+1} = T_{k+1} S_{k+1}
+      f64x4 sv = S[0];
+#pragma unroll
+      for (int t = 1; t < 4; ++t) sv = (t == tn) ? S[t] : sv;
+      f64x4 xv = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) xv = mfma64(Tv[(k + 1) * 256 + c * 16 + g + 4 * kk], sv[kk], xv);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Xs[(k + 1) * 256 + (g + 4 * r) * 16 + c] = xv[r];
+        const int i = 16 * (jb + k + 1) + g + 4 * r, j = 16 * jb + c;
+        if (i < M && j < M) Linv[(size_t)i * M + j] = xv[r];
+      }
+    }
+    lds_barrier();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2014,7 +2032,14 @@ int launch_kzz(const GpkKzzArgs& a, size_t lds, hipStream_t stream) {
   set_lds_once<gpk_kzz_kernel<NS>>();
   hipLaunchKernelGGL((gpk_kzz_kernel<NS>), dim3(1), dim3(KT), lds, stream, a.Z, a.hyp, a.M, a.D,
                      a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.Linv, a.info);
-  const hipError_t e = hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  if (GPK_KZZ_STAMPS) return 0;   // (the stamps build reports its clocks through Linv)
+  const int T16 = (a.M + 15) >> 4;
+  set_lds_once<gpk_kzz_inv_kernel>();
+  hipLaunchKernelGGL(gpk_kzz_inv_kernel, dim3(T16), dim3(KIT), (size_t)2 * T16 * 256 * sizeof(double),
+                     stream, a.L, a.M, a.info, a.Linv);
+  e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
 
