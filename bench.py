@@ -4,7 +4,9 @@ Headline workload (BASELINE.json configs[3], the north-star shape, which fits on
 synthetic exact-GP windows, N=256, D=32 -- per step the fused kernel builds the RBF Gram,
 runs the jittered Cholesky, the forward solve and the MLL for every window and writes L
 (B,N,N) and the MLL. Weak scaling (default): every rank owns B=512 windows. Strong
-scaling (--strong): B=512 windows in total, sharded with shard_range. The per-step MLL
+scaling (--strong): B=512 windows in total, sharded with shard_range. The K timed steps
+are bracketed by one pair of HIP events on the launch stream (roofline.kernel_ms = their
+elapsed time / K, which agrees with the rocprofv3 kernel average). The per-step MLL
 partial sums stay on the device and are SUM-all-reduced across ranks once (RCCL over
 xGMI) at the end of the timed region (distributed.ObjectiveAccumulator), so no
 collective sits on a step's critical path.
@@ -83,26 +85,17 @@ def make_inputs(B, N, D, device, seed):
     return X, y
 
 
-class EventTimer:
-    """HIP events recorded on the launching (current) stream around each launch. Events
-    are created up front: creating them inside the timed loop costs more host time than
-    the kernels themselves."""
-
-    def __init__(self, n):
-        self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                   for _ in range(n)]
-        self.n = 0
-
-    def __enter__(self):
-        self.ev[self.n][0].record()
-        return self
-
-    def __exit__(self, *exc):
-        self.ev[self.n][1].record()
-        self.n += 1
-
-    def mean_ms(self):
-        return float(np.mean([a.elapsed_time(b) for a, b in self.ev[:self.n]])) if self.n else 0.0
+def time_launches(fn, n):
+    """Mean time of n back-to-back calls of ``fn`` from ONE pair of HIP events on the
+    current (launch) stream. An event pair around every launch would add several us of
+    event overhead to each measured kernel."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        out = fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n, out
 
 
 def cpu_exact_baseline(N, D, seconds, threads):
@@ -177,7 +170,7 @@ def load_traffic(key):
 
 def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
     """BASELINE configs[4] per GPU: forward (K_ZZ factor + predictive mean / var / ELL)
-    and the fused backward, HIP events per kernel launch."""
+    and the fused backward, each timed over back-to-back launches (time_launches)."""
     g = torch.Generator().manual_seed(seed)
     X = (torch.randn(B, N, D, generator=g) / math.sqrt(D)).to(dev)
     y = torch.randn(B, N, generator=g).to(dev)
@@ -190,29 +183,20 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
     hyper = ops.pack_variational_hyper(LN2, LN2 + 1e-4, 1e-4, 0.1, w, ls, D, dev)
     gm = torch.randn(B, N, device=dev)
     gv = torch.randn(B, N, device=dev)
-    t_kzz, t_fwd, t_bwd = EventTimer(steps), EventTimer(steps), EventTimer(steps)
-
-    def step(timed):
-        if timed:
-            with t_kzz:
-                kz = ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h)
-            with t_fwd:
-                out = ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False)
-            with t_bwd:
-                adj = ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv)
-        else:
-            kz = ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h)
-            out = ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False)
-            adj = ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv)
+    def step():
+        kz = ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h)
+        out = ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False)
+        adj = ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv)
         return kz, out, adj
 
     for _ in range(warmup):
-        step(False)
+        kz, out, adj = step()
     torch.cuda.synchronize()
-    for _ in range(steps):
-        kz, out, adj = step(True)
-    torch.cuda.synchronize()
-    ms = {"kzz": t_kzz.mean_ms(), "fwd": t_fwd.mean_ms(), "bwd": t_bwd.mean_ms()}
+    # each phase in its own back-to-back loop (same inputs as the step's)
+    ms = {"kzz": time_launches(lambda: ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h), steps)[0],
+          "fwd": time_launches(lambda: ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper,
+                                                               want_flags=False), steps)[0],
+          "bwd": time_launches(lambda: ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv), steps)[0]}
     if world > 1:
         t = torch.tensor([ms["kzz"], ms["fwd"], ms["bwd"]], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -301,10 +285,12 @@ def main():
     hyper = ops.pack_exact_hyper(LN2, LN2 + 1e-4, 0.0, LN2, dev)   # GPyTorch init values
 
     info = torch.empty(B, device=dev, dtype=torch.int32)
+    Lbuf = torch.empty(B, N, N, device=dev, dtype=torch.float32)   # L written every step
 
     def step(mll_out):
         # one launch per step: the per-window MLL lands in the accumulator's row
-        return ops.exact_mll(X, y, None, None, None, None, hyper=hyper, mll_out=mll_out, info_out=info)
+        return ops.exact_mll(X, y, None, None, None, None, hyper=hyper, mll_out=mll_out,
+                             info_out=info, L_out=Lbuf)
 
     warm = ObjectiveAccumulator(args.warmup, dev, width=B)
     for _ in range(args.warmup):
@@ -313,22 +299,27 @@ def main():
     torch.cuda.synchronize()
     ops.check_cholesky_info(out.info, 1e-6, inputs=(X,))   # one sync, outside the timed region
 
-    timer = EventTimer(args.steps)
+    # the timed region: K eager launches bracketed by ONE pair of HIP events on the launch
+    # stream; roofline.kernel_ms = their elapsed time / K (an event pair around every
+    # launch adds 4-12 us of event overhead per 70 us kernel, and the same to the timed loop)
     acc = ObjectiveAccumulator(args.steps, dev, width=B)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(args.steps):
-        with timer:
-            out = step(acc.slot())
+        step(acc.slot())
+    ev1.record()
     totals, work = acc.reduce()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = timer.mean_ms()
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    ops.check_cholesky_info(info, 1e-6, inputs=(X,))
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -341,12 +332,7 @@ def main():
         X2, y2 = make_inputs(128, 128, D, dev, seed=11)
         for _ in range(3):
             ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper)
-        t2 = EventTimer(20)
-        for _ in range(20):
-            with t2:
-                o2 = ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper)
-        torch.cuda.synchronize()
-        ms2 = t2.mean_ms()
+        ms2, o2 = time_launches(lambda: ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper), 20)
         b2, f2 = bytes_per_window(128, D), flops_per_window(128, D)
         cfg2 = {"workload": "exact-GP windows B=128 N=128 D=32 (BASELINE configs[1]), L written",
                 "kernel_ms": ms2, "windows_per_s": 128 / (ms2 * 1e-3),
@@ -361,22 +347,12 @@ def main():
         gout = torch.ones(B, device=dev)
         ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
         torch.cuda.synchronize()
-        gt = EventTimer(5)
-        for _ in range(5):
-            with gt:
-                ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
-        torch.cuda.synchronize()
-        grad_ms = gt.mean_ms()
+        grad_ms = time_launches(lambda: ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout), 5)[0]
         # eval-mode posterior at Ns = N new points per window from the same factor
         Xs = make_inputs(B, N, D, dev, seed=77 + rank)[0]
         ops.exact_posterior(X, fw.L, fw.z, hyper, Xs)
         torch.cuda.synchronize()
-        pt = EventTimer(5)
-        for _ in range(5):
-            with pt:
-                ops.exact_posterior(X, fw.L, fw.z, hyper, Xs)
-        torch.cuda.synchronize()
-        post_ms = pt.mean_ms()
+        post_ms = time_launches(lambda: ops.exact_posterior(X, fw.L, fw.z, hyper, Xs), 5)[0]
 
     var = None
     if not args.no_var:

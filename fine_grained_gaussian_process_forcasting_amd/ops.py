@@ -54,7 +54,8 @@ class ExactMLLOut:
 def exact_mll(X: torch.Tensor, y: torch.Tensor, lengthscale, outputscale, mean_constant, noise,
               jitter: float = 1e-6, max_tries: int = 3, want_L: bool = True,
               want_z: bool = False, hyper: Optional[torch.Tensor] = None,
-              mll_out: Optional[torch.Tensor] = None, info_out: Optional[torch.Tensor] = None) -> ExactMLLOut:
+              mll_out: Optional[torch.Tensor] = None, info_out: Optional[torch.Tensor] = None,
+              L_out: Optional[torch.Tensor] = None) -> ExactMLLOut:
     """Fused exact-GP log marginal likelihood per window (one gfx950 kernel launch).
 
     X: (B, N, D) float32, y: (B, N) float32 on the same ROCm device. ``lengthscale``
@@ -83,7 +84,10 @@ def exact_mll(X: torch.Tensor, y: torch.Tensor, lengthscale, outputscale, mean_c
         raise ValueError("info_out must be a contiguous (B,) int32 tensor on X's device")
     mll = mll_out if mll_out is not None else torch.empty(B, device=dev, dtype=torch.float32)
     info = info_out if info_out is not None else torch.empty(B, device=dev, dtype=torch.int32)
-    L = torch.empty(B, N, N, device=dev, dtype=torch.float32) if want_L else None
+    if L_out is not None and (L_out.shape != (B, N, N) or L_out.dtype != torch.float32
+                              or not L_out.is_contiguous() or L_out.device != dev):
+        raise ValueError("L_out must be a contiguous (B, N, N) float32 tensor on X's device")
+    L = (L_out if L_out is not None else torch.empty(B, N, N, device=dev, dtype=torch.float32)) if want_L else None
     z = torch.empty(B, N, device=dev, dtype=torch.float32) if want_z else None
     rc = _native.lib().gpk_exact_mll_f32(
         X.data_ptr(), y.data_ptr(), hyper.data_ptr(), n_ls, B, N, D, float(jitter), int(max_tries),
