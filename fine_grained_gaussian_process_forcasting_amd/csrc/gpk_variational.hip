@@ -175,9 +175,20 @@ gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M
 #endif
   KZ_STAMP(0);
 
-  for (int e = tid; e < M * ZS; e += KT) {
-    const int m = e / ZS, d = e - m * ZS;
-    zt[e] = d < D ? Z[m * D + d] / ls[d] : 0.f;
+  for (int base = 0; base < M * ZS; base += 8 * KT) {   // 8 loads in flight per thread
+    float v[8], l[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * KT + tid, m = e / ZS, d = e - m * ZS;
+      const bool ok = e < M * ZS && d < D;
+      v[u] = Z[ok ? m * D + d : 0];
+      l[u] = ls[ok ? d : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * KT + tid, d = e % ZS;
+      if (e < M * ZS) zt[e] = d < D ? v[u] / l[u] : 0.f;
+    }
   }
   for (int e = tid; e < 6 * Mp * 4; e += KT) P[e] = 0.0;   // both parities of P / lb / xr
   lds_barrier();
@@ -502,9 +513,22 @@ GPK_DEVICE void stage_inducing(const float* __restrict__ Z, const float* __restr
                                int M, int D, int MP, int Dq, int ds, float* zs, float* zn, float* cm,
                                float* vm, float* sm1) {
   const int tid = threadIdx.x, T = blockDim.x;
-  for (int e = tid; e < MP * Dq; e += T) {
-    const int m = e / Dq, d = e - m * Dq;
-    zs[m * ds + d] = (m < M && d < D) ? Z[m * D + d] / ls[d] : 0.f;
+  // 8 unconditional loads (clamped addresses) in flight per thread, then the stores:
+  // a predicated load per loop iteration costs one full memory latency each
+  for (int base = 0; base < MP * Dq; base += 8 * T) {
+    float v[8], l[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * T + tid, m = e / Dq, d = e - m * Dq;
+      const bool ok = e < MP * Dq && m < M && d < D;
+      v[u] = Z[ok ? m * D + d : 0];
+      l[u] = ls[ok ? d : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * T + tid, m = e / Dq, d = e - m * Dq;
+      if (e < MP * Dq) zs[m * ds + d] = (m < M && d < D) ? v[u] / l[u] : 0.f;
+    }
   }
   for (int m = tid; m < MP; m += T) {
     vm[m] = (m < M) ? vmean[m] : 0.f;
@@ -534,9 +558,20 @@ GPK_DEVICE void stage_inducing(const float* __restrict__ Z, const float* __restr
 GPK_DEVICE void stage_points(const float* __restrict__ Xw, const float* __restrict__ ls, int nvalid,
                              int D, int TW, int Dq, int ds, const float* cm, float* xs, float* xn) {
   const int tid = threadIdx.x, T = blockDim.x;
-  for (int e = tid; e < TW * Dq; e += T) {
-    const int j = e / Dq, d = e - j * Dq;
-    xs[j * ds + d] = (j < nvalid && d < D) ? Xw[(size_t)j * D + d] / ls[d] - cm[d] : 0.f;
+  for (int base = 0; base < TW * Dq; base += 4 * T) {   // loads in flight together (stage_inducing)
+    float v[4], l[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = base + u * T + tid, j = e / Dq, d = e - j * Dq;
+      const bool ok = e < TW * Dq && j < nvalid && d < D;
+      v[u] = Xw[ok ? (size_t)j * D + d : 0];
+      l[u] = ls[ok ? d : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = base + u * T + tid, j = e / Dq, d = e - j * Dq;
+      if (e < TW * Dq) xs[j * ds + d] = (j < nvalid && d < D) ? v[u] / l[u] - cm[d] : 0.f;
+    }
   }
   lds_barrier();
   for (int j = tid; j < TW; j += T) {
@@ -1332,9 +1367,18 @@ GPK_DEVICE void stage_reg(const float* Z, const float* ls, const float* vmean, c
   stage_inducing(Z, ls, vmean, vstd, M, D, 64, DQ, L::ZS, sm + L::zs, sm + L::zn, sm + L::cm,
                  sm + L::vm, sm + L::sm1);
   double* li = (double*)(sm + L::li);
-  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
-    const int r = e >> 6, c = e & 63;
-    li[r * RLS + c] = (r < M && c < M) ? Linv[(size_t)r * M + c] : 0.0;
+  for (int base = 0; base < 64 * 64; base += 8 * (int)blockDim.x) {   // 8 loads in flight
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * blockDim.x + threadIdx.x, r = e >> 6, c = e & 63;
+      v[u] = Linv[(e < 64 * 64 && r < M && c < M) ? (size_t)r * M + c : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * blockDim.x + threadIdx.x, r = e >> 6, c = e & 63;
+      if (e < 64 * 64) li[r * RLS + c] = (r < M && c < M) ? v[u] : 0.0;
+    }
   }
   lds_barrier();
 }
