@@ -344,11 +344,22 @@ __global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : 8) gpk_grad_gram_kerne
   float* xs = smem;                  // NP x XS
   float* nrm = xs + NP * XS;         // NP
   float* al = nrm + NP;              // NP
-  for (int e = tid; e < NP * DP; e += 64 * kGW) {
-    const int n = e / DP, d = e - n * DP;
-    float v = 0.f;
-    if ((FULL || n < N) && d < D) v = Xb[(size_t)n * D + d] / hyp[3 + (ard ? d : 0)] - wsb[ws.mean + d];
-    xs[n * XS + d] = v;
+  // loads of 4 iterations in flight (clamped unconditional addresses), then the stores
+  for (int base = 0; base < NP * DP; base += 4 * 64 * kGW) {
+    float v[4], l[4], mu[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = base + u * 64 * kGW + tid, n = e / DP, d = e - n * DP;
+      const bool ok = e < NP * DP && (FULL || n < N) && d < D;
+      v[u] = Xb[ok ? (size_t)n * D + d : 0];
+      l[u] = hyp[3 + ((ok && ard) ? d : 0)];
+      mu[u] = wsb[ws.mean + (ok ? d : 0)];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = base + u * 64 * kGW + tid, n = e / DP, d = e - n * DP;
+      if (e < NP * DP) xs[n * XS + d] = ((FULL || n < N) && d < D) ? v[u] / l[u] - mu[u] : 0.f;
+    }
   }
   for (int n = tid; n < NP; n += 64 * kGW) al[n] = wsb[ws.alpha + n];
   lds_barrier();

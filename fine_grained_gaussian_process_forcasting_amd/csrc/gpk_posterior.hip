@@ -89,22 +89,39 @@ __global__ __launch_bounds__(256) void gpk_post_kernel(GpkPostArgs a) {
   const float* Lb = a.L + (size_t)b * N * N;
 
   // ---- prologue: training inputs / l into LDS (zero padded), z, diagonal blocks of L
-  for (int e = tid; e < NP * DP; e += 256) {
-    const int n = e / DP, d = e - n * DP;
-    float v = 0.f;
-    if (n < N && d < D) v = Xb[(size_t)n * D + d] / (ard ? ls[d] : ls[0]);
-    xtr[n * XS + d] = v;
+  // 8 unconditional loads (clamped addresses) in flight per thread, then the stores: a
+  // predicated load per loop iteration would cost one full memory latency each
+  for (int base = 0; base < NP * DP; base += 8 * 256) {
+    float v[8], l[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * 256 + tid, n = e / DP, d = e - n * DP;
+      const bool ok = e < NP * DP && n < N && d < D;
+      v[u] = Xb[ok ? (size_t)n * D + d : 0];
+      l[u] = ls[(ok && ard) ? d : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * 256 + tid, n = e / DP, d = e - n * DP;
+      if (e < NP * DP) xtr[n * XS + d] = (n < N && d < D) ? v[u] / l[u] : 0.f;
+    }
   }
   for (int n = tid; n < NP; n += 256) zv[n] = n < N ? a.z[(size_t)b * N + n] : 0.f;
   {
     const int bi = tid >> 4, m = tid & 15;   // tile bi, row m (NB <= 16 -> 256 rows)
     if (bi < NB) {
       const int row = 16 * bi + m;
+      float lv[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {   // unconditional (clamped) loads, all in flight
+        const bool ok = k <= m && row < N;
+        lv[k] = Lb[ok ? (size_t)row * N + 16 * bi + k : 0];
+      }
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int col = 16 * bi + k;
         float v = (row == col) ? 1.f : 0.f;  // identity on padded rows
-        if (k <= m && row < N) v = Lb[(size_t)row * N + col];
+        if (k <= m && row < N) v = lv[k];
         ltmp[bi * 256 + m * 16 + k] = v;
       }
     }
