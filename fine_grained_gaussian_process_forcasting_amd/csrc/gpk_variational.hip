@@ -1590,9 +1590,10 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) {
     const int d = 16 * dt + c;
-    ilc[dt] = d < D ? 1.f / ls[d] : 0.f;
+    const float lsv = ls[d < D ? d : 0], wv_ = w[d < D ? d : 0];   // unconditional loads
+    ilc[dt] = d < D ? 1.f / lsv : 0.f;
     cmc[dt] = vsm[L::cm + d];
-    wc[dt] = d < D ? w[d] : 0.f;
+    wc[dt] = d < D ? wv_ : 0.f;
   }
   f32x4 qx[4][NDT];
 #pragma unroll
@@ -1739,16 +1740,19 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     for (int q = 0; q < 2; ++q) {
       float xb2[4][NDT];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int i = i0 + 16 * q + 4 * s + g;
-        const bool ok = i < N;
-        const float* xr = X + (col0 + (ok ? i : 0)) * D;
+      for (int s = 0; s < 4; ++s)     // unconditional (clamped) loads: all in flight together
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
-          const int d = 16 * dt + c;
-          xb2[s][dt] = (ok && d < D) ? xr[d] * ilc[dt] - cmc[dt] : 0.f;
+          const int i = i0 + 16 * q + 4 * s + g, d = 16 * dt + c;
+          xb2[s][dt] = X[(i < N && d < D) ? (col0 + i) * D + d : 0];
         }
-      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int i = i0 + 16 * q + 4 * s + g, d = 16 * dt + c;
+          xb2[s][dt] = (i < N && d < D) ? xb2[s][dt] * ilc[dt] - cmc[dt] : 0.f;
+        }
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt) {
 #pragma unroll
@@ -1765,6 +1769,17 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       }
     }
     // dX_i = ((Q^T zs)_i - xs_i r_i) / l + gmean_i w; sum_i r_i xs_i^2, sum_i gmean_i xs_i
+    // (the point values are requested up front, unconditionally: clamped addresses)
+    float xo[2][4][NDT];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int i = i0 + 16 * q + 4 * g + r, d = 16 * dt + c;
+          xo[q][r][dt] = X[(i < N && d < D) ? (col0 + i) * D + d : 0];
+        }
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -1774,12 +1789,11 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         const float gm = __shfl(gmq[q], pc, 64);
         const int i = i0 + 16 * q + pc;
         if (i < N) {
-          const float* xr = X + (col0 + i) * D;
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) {
             const int d = 16 * dt + c;
             if (d < D) {
-              const float xv = xr[d] * ilc[dt] - cmc[dt];
+              const float xv = xo[q][r][dt] * ilc[dt] - cmc[dt];
               dX[(col0 + i) * D + d] = (xz[q][dt][r] - xv * rr) * ilc[dt] + gm * wc[dt];
               rx2[dt] = __builtin_fmaf(rr * xv, xv, rx2[dt]);
               gx[dt] = __builtin_fmaf(gm, xv, gx[dt]);
