@@ -883,17 +883,23 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
             for (int r = 0; r < 4; ++r) v[4 * u + r] = t[r];
           }
         } else {
+          // ragged: clamped unconditional loads (all 16 in flight), masked afterwards
+#pragma unroll
+          for (int e = 0; e < 16; ++e) v[e] = Xb[(n < N && d0 + e < D) ? (size_t)n * D + d0 + e : 0];
 #pragma unroll
           for (int e = 0; e < 16; ++e)
-            v[e] = (n < N && d0 + e < D) ? Xb[(size_t)n * D + d0 + e] : 0.f;
+            if (!(n < N && d0 + e < D)) v[e] = 0.f;
         }
         if (n_ls == 1) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) v[e] *= inv_l0;
         } else {
+          float l[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) l[e] = hyp[3 + (d0 + e < D ? d0 + e : 0)];
 #pragma unroll
           for (int e = 0; e < 16; ++e)
-            if (d0 + e < D) v[e] = v[e] / hyp[3 + d0 + e];
+            if (d0 + e < D) v[e] = v[e] / l[e];
         }
 #pragma unroll
         for (int e = 0; e < 16; ++e) mx = __builtin_fmaxf(mx, __builtin_fabsf(v[e]));

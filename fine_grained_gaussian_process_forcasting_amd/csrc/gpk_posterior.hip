@@ -177,15 +177,28 @@ __global__ __launch_bounds__(256) void gpk_post_kernel(GpkPostArgs a) {
   const bool live = col < Ns;
   f32x4 xs[DQ];
   float nxs = 0.f;
+  {
+    // all DQ*4 coordinates requested before any is used: clamped in-bounds addresses,
+    // the dead lanes/coordinates masked afterwards
+    const float* xrow = a.Xs + ((size_t)b * Ns + (live ? col : 0)) * D;
+    float raw[DQ][4];
 #pragma unroll
-  for (int q = 0; q < DQ; ++q) {
+    for (int q = 0; q < DQ; ++q)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int d = 16 * q + 4 * g + r;
-      float v = 0.f;
-      if (live && d < D) v = a.Xs[((size_t)b * Ns + col) * D + d] / (ard ? ls[d] : ls[0]) - red[256 + d];
-      xs[q][r] = v;
-      nxs = __builtin_fmaf(v, v, nxs);
+      for (int r = 0; r < 4; ++r) {
+        const int d = 16 * q + 4 * g + r;
+        raw[q][r] = xrow[d < D ? d : 0];
+      }
+#pragma unroll
+    for (int q = 0; q < DQ; ++q) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int d = 16 * q + 4 * g + r;
+        float v = 0.f;
+        if (live && d < D) v = raw[q][r] / (ard ? ls[d] : ls[0]) - red[256 + d];
+        xs[q][r] = v;
+        nxs = __builtin_fmaf(v, v, nxs);
+      }
     }
   }
   nxs += __shfl_xor(nxs, 16, 64);
@@ -196,6 +209,18 @@ __global__ __launch_bounds__(256) void gpk_post_kernel(GpkPostArgs a) {
   float mp = 0.f, vp = 0.f;
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
+    // FULL: this lane's L row-block operands for the update below, all requested up front
+    // (they come from L2: one latency per block row, hidden under the Gram tile and exp2;
+    // fetching them a block row earlier measured no faster). The ragged path keeps
+    // per-element predicated loads at their use (hoisting 4 scalars per block would double
+    // its register footprint).
+    const int lrow = 16 * i + c;
+    f32x4 la[NB > 1 ? NB - 1 : 1];
+    if (FULL) {
+#pragma unroll
+      for (int j = 0; j < i; ++j) la[j] = *(const f32x4*)&Lb[(size_t)lrow * N + 16 * j + 4 * g];
+      __builtin_amdgcn_sched_barrier(0);   // keep the loads issued here, ahead of the Gram
+    }
     // K*_i (acc layout: reg r = row 16i + 4g + r, column c)
     f32x4 G = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -214,18 +239,17 @@ __global__ __launch_bounds__(256) void gpk_post_kernel(GpkPostArgs a) {
     }
     // - sum_{j<i} L_ij V_j (two accumulators: halves the dependent MFMA chain)
     f32x4 U0 = {0.f, 0.f, 0.f, 0.f}, U1 = {0.f, 0.f, 0.f, 0.f};
-    const int lrow = 16 * i + c;
 #pragma unroll
     for (int j = 0; j < i; ++j) {
-      f32x4 la;
+      f32x4 lj;
       if (FULL) {
-        la = *(const f32x4*)&Lb[(size_t)lrow * N + 16 * j + 4 * g];
+        lj = la[j];
       } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) la[r] = lrow < N ? Lb[(size_t)lrow * N + 16 * j + 4 * g + r] : 0.f;
+        for (int r = 0; r < 4; ++r) lj[r] = lrow < N ? Lb[(size_t)lrow * N + 16 * j + 4 * g + r] : 0.f;
       }
-      if (j & 1) U1 = mfma4(la, V[j], U1);
-      else U0 = mfma4(la, V[j], U0);
+      if (j & 1) U1 = mfma4(lj, V[j], U1);
+      else U0 = mfma4(lj, V[j], U0);
     }
     Cm = Cm - U0 - U1;
     const f32x4 di = *(const f32x4*)&dinv[i * 256 + c * 16 + 4 * g];
