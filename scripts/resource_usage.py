@@ -8,10 +8,11 @@ import sys
 
 ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
 src = sys.argv[1]
-flt = sys.argv[2] if len(sys.argv) > 2 else ""
+flt = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("-D") else ""
+defs = [a for a in sys.argv[2:] if a.startswith("-D")]
 r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC",
                     "-I", f"{ROOT}/include", "-c", src, "-o", "/tmp/_ru.o",
-                    "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+                    "-Rpass-analysis=kernel-resource-usage"] + defs, capture_output=True, text=True)
 rows, cur = [], None
 for line in r.stderr.splitlines():
     m = re.search(r"remark: Function Name: (\S+)", line)
