@@ -1494,12 +1494,20 @@ GPK_DEVICE void dim_consts(const float* sm, const float* ls, const float* w, int
                            float (&cmv)[DQ / 4], float (&wv)[DQ / 4]) {
   using L = RegLds<DQ>;
   const int g = (threadIdx.x & 63) >> 4;
+  // every load issued first (clamped in-bounds addresses), then masked
+  float lv[DQ / 4], wl[DQ / 4];
+#pragma unroll
+  for (int s = 0; s < DQ / 4; ++s) {
+    const int d = 4 * s + g, dc = d < D ? d : 0;
+    lv[s] = ls[dc];
+    wl[s] = w != nullptr ? w[dc] : 0.f;
+  }
 #pragma unroll
   for (int s = 0; s < DQ / 4; ++s) {
     const int d = 4 * s + g;
-    il[s] = d < D ? 1.f / ls[d] : 0.f;
+    il[s] = d < D ? 1.f / lv[s] : 0.f;
     cmv[s] = sm[L::cm + d];
-    wv[s] = (d < D && w != nullptr) ? w[d] : 0.f;
+    wv[s] = d < D ? wl[s] : 0.f;
   }
 }
 
