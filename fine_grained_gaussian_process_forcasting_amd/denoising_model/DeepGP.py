@@ -53,14 +53,26 @@ class ToyDeepGPHiddenLayer(nn.Module):
         return self.variational_strategy(x)
 
     def __call__(self, x, *other_inputs, **kwargs):
-        if len(other_inputs):
-            raise NotImplementedError("skip-connection inputs are unused by the reference path")
-        if not isinstance(self.mean_module, LinearMean):
-            raise NotImplementedError("the fused kernel implements DeepGPp's LinearMean (DeepGP.py:81)")
-        output = self.variational_strategy(x)
-        # DeepGPLayer.__call__: deterministic inputs -> expand to (S, *batch) with
-        # S = settings.num_likelihood_samples (1 under train.py:20)
+        """DeepGP.py:56-73 + DeepGPLayer.__call__ (upstream models/deep_gps/deep_gp.py).
+
+        Skip connections (``other_inputs``): each extra input is expanded to
+        (S, *shape) and concatenated to ``x`` on the feature axis; ``x`` is then taken
+        as samples (``are_samples=True``: shape (S, ..., N, D_x)) and the output is NOT
+        expanded again. Otherwise the deterministic inputs give q(f) with batch (..., )
+        expanded to (S, ...), S = settings.num_likelihood_samples (1 under train.py:20).
+        Both mean types run on the fused kernel: ConstantMean is LinearMean with w = 0
+        and b0 = the constant (ops_autograd.variational_predict)."""
+        are_samples = bool(len(other_inputs))
         S = settings.num_likelihood_samples.value()
+        if are_samples:
+            processed = [inp.unsqueeze(0).expand(S, *inp.shape) for inp in other_inputs]
+            x = torch.cat([x] + processed, dim=-1)
+        if x.size(-1) != self.input_dims:
+            raise RuntimeError(f"Input shape did not match self.input_dims. Got total feature dims "
+                               f"[{x.size(-1)}], expected [{self.input_dims}]")
+        output = self.variational_strategy(x)
+        if are_samples:
+            return output
         return output.expand(torch.Size([S]) + output.batch_shape)
 
 

@@ -21,7 +21,23 @@ rewritten by every replay.
 
 Requirements (checked): CUDA/ROCm tensors, an optimizer built with
 ``capturable=True`` (Adam/AdamW keep their step counters on the device), input shapes
-fixed across steps. The ``warmup`` eager steps that precede the capture are real
+fixed across steps, and a learning rate that the graph can see: a float ``lr`` is baked
+into the captured optimizer step, so a schedule that rewrites ``param_group['lr']`` on
+the host (the reference's NoamOpt, train.py:147) must hold the lr in a device tensor
+(``Adam(..., lr=torch.tensor(0.0, device=...), capturable=True)``) and update it in
+place; changing a float lr after capture raises instead of silently training at the
+capture-time rate.
+
+Failure semantics match the eager step: eager ``psd_safe_cholesky`` raises
+NotPSDError / NanError in the forward, before the backward and the optimizer step
+touch anything. A replay has already run the optimizer step when its verdict is
+read, so every replay that a check covers is bracketed: the parameters and the
+optimizer state are snapshotted (device copies) when a check block starts, a sticky
+device flag collects every hard failure (info > 0) of every replay in the block, and
+on a failure the snapshot is restored before the error is raised -- the parameters
+and Adam moments come back exactly as they were before the failing block.
+
+The ``warmup`` eager steps that precede the capture are real
 training steps on the sample inputs (PyTorch's documented whole-network capture
 recipe). The package's factor caches are keyed on tensor version counters, which a
 replay does not bump, so they are invalidated after every replay.
@@ -51,6 +67,7 @@ class GraphedStep:
                                  "to be captured in a HIP graph")
         if check_every < 1:
             raise ValueError("check_every must be >= 1")
+        self._lr_captured = [g.get("lr") for g in optimizer.param_groups]
         self.loss_fn = loss_fn
         self.optimizer = optimizer
         self.check_every = check_every
@@ -66,7 +83,7 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
 
         self.graph = torch.cuda.CUDAGraph()
-        self.checks = ops.DeferredChecks()
+        self.checks = ops.DeferredChecks(device=self.static_inputs[0].device)
         optimizer.zero_grad(set_to_none=True)
         ops._RECORDERS.append(self.checks)
         try:
@@ -79,6 +96,14 @@ class GraphedStep:
         finally:
             ops._RECORDERS.remove(self.checks)
         invalidate_caches()
+        # rollback state: every parameter of the optimizer and every tensor of its state
+        self._state = [p for g in optimizer.param_groups for p in g["params"]]
+        for p in list(self._state):
+            for v in optimizer.state.get(p, {}).values():
+                if isinstance(v, torch.Tensor) and v.is_cuda:
+                    self._state.append(v)
+        self._backup = [t.detach().clone() for t in self._state]
+        self._block_open = False
 
     def _loss(self, outputs) -> torch.Tensor:
         return outputs[self.loss_index] if isinstance(outputs, (tuple, list)) else outputs
@@ -96,9 +121,37 @@ class GraphedStep:
                 raise ValueError(f"input shape {tuple(src.shape)} != captured {tuple(dst.shape)}")
             if src.data_ptr() != dst.data_ptr():
                 dst.copy_(src, non_blocking=True)
+        for g, lr0 in zip(self.optimizer.param_groups, self._lr_captured):
+            lr = g.get("lr")
+            if isinstance(lr0, torch.Tensor):
+                if lr is not lr0:
+                    raise ValueError("param_group['lr'] was replaced after capture; update the "
+                                     "captured lr tensor in place (lr.fill_(...)) instead")
+            elif lr != lr0:
+                raise ValueError(f"param_group['lr'] changed from {lr0} to {lr} after capture, but a "
+                                 "float lr is fixed inside the HIP graph; build the optimizer with a "
+                                 "device-tensor lr and update it in place")
+        if not self._block_open:
+            # start of a check block: snapshot parameters + optimizer state (device copies,
+            # stream-ordered before the replay) and clear the sticky failure flag
+            torch._foreach_copy_(self._backup, [t.detach() for t in self._state])
+            self.checks.reset_sticky()
+            self._block_open = True
         self.graph.replay()
         invalidate_caches()
         self._n += 1
         if self._n % self.check_every == 0:
-            self.checks.check()
+            self._block_open = False
+            try:
+                self.checks.check()
+            except Exception:
+                self.rollback()
+                raise
         return self.static_outputs
+
+    def rollback(self) -> None:
+        """Restore the parameters and optimizer state saved at the start of the current
+        check block (called automatically when a replay's verdict raises)."""
+        with torch.no_grad():
+            torch._foreach_copy_([t.detach() for t in self._state], self._backup)
+        self._block_open = False

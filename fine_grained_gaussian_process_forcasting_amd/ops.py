@@ -178,17 +178,39 @@ class DeferredChecks:
     would have for that replay's data (graphs.GraphedStep calls it).
     """
 
-    def __init__(self):
+    def __init__(self, device=None):
         self.items = []
+        # (1,) int32 device flag: any hard failure since reset_sticky(). Allocated before
+        # the capture (a tensor created inside it would be re-zeroed by every replay)
+        self.sticky = torch.zeros(1, dtype=torch.int32, device=device) if device is not None else None
+
+    def add(self, kind: str, args: tuple) -> None:
+        self.items.append((kind, args))
+        if kind == "cholesky":
+            # fold this replay's hard failures (info > 0: NotPSD / NaN / timeout) into the
+            # sticky flag IN the graph, so failures of replays that are not checked
+            # individually (check_every > 1) are not lost
+            info = args[0]
+            if self.sticky is None:
+                raise RuntimeError("DeferredChecks used in a capture without a device flag "
+                                   "(construct it with device=...)")
+            self.sticky.copy_(torch.maximum(self.sticky, (info > 0).any().to(torch.int32).reshape(1)))
+
+    def reset_sticky(self) -> None:
+        if self.sticky is not None:
+            self.sticky.zero_()
 
     def check(self) -> None:
         for kind, args in self.items:
             if kind == "cholesky":
-                info, jitter, what, max_tries = args
-                check_cholesky_info(info, jitter, (), what, max_tries)
+                info, jitter, what, max_tries, inputs = args
+                check_cholesky_info(info, jitter, inputs, what, max_tries)
             else:
                 from .gp import warn_if_clamped
                 warn_if_clamped(*args)
+        if self.sticky is not None and int(self.sticky.item()) != 0:
+            raise NotPSDError("a replay of this check block failed psd_safe_cholesky (not PD after "
+                              "the jitter ladder, or NaN inputs); state rolled back to the block start")
 
 
 _RECORDERS: list = []
@@ -200,7 +222,7 @@ def record_or_run(kind: str, args: tuple, run) -> None:
         if not _RECORDERS:
             raise RuntimeError("gpk: a HIP graph capture reached a host-side numerical check; "
                                "capture through graphs.GraphedStep, which defers the checks")
-        _RECORDERS[-1].items.append((kind, args))
+        _RECORDERS[-1].add(kind, args)
         return
     run()
 
@@ -216,7 +238,7 @@ def check_cholesky_info(info: torch.Tensor, jitter: float, inputs=(), what: str 
     Under HIP graph capture the check is recorded (DeferredChecks) instead.
     """
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-        record_or_run("cholesky", (info, jitter, what, max_tries), None)
+        record_or_run("cholesky", (info, jitter, what, max_tries, tuple(inputs)), None)
         return
     info_h = info.detach().to("cpu")
     if not bool((info_h != 0).any()):

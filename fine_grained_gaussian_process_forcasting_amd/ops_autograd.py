@@ -101,17 +101,32 @@ class KzzCache:
             ops.check_cholesky_info(info, 1e-8, inputs=(Z,), what="K_ZZ cholesky")
 
 
+def _mean_params(mean_module, D, device):
+    """(w, b0) of the kernel's mean x.w + b0 (DeepGP.py:42-45): LinearMean as is;
+    ConstantMean c as w = 0 (no gradient), b0 = c, so d/dc = sum of the mean gradient."""
+    if hasattr(mean_module, "weights"):
+        w = mean_module.weights.reshape(-1)
+        b0 = mean_module.bias.reshape(()) if mean_module.bias is not None else torch.zeros((), device=device)
+        return w, b0
+    if hasattr(mean_module, "constant"):
+        return torch.zeros(D, device=device), mean_module.constant.reshape(())
+    raise NotImplementedError(f"mean module {type(mean_module).__name__} is not on the reference path "
+                              "(DeepGP.py:42-45: ConstantMean or LinearMean)")
+
+
 def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module, jitter,
                         cache: Optional[KzzCache] = None, key_tensors=None):
     """q(f) mean / variance / clamp flag for (B, N, D) windows (HIP forward and backward;
     see module docstring). ``cache`` shares the K_ZZ factor between calls."""
-    w = mean_module.weights.reshape(-1)
-    b0 = mean_module.bias.reshape(()) if mean_module.bias is not None else torch.zeros((), device=x.device)
+    w, b0 = _mean_params(mean_module, x.shape[-1], x.device)
     s2 = outputscale.reshape(())
     ls = lengthscale.reshape(-1)
-    if cache is None:
+    if cache is None or key_tensors is None:
+        # no caller-held parameters to key on: a fresh, private factor (keys on derived
+        # temporaries could alias reused allocator memory and return a stale factor)
         cache = KzzCache()
-    Linv = cache.factor(Z, s2, ls, jitter, key_tensors if key_tensors is not None else (Z, s2, ls))
+        key_tensors = (Z, s2, ls)
+    Linv = cache.factor(Z, s2, ls, jitter, key_tensors)
     out = torch.ops.gpk.variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, float(jitter))
     cache.check_pending()
     return out

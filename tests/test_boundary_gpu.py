@@ -1,0 +1,195 @@
+"""The rest of the reference class surface on the GPU kernels (VERDICT r02 "missing" 2 and
+row a12), each against the fp64 oracle at 1e-4, forward and backward:
+
+* ``ToyDeepGPHiddenLayer(mean_type='constant')`` -- the class default
+  (/root/reference/denoising_model/DeepGP.py:15,42-43): ConstantMean runs on the fused
+  kernel as LinearMean with w = 0, b0 = c; d/dc = sum of the mean gradient.
+* the skip-connection branch of ``ToyDeepGPHiddenLayer.__call__`` (DeepGP.py:56-73):
+  x taken as samples (S, b, N, D1), other inputs expanded to (S, b, N, D2) and
+  concatenated; no second expansion (``are_samples=True``).
+* ``denoise_model_2.add_gp_noise`` and ``forward`` with ``gp=True``
+  (denoise_model_2.py:32-59): x + proj_up(mean) with proj_up = nn.Linear(1, d) restored
+  (SURVEY B1), compared with oracle mean -> nn.Linear(1, d) -> + x at the cfg-3 shape.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from oracle import gp_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _rows_rel(got, want):
+    got = np.asarray(got, np.float64).reshape(want.shape[0], -1)
+    want = np.asarray(want, np.float64).reshape(want.shape[0], -1)
+    return float(np.max(np.linalg.norm(got - want, axis=1) / np.maximum(np.linalg.norm(want, axis=1), 1e-30)))
+
+
+def _layer_params(hl, linear=True):
+    vs = hl.variational_strategy
+    P = dict(Z=vs.inducing_points.detach().cpu().double().numpy(),
+             m=vs._variational_distribution.variational_mean.detach().cpu().double().numpy(),
+             s=vs._variational_distribution._variational_stddev.detach().cpu().double().numpy(),
+             ls=hl.covar_module.base_kernel.lengthscale.detach().cpu().double().numpy().reshape(-1),
+             s2=float(hl.covar_module.outputscale.item()))
+    D = P["Z"].shape[1]
+    if linear:
+        P["w"] = hl.mean_module.weights.detach().cpu().double().numpy().reshape(-1)
+        P["b0"] = float(hl.mean_module.bias.item())
+    else:
+        P["w"] = np.zeros(D)
+        P["b0"] = float(hl.mean_module.constant.item())
+    return P
+
+
+def test_constant_mean_layer_forward_backward(cuda_device):
+    from fine_grained_gaussian_process_forcasting_amd import settings
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.DeepGP import ToyDeepGPHiddenLayer
+    from fine_grained_gaussian_process_forcasting_amd.gp import ConstantMean
+    dev = cuda_device
+    D, b, N, M = 16, 6, 40, 64
+    hl = ToyDeepGPHiddenLayer(D, None, 1234, num_inducing=M).to(dev)       # mean_type='constant'
+    assert isinstance(hl.mean_module, ConstantMean)
+    assert "mean_module.constant" in dict(hl.named_parameters())
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(b, N, D, generator=g) / math.sqrt(D)).to(dev).requires_grad_(True)
+    with torch.no_grad():
+        hl.mean_module.constant.fill_(0.37)
+    with settings.num_likelihood_samples(1):
+        dist = hl(x)
+    assert tuple(dist.mean.shape) == (1, b, N)
+    P = _layer_params(hl, linear=False)
+    args = (P["Z"], P["ls"], P["s2"], P["w"], P["b0"], P["m"], P["s"])
+    ref = O.variational_forward(x.detach().cpu().double().numpy(), *args, jitter=1e-4, dtype=np.float64)
+    assert _rows_rel(dist.mean[0].detach().cpu(), ref.mean) <= TOL
+    assert _rows_rel(dist.variance[0].detach().cpu(), ref.var) <= TOL
+    gm = torch.randn(b, N, generator=g)
+    gv = torch.randn(b, N, generator=g)
+    ((dist.mean[0] * gm.to(dev)).sum() + (dist.variance[0] * gv.to(dev)).sum()).backward()
+    want = O.variational_grads(x.detach().cpu().double().numpy(), *args, gm.double().numpy(),
+                               gv.double().numpy(), jitter=1e-4)
+    assert _rel(hl.mean_module.constant.grad.cpu(), want["bias"]) <= TOL          # d/dc
+    assert _rel(x.grad.cpu(), want["X"]) <= TOL
+    assert _rel(hl.variational_strategy.inducing_points.grad.cpu(), want["Z"]) <= TOL
+    vd = hl.variational_strategy._variational_distribution
+    assert _rel(vd.variational_mean.grad.cpu(), want["m"]) <= TOL
+    assert _rel(vd._variational_stddev.grad.cpu(), want["s"]) <= TOL
+
+
+def test_skip_connection_inputs(cuda_device):
+    """hidden_layer(x_samples, other) == the layer on cat([x_samples, other expanded], -1),
+    with the output kept at the samples' batch (S, b) (DeepGPLayer are_samples=True)."""
+    from fine_grained_gaussian_process_forcasting_amd import settings
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.DeepGP import ToyDeepGPHiddenLayer
+    dev = cuda_device
+    D1, D2, b, N, M, S = 8, 4, 5, 24, 32, 3
+    hl = ToyDeepGPHiddenLayer(D1 + D2, None, 7, num_inducing=M, mean_type='linear').to(dev)
+    g = torch.Generator().manual_seed(11)
+    xs = (torch.randn(S, b, N, D1, generator=g) / 3).to(dev)
+    other = (torch.randn(b, N, D2, generator=g) / 3).to(dev)
+    with settings.num_likelihood_samples(S):
+        dist = hl(xs, other)
+        with pytest.raises(RuntimeError, match="input_dims"):
+            hl(xs)                                          # D1 != input_dims
+    assert tuple(dist.mean.shape) == (S, b, N)
+    cat = torch.cat([xs, other.unsqueeze(0).expand(S, b, N, D2)], -1).reshape(S * b, N, D1 + D2)
+    P = _layer_params(hl)
+    ref = O.variational_forward(cat.cpu().double().numpy(), P["Z"], P["ls"], P["s2"], P["w"], P["b0"],
+                                P["m"], P["s"], jitter=1e-4, dtype=np.float64)
+    assert _rows_rel(dist.mean.reshape(S * b, N).detach().cpu(), ref.mean) <= TOL
+    assert _rows_rel(dist.variance.reshape(S * b, N).detach().cpu(), ref.var) <= TOL
+
+
+def _dm(d, dev, backbone=None):
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.denoise_model_2 import denoise_model_2
+    return denoise_model_2(backbone if backbone is not None else nn.Identity(), "ATA", True, d, dev, 1234).to(dev)
+
+
+def test_add_gp_noise_vs_oracle_cfg3(cuda_device):
+    """add_gp_noise at the cfg-3 shape (b=256, enc N=192, d=32, M=256): x + Linear(1, d)(mean)
+    against the oracle mean pushed through the same Linear, and every gradient of
+    sum(c * x_noisy) (x, proj_up.weight / bias, the GP parameters)."""
+    from fine_grained_gaussian_process_forcasting_amd import settings
+    dev = cuda_device
+    b, N, d = 256, 192, 32
+    dm = _dm(d, dev)
+    g = torch.Generator().manual_seed(21)
+    x = (torch.randn(b, N, d, generator=g) / math.sqrt(d)).to(dev).requires_grad_(True)
+    c = torch.randn(b, N, d, generator=g).to(dev)
+    with settings.num_likelihood_samples(1):
+        x_noisy, dist = dm.add_gp_noise(x)
+    assert tuple(x_noisy.shape) == (b, N, d)
+    hl = dm.deep_gp.hidden_layer
+    P = _layer_params(hl)
+    args = (P["Z"], P["ls"], P["s2"], P["w"], P["b0"], P["m"], P["s"])
+    X64 = x.detach().cpu().double().numpy()
+    ref = O.variational_forward(X64, *args, jitter=1e-4, dtype=np.float64)
+    W = dm.proj_up.weight.detach().cpu().double().numpy().reshape(-1)      # (d,) of Linear(1, d)
+    bias = dm.proj_up.bias.detach().cpu().double().numpy()
+    want = X64 + ref.mean[..., None] * W + bias                              # nn.Linear(1, d) + x
+    assert _rows_rel(x_noisy.detach().cpu(), want) <= TOL
+    (c * x_noisy).sum().backward()
+    c64 = c.cpu().double().numpy()
+    gmean = (c64 * W).sum(-1)                                                # d/d mean
+    gr = O.variational_grads(X64, *args, gmean, np.zeros_like(gmean), jitter=1e-4)
+    checks = {
+        "x": (x.grad, c64 + gr["X"]),
+        "proj_up.weight": (dm.proj_up.weight.grad.reshape(-1), (c64 * ref.mean[..., None]).sum((0, 1))),
+        "proj_up.bias": (dm.proj_up.bias.grad, c64.sum((0, 1))),
+        "Z": (hl.variational_strategy.inducing_points.grad, gr["Z"]),
+        "m": (hl.variational_strategy._variational_distribution.variational_mean.grad, gr["m"]),
+        "weights": (hl.mean_module.weights.grad.reshape(-1), gr["weights"]),
+        "bias": (hl.mean_module.bias.grad, gr["bias"]),
+    }
+    for k, (got, w_) in checks.items():
+        e = _rel(got.detach().cpu(), w_)
+        assert e <= TOL, (k, e)
+
+
+class _Half(nn.Module):
+    def forward(self, enc, dec):
+        return 0.5 * enc, 0.5 * dec
+
+
+def test_forward_gp_branch_vs_oracle(cuda_device):
+    """denoise_model_2.forward(enc, dec) with gp=True (denoise_model_2.py:42-59): both GP
+    calls, the backbone on the noisy inputs, dec_output = dec + dec_rec, and the dec dist
+    returned for the ELBO; forward and d/d(enc, dec) against the oracle."""
+    from fine_grained_gaussian_process_forcasting_amd import settings
+    dev = cuda_device
+    b, Ne, Nd, d = 32, 192, 96, 32
+    dm = _dm(d, dev, _Half())
+    g = torch.Generator().manual_seed(4)
+    enc = (torch.randn(b, Ne, d, generator=g) / math.sqrt(d)).to(dev).requires_grad_(True)
+    dec = (torch.randn(b, Nd, d, generator=g) / math.sqrt(d)).to(dev).requires_grad_(True)
+    with settings.num_likelihood_samples(1):
+        out, dist = dm(enc, dec)
+    hl = dm.deep_gp.hidden_layer
+    P = _layer_params(hl)
+    args = (P["Z"], P["ls"], P["s2"], P["w"], P["b0"], P["m"], P["s"])
+    D64 = dec.detach().cpu().double().numpy()
+    rd = O.variational_forward(D64, *args, jitter=1e-4, dtype=np.float64)
+    W = dm.proj_up.weight.detach().cpu().double().numpy().reshape(-1)
+    bias = dm.proj_up.bias.detach().cpu().double().numpy()
+    dec_noisy = D64 + rd.mean[..., None] * W + bias
+    want = D64 + 0.5 * dec_noisy
+    assert _rows_rel(out.detach().cpu(), want) <= TOL
+    assert _rows_rel(dist.mean[0].detach().cpu(), rd.mean) <= TOL
+    assert _rows_rel(dist.variance[0].detach().cpu(), rd.var) <= TOL
+    out.sum().backward()
+    # d out / d dec = 1 + 0.5 (1 + d(mean W)/d dec); enc does not reach out (only dec_rec does)
+    gr = O.variational_grads(D64, *args, 0.5 * np.full(rd.mean.shape, W.sum()), np.zeros_like(rd.mean),
+                             jitter=1e-4)
+    assert _rel(dec.grad.cpu(), 1.5 + gr["X"]) <= TOL
+    assert enc.grad is None or float(enc.grad.abs().max()) == 0.0

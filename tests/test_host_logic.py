@@ -172,7 +172,7 @@ def test_deferred_checks_record_during_capture_and_replay_verdicts(monkeypatch):
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
     with pytest.raises(RuntimeError, match="GraphedStep"):
         ops.check_cholesky_info(torch.tensor([0, -1], dtype=torch.int32), 1e-6)   # no recorder
-    rec = ops.DeferredChecks()
+    rec = ops.DeferredChecks(device="cpu")
     ops._RECORDERS.append(rec)
     try:
         info = torch.tensor([0, -2], dtype=torch.int32)
@@ -193,6 +193,23 @@ def test_deferred_checks_record_during_capture_and_replay_verdicts(monkeypatch):
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             rec.check()
+    # the sticky flag keeps a hard failure of a replay that was not checked itself
+    # (check_every > 1): recorded ops fold info > 0 into it
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    rec2 = ops.DeferredChecks(device="cpu")
+    ops._RECORDERS.append(rec2)
+    try:
+        info2 = torch.tensor([0, 2], dtype=torch.int32)
+        ops.check_cholesky_info(info2, 1e-6)
+    finally:
+        ops._RECORDERS.remove(rec2)
+    monkeypatch.undo()
+    info2.zero_()                        # the last replay of the block was fine ...
+    with pytest.raises(NotPSDError, match="rolled back"):
+        rec2.check()                     # ... but an earlier one failed
+    rec2.reset_sticky()
+    rec2.check()
 
 
 def test_graphed_step_requires_capturable_optimizer_and_device():
