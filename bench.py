@@ -225,8 +225,26 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
                               "unit": "TFLOP/s", "frac": adj_roof_s * B / (ms["bwd"] * 1e-3),
                               "flops_per_window": dict(zip(("fp32", "fp64"), var_adj_flops_per_window(N, M, D)))},
         "mean_ell": float(out.ell.double().mean()),
+        "elbo_rel_err_vs_fp64_oracle": elbo_rel_err(X, y, Z, ls, w, vm, vs, out.ell, D),
         "info": int(kz.info.item()),
     }
+
+
+def elbo_rel_err(X, y, Z, ls, w, vm, vs, ell_gpu, num_data, n=32):
+    """BASELINE's 'ELBO rel-err' on a window sample (outside every timed region): the
+    per-window ELBO of forecast_denoising.py:86-89 -- sum_i ELL_i / N - KL / num_data with
+    num_data = d -- from the kernel's ELL sums, against the fp64 oracle
+    (oracle.variational_forward + oracle.deep_elbo; parity unpinned vs GPyTorch itself)."""
+    from oracle import gp_oracle as O
+    idx = np.linspace(0, X.shape[0] - 1, min(n, X.shape[0])).astype(int)
+    N = X.shape[1]
+    m64, s64 = vm.cpu().double().numpy(), vs.cpu().double().numpy()
+    ref = O.variational_forward(X[idx].cpu().double().numpy(), Z.cpu().double().numpy(),
+                                ls.cpu().double().numpy(), LN2, w.cpu().double().numpy(), 0.1,
+                                m64, s64, jitter=1e-4, dtype=np.float64)
+    want = O.deep_elbo(y[idx].cpu().double().numpy(), ref.mean, ref.var, LN2 + 1e-4, m64, s64, num_data)
+    got = ell_gpu[idx].cpu().double().numpy() / N - O.kl_meanfield(m64, s64) / num_data
+    return float(np.max(np.abs(got - want) / np.abs(want)))
 
 
 def e2e_leg(steps=10):
@@ -341,6 +359,24 @@ def main():
                 "note": "128 windows occupy half of the 256 CUs: latency-bound by one window's chain"}
         assert bool((o2.info == 0).all())
 
+    # the per-rank share of a strong-scaled B=512 job at G = 2, 4, 8 GPUs, timed on this GPU
+    # (window sharding has no exchange on the step's path, so the G-GPU step time is the
+    # slowest rank's kernel time plus the one all-reduce at the end of the timed region)
+    strong_share = None
+    if rank == 0 and world == 1 and not args.strong and not args.no_cfg2:
+        strong_share = {"note": "per-rank share of a strong-scaled B=512 job timed on one GPU; "
+                                "implied G-GPU speed-up = t(512) / t(512/G)"}
+        for G in (2, 4, 8):
+            Bs = 512 // G
+            Xs_, ys_ = X[:Bs].contiguous(), y[:Bs].contiguous()
+            Ls_ = torch.empty(Bs, N, N, device=dev)
+            f = lambda: ops.exact_mll(Xs_, ys_, None, None, None, None, hyper=hyper, L_out=Ls_)  # noqa: E731
+            for _ in range(3):
+                f()
+            msG, _ = time_launches(f, 20)
+            strong_share[f"G{G}"] = {"windows_per_rank": Bs, "kernel_ms": msG,
+                                     "implied_speedup": kern_ms / msG if B == 512 else None}
+
     grad_ms = post_ms = None
     if not args.no_grad:
         fw = ops.exact_mll(X, y, None, None, None, None, hyper=hyper, want_L=True, want_z=True)
@@ -406,6 +442,9 @@ def main():
             line["cfg2"] = cfg2
         if var is not None:
             line["variational"] = var
+            line["elbo_rel_err_vs_fp64_oracle"] = var["elbo_rel_err_vs_fp64_oracle"]
+        if rank == 0 and strong_share is not None:
+            line["strong_share"] = strong_share
         if world == 1 and not args.no_e2e:
             line["e2e_step"] = e2e_leg()
         if world == 1 and not args.no_cpu_baseline:

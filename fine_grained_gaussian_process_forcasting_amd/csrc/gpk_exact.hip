@@ -44,6 +44,18 @@
 #ifndef GPK_SPLIT_UPDATE
 #define GPK_SPLIT_UPDATE 1
 #endif
+#ifndef GPK_EXACT_FLOW
+#define GPK_EXACT_FLOW 0  // 1: dataflow step order (TRSM -> counter -> hand-over -> bulk); 0: round-2 order
+#endif
+#ifndef GPK_EXACT_SMALLB
+#define GPK_EXACT_SMALLB 1   // B <= CUs: one window per CU with 16 waves (launch_exact_nb)
+#endif
+#ifndef GPK_TRSM_F16
+#define GPK_TRSM_F16 0   // 1: trailing-tile TRSM on split-f16 MFMA (measured 3 % slower: more spills); 0 = fp32 MFMA
+#endif
+#ifndef GPK_DIAG_DPP
+#define GPK_DIAG_DPP 1   // diagonal sweep as DPP-broadcast FMAs (gpk_diag_dpp.inc); 0 = readlane form
+#endif
 
 namespace {
 
@@ -252,6 +264,8 @@ GPK_DEVICE void diag_sweep(float (&v)[16]) {
   if constexpr (M < 15) diag_sweep<M + 1>(v);
 }
 
+#include "gpk_diag_dpp.inc"
+
 // Flag words (ints in LDS, monotone epochs -- nothing is ever reset within a
 // launch; epoch = 32 * attempt + k):
 enum : int {
@@ -296,7 +310,7 @@ GPK_DEVICE void publish_tile(float* dst, int lane, const f32x4 v, lds_vint* flag
 // Two independent 2-MFMA chains (80 cycles of dependent latency instead of 160).
 // Used by the worker TRSM and by the diagonal wave's look-ahead alike, so both
 // produce bit-identical panels.
-GPK_DEVICE f32x4 trsm_tile(const f32x4 q, const f32x4 t) {
+GPK_DEVICE f32x4 trsm_tile_f32(const f32x4 q, const f32x4 t) {
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
   f32x4 d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(q[0], t[0], z, 0, 0, 0);
   f32x4 d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(q[2], t[2], z, 0, 0, 0);
@@ -304,6 +318,49 @@ GPK_DEVICE f32x4 trsm_tile(const f32x4 q, const f32x4 t) {
   d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(q[3], t[3], d1, 0, 0, 0);
   return d0 + d1;
 }
+
+#if GPK_TRSM_F16
+// Split-f16 TRSM of a trailing tile (GPK_TRSM_F16=1): R_kj = W T with W = R_kk^{-T}
+// rounded to hi + lo f16 planes (after an exact 2^8 scale that puts its entries in the
+// normal f16 range) and T (|T_ij| <= 2^15: Schur-complement entries are bounded by the
+// diagonal, which the sigma^2 scaling puts below 2^15) rounded to hi + lo on the fly:
+//   A = {W_hi, W_hi} / {W_lo, W_lo},  B = {T_hi, T_lo}  (k-slots 8g..8g+3 <-> rows 4g..4g+3
+//   hi, 8g+4..8g+7 <-> the same rows lo: the acc layout IS the operand layout),
+// two mfma_f32_16x16x32_f16 = (W_hi + W_lo)(T_hi + T_lo) with every product exact:
+// 32 matrix-pipe cycles instead of the four 16x16x4 f32 MFMAs' 128. The rounding is the
+// same 22-bit split the panel tiles get (pan_store) right after.
+struct WOp {
+  half8_t hh, ll;
+};
+GPK_DEVICE WOp w_split(const f32x4 q) {
+  half4_t h, l;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float x = q[r] * 256.f;
+    h[r] = (_Float16)x;
+    l[r] = (_Float16)(x - (float)h[r]);
+  }
+  return WOp{half8_t{h[0], h[1], h[2], h[3], h[0], h[1], h[2], h[3]},
+             half8_t{l[0], l[1], l[2], l[3], l[0], l[1], l[2], l[3]}};
+}
+GPK_DEVICE f32x4 trsm_tile(const WOp& w, const f32x4 t) {
+  half4_t h, l;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    h[r] = (_Float16)t[r];
+    l[r] = (_Float16)(t[r] - (float)h[r]);
+  }
+  const half8_t b = {h[0], h[1], h[2], h[3], l[0], l[1], l[2], l[3]};
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.hh, b, z, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.ll, b, d, 0, 0, 0);
+  return d * (1.f / 256.f);
+}
+#else
+typedef f32x4 WOp;
+GPK_DEVICE WOp w_split(const f32x4 q) { return q; }
+GPK_DEVICE f32x4 trsm_tile(const WOp& w, const f32x4 t) { return trsm_tile_f32(w, t); }
+#endif
 
 GPK_DEVICE f32x4 load_w(const float* wb, int c, int grp) {
   f32x4 q;
@@ -403,7 +460,11 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
     t0 = t1;
     __builtin_amdgcn_sched_barrier(0);
   }
+#if GPK_DIAG_DPP
+  diag_sweep_dpp(v);
+#else
   diag_sweep<0>(v);
+#endif
   if constexpr (ST) {
     __builtin_amdgcn_sched_barrier(0);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -491,16 +552,22 @@ GPK_DEVICE f32x4 rbf_tile(const float* smem, const RbfK& k, int i, int j, int la
   const f32x4 nr = *(const f32x4*)&nrm[16 * i + 4 * grp];
   const int col = 16 * j + c;
   const float nc = nrm[col];
+  // first 32-column chunk peeled (D <= 32 is the whole Gram): its four operand loads
+  // go out together with the norms, one LDS round trip per tile
+  const half8_t al = x8[NB * 64 + i * 64 + lane], ah = x8[i * 64 + lane];
+  const half8_t bh = x8[j * 64 + lane], bl = x8[NB * 64 + j * 64 + lane];
   f32x4 g = {0.f, 0.f, 0.f, 0.f};
-  for (int dd = 0; dd < DC32; ++dd) {
+  g = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, g, 0, 0, 0);
+  g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, g, 0, 0, 0);
+  g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, g, 0, 0, 0);
+  for (int dd = 1; dd < DC32; ++dd) {
     const half8_t* xhv = x8 + (2 * dd) * NB * 64;
     const half8_t* xlv = x8 + (2 * dd + 1) * NB * 64;
-    const half8_t al = xlv[i * 64 + lane], bh = xhv[j * 64 + lane];
-    const half8_t ah = xhv[i * 64 + lane];
-    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, g, 0, 0, 0);
-    const half8_t bl = xlv[j * 64 + lane];
-    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, g, 0, 0, 0);
-    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, g, 0, 0, 0);
+    const half8_t al2 = xlv[i * 64 + lane], bh2 = xhv[j * 64 + lane];
+    const half8_t ah2 = xhv[i * 64 + lane], bl2 = xlv[j * 64 + lane];
+    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(al2, bh2, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah2, bh2, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah2, bl2, g, 0, 0, 0);
   }
   const float gm2 = k.gm2, s2 = k.s2, diagval = k.diagval;
   f32x4 o;
@@ -594,7 +661,197 @@ GPK_DEVICE void worker_sync(WorkerCtx& x) {
   worker_wait<WK>(x);
 }
 
-// One right-looking step K for the worker waves. The diagonal wave owns the
+// One right-looking step K for the worker waves (panel K is produced and applied in
+// the same step). The diagonal wave owns the diagonal tiles: at its step K it factors
+// (K,K), publishes R_KK^{-T}, and then -- look-ahead -- computes R_{K,K+1} itself and
+// applies that last update to (K+1,K+1), from the hand-over of (K,K+1) and (K+1,K+1)
+// through panel K-1. The workers, per step:
+//   1. wait for R_KK^{-T}, TRSM their tiles of block row K into panel K (+ z_K);
+//   2. count in / wait on the worker-only step counter: panel K is complete;
+//   3. hand over what the diagonal wave's NEXT look-ahead needs -- (K+1,K+2) and
+//      (K+2,K+2) updated through panel K -- FIRST (hbuf[(K+1) & 1], flags HA / HB);
+//   4. apply panel K to every other tile with i >= K+1 except (K+1,K+1) (the
+//      diagonal wave's), block row K+1 first: it is what the next TRSM reads;
+//   5. right-hand side (rw_i += R_{K,i}^T z_K), zero L's upper block row K, and the
+//      deferred RBF of block row K+3 (the Gram is additive; row K+3 is first read by
+//      the hand-over of step K+1).
+// Step K's hand-over is ready one TRSM + one counter after R_KK^{-T}, while the
+// diagonal wave runs its look-ahead and the whole factorisation of (K+1,K+1): the
+// bulk of step K overlaps that instead of sitting between the diagonal wave's steps.
+// Buffer reuse: panel K+2 overwrites panel K only after the step-(K+1) counter,
+// which every wave passes after finishing step K; hbuf[(K+1) & 1] is rewritten for
+// step K+2's hand-over only after R_{K+1,K+1}^{-T} exists, i.e. after the diagonal
+// wave has consumed it; wbuf[K & 1] is rewritten by the factor of (K+2,K+2), which
+// needs step K's hand-over, i.e. every worker past its step-K TRSM.
+// Returns nonzero when the diagonal wave reported a failed factorisation.
+template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL>
+GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
+  constexpr int Pk = plan_P<NB>(K);
+  constexpr bool LAST = (K == NB - 1);
+  constexpr bool HAND = (K + 2 < NB);                     // a look-ahead at diagonal step K+1
+  constexpr int TD = LAST ? -1 : plan_P<NB>(K + 1);       // (K+1, K+1): the diagonal wave's
+  constexpr int TA = HAND ? plan_P<NB>(K + 1) + 1 : -1;   // (K+1, K+2)
+  constexpr int TB = HAND ? plan_P<NB>(K + 2) : -1;       // (K+2, K+2)
+  // launder per step: keeps the per-slot plan loads / LDS addresses of this
+  // step from being hoisted (and pinned in registers) across all NB steps
+  const int wv = launder_s(x.wv);
+  const int e0 = launder_s(x.epoch0);
+  int lane = x.lane;
+  asm volatile("" : "+v"(lane));
+  const int c = lane & 15, grp = lane >> 4;
+  float* pcur = x.panel + (K & 1) * (NB + 1) * 256;                // panel K
+  float* hA = x.hbuf + ((K + 1) & 1) * 512;
+  if constexpr (ST) {
+    if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8] = __builtin_amdgcn_s_memtime();
+  }
+  // ---- 1. TRSM of the row-K off-diagonal tiles (P(K) < t <= P(K) + NB - K - 1) and,
+  // by the owner of RHS block row K, of the right-hand side: z_K.
+  // One LDS round trip in the usual case (the diagonal wave is ahead): the epoch flag, the
+  // failure word, R_KK^{-T} and 1/sigma are requested together. A wave's LDS reads are
+  // served in order, and the diagonal wave completes its R_KK^{-T} and failure-word writes
+  // before it releases the flag, so reads issued after a flag read that sees epoch K see
+  // them too (all volatile: the compiler keeps the order). Otherwise: wait, re-read.
+  const float* wbk = x.wbuf + (K & 1) * 256;
+  const int flag_now = x.vflag[kFlagFact];
+  int fail = x.vflag[kFlagFail + e0 / 32];
+  f32x4 q = load_w_v(wbk, c, grp);
+  // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
+  const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
+  if (flag_now < e0 + K) {
+    spin_until(x.vflag, kFlagFact, e0 + K);
+    fail = x.vflag[kFlagFail + e0 / 32];
+    q = load_w_v(wbk, c, grp);
+  }
+  GPK_WSTAMP(7, 1)  // wait for R_KK^{-T}
+  if (fail != 0) return 1;
+  const WOp wq = w_split(q);
+  const int rfirst = K + (((wv - K) % WK) + WK) % WK;   // this wave's first RHS block row >= K
+  {
+    constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
+    constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
+    constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
+    if constexpr (THI >= TLO) {
+      static_for_range<SLO, SHI>([&](auto I) {
+        constexpr int s = decltype(I)::value;
+        const int t = wv + WK * s;
+        if (t >= TLO && t <= THI) {
+          const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
+          const f32x4 rkj = pan_store(pcur + j * 256, lane, trsm_tile(wq, acc[s]));
+          // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
+          if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
+        }
+      });
+    }
+    if (rfirst == K) {
+      f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
+      if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 zk = pan_store(pcur + NB * 256, lane, trsm_tile_f32(q, d));   // (y unbounded: fp32)
+      if (c == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
+        if (x.zout != nullptr) {
+          const int row = 16 * K + 4 * grp;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (FULL || row + r < x.N) x.zout[(size_t)x.b * x.N + row + r] = zk[r];
+        }
+      }
+    }
+  }
+  GPK_WSTAMP(4, 2)  // TRSM
+  if constexpr (LAST) return 0;
+  // ---- 2. panel K complete
+  worker_sync<WK>(x);
+  GPK_WSTAMP(5, 3)  // step counter
+  // ---- 3. hand-over for the diagonal wave's look-ahead at step K+1
+  // (compile-time (i, j): no plan lookup, so nothing wave-specialised gets hoisted)
+  auto upd_ij = [&](f32x4& d, auto I, auto J) {
+    constexpr int i = decltype(I)::value, j = decltype(J)::value;
+    d = pan_mma(pan_load(pcur + i * 256, lane), pcur + j * 256, lane, d);
+  };
+  if constexpr (HAND) {
+    if (wv == TA % WK) {
+      upd_ij(acc[TA / WK], IC<K + 1>{}, IC<K + 2>{});
+      publish_tile(hA, lane, acc[TA / WK], x.vflag, kFlagHA, e0 + K + 1);
+    }
+    if (wv == TB % WK) {
+      upd_ij(acc[TB / WK], IC<K + 2>{}, IC<K + 2>{});
+      publish_tile(hA + 256, lane, acc[TB / WK], x.vflag, kFlagHB, e0 + K + 1);
+    }
+  }
+  GPK_WSTAMP(6, 4)  // hand-over
+  // ---- 4. trailing update from panel K over the other tiles with i >= K+1
+  // (t < P(K)), highest slot first (= block row K+1 first). Re-laundered: the
+  // hand-over branches above pin wv to a constant, and code tail-duplicated into
+  // them would turn plan lookups into constants hoisted out of the attempt loop.
+  {
+    const int wv = launder_s(x.wv);
+    auto upd = [&](f32x4& d, auto I) {
+      constexpr int s = decltype(I)::value;
+      const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(wv + WK * s);
+      d = pan_mma(pan_load(pcur + (p & 255) * 256, lane), pcur + (p >> 8) * 256, lane, d);
+    };
+    constexpr int NALL = Pk / WK;
+    auto bulk = [&](auto I) {
+      constexpr int s = decltype(I)::value;
+      bool sk = false;
+      if constexpr (s == TD / WK) sk = sk || (wv == TD % WK);
+      if constexpr (HAND && s == TA / WK) sk = sk || (wv == TA % WK);
+      if constexpr (HAND && s == TB / WK) sk = sk || (wv == TB % WK);
+      if (!sk) upd(acc[s], I);
+    };
+    if constexpr (NALL < SLOTS && (Pk % WK) != 0) {
+      if (wv < Pk % WK) bulk(IC<NALL>{});
+    }
+    static_for_desc<NALL>(bulk);
+  }
+  GPK_WSTAMP(2, 5)  // trailing update
+  // ---- 5. right-hand side rows i >= K+1 owned by this wave: rw_i += R_{K,i}^T z_K
+  // (rw holds -(y - c); only column 0 of the tile is live, so it round-trips
+  // through LDS on the c == 0 lanes)
+  for (int i = rfirst == K ? K + WK : rfirst; i < NB; i += WK) {
+    f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
+    if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+    d = pan_mma(pan_load(pcur + i * 256, lane), pcur + NB * 256, lane, d);
+    if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
+  }
+  // zero L's strictly-upper part of block-row K (streams out behind the MFMAs)
+  if (x.Lb != nullptr) {
+    const int N = FULL ? 16 * NB : x.N;
+    const int c0 = 16 * (K + 1);
+    for (int qq = wv; qq < 16; qq += WK) {
+      const int row = 16 * K + qq;
+      if (row < N) {
+        if ((N & 3) == 0) {
+          for (int cc = c0 + 4 * lane; cc < N; cc += 256)
+            *(f32x4*)&x.Lb[(size_t)row * N + cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+          for (int cc = c0 + lane; cc < N; cc += 64) x.Lb[(size_t)row * N + cc] = 0.f;
+        }
+      }
+    }
+  }
+  // deferred RBF of block row K+3 (its tiles are first read by step K+1's hand-over)
+  if constexpr (K + 3 < NB) {
+    constexpr int RLO = plan_P<NB>(K + 3), RHI = plan_P<NB>(K + 2) - 1;
+    constexpr int SLO = RLO / WK;
+    constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
+    const RbfK rk = read_rbfk(x.smem + x.rbfc);
+    static_for_range<SLO, SHI>([&](auto I) {
+      constexpr int s = decltype(I)::value;
+      const int t = wv + WK * s;
+      if (t >= RLO && t <= RHI) {
+        const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(t);
+        acc[s] += rbf_tile<NB, FULL>(x.smem, rk, p & 255, p >> 8, lane, x.N);
+      }
+    });
+  }
+  GPK_WSTAMP(3, 6)  // RHS + zero-L + deferred RBF
+  return 0;
+}
+
+// GPK_EXACT_FLOW=0: the round-2 step order (panel K-1 applied at step K, split-phase
+// worker barrier at the end). One right-looking step K for the worker waves. The diagonal wave owns the
 // diagonal tiles from the moment they are handed over: at step K it factors
 // (K,K), computes R_{K,K+1} itself and applies that last update to (K+1,K+1)
 // (look-ahead), so the workers
@@ -611,7 +868,7 @@ GPK_DEVICE void worker_sync(WorkerCtx& x) {
 //      imbalance; measured 5-7 % per launch over a plain barrier after 4.).
 // Returns nonzero when the diagonal wave reported a failed factorisation.
 template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL>
-GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
+GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   constexpr int Pk = plan_P<NB>(K);
   constexpr bool LAST = (K == NB - 1);
   constexpr int TD = Pk;                                  // (K, K): the diagonal wave's
@@ -722,6 +979,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
   if (fail != 0) return 1;
+  const WOp wq = w_split(q);
   constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
   constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
   constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
@@ -732,7 +990,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
         const int t = wv + WK * s;
         if (t >= TLO && t <= THI) {
           const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
-          const f32x4 rkj = pan_store(pcur + j * 256, lane, trsm_tile(q, acc[s]));
+          const f32x4 rkj = pan_store(pcur + j * 256, lane, trsm_tile(wq, acc[s]));
           // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
           if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
         }
@@ -741,7 +999,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     if (rfirst == K) {
       f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 zk = pan_store(pcur + NB * 256, lane, trsm_tile(q, d));
+      const f32x4 zk = pan_store(pcur + NB * 256, lane, trsm_tile_f32(q, d));   // (y unbounded: fp32)
       if (c == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
@@ -782,15 +1040,22 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
 template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL>
 GPK_DEVICE int worker_steps(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   if constexpr (K < NB) {
+#if GPK_EXACT_FLOW
     if (worker_step<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
+#else
+    if (worker_step_split<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
+#endif
     return worker_steps<NB, WK, SLOTS, K + 1, ST, FULL>(acc, x);
   } else {
     return 0;
   }
 }
 
-template <int NB, int W, bool STAMPS, bool FULL>
-__global__ void __launch_bounds__(64 * W, (2 * W) / 4)
+// OCC = workgroups per CU the register budget is sized for: 2 (the B >= 2 x CUs
+// layout, two windows per CU) or 1 (small batches: one window per CU with W = 16
+// waves, twice the workers per window -- launch_exact_nb).
+template <int NB, int W, bool STAMPS, bool FULL, int OCC = 2>
+__global__ void __launch_bounds__(64 * W, (OCC * W) / 4)
 gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
                  const float* __restrict__ hyp, int n_ls, int N_in, int D, int DC,
                  double jitter0, int max_tries, float* __restrict__ Lout,
@@ -860,112 +1125,114 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   const float* Xb = X + (size_t)b * N * D;
   float* Lb = Lout ? Lout + (size_t)b * N * N : nullptr;
 
-  // ---- 1. stage X / l into LDS in fragment layout (zero padded) ----------
-  // Each thread owns 16-column chunks of rows; all of its global loads are
-  // issued before any is consumed.
-  {
-    const int chunks = NP * DC;  // (row, 16-col chunk) pairs
-    float mx = 0.f;              // max |x / l| (bounds the centred values for the f16 split)
-    // x / l as x * (1 / l): one uniform division (GPyTorch divides; the <= 1 ulp
-    // difference is far inside the 1e-4 parity bound)
-    const float inv_l0 = 1.f / hyp[3];
-    for (int base = 0; base < chunks; base += T) {
-      const int q = base + tid;
-      float v[16];
-      const int n = q / DC, dd = q - n * DC;
-      if (q < chunks) {
-        const int d0 = dd * 16;
-        if (n < N && (D & 3) == 0 && d0 + 16 <= D) {
+  // Fast prologue (DC in {1, 2, 4} and one (row, 16-column chunk) item per thread, e.g.
+  // N=256 D=32): X stays in registers from the load to the f16 images -- column sums by a
+  // register butterfly (permlane32 / permlane16 swaps, DPP) and one LDS partial per wave,
+  // the y load issued with the X loads. Otherwise the staged path below.
+  const bool fast = (DC == 1 || DC == 2 || DC == 4) && NP * DC <= T;
+  if (fast) {
+    const int q = tid;
+    const int n = q / DC, dd = q & (DC - 1), d0 = 16 * dd;
+    const bool live = q < NP * DC;
+    float v[16];
+    float yv = 0.f;
+    if (live && dd == 0 && n < N) yv = y[(size_t)b * N + n];
+    if (live && n < N && (D & 3) == 0 && d0 + 16 <= D) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const f32x4 t = *(const f32x4*)&Xb[(size_t)n * D + d0 + 4 * u];
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 t = *(const f32x4*)&Xb[(size_t)n * D + d0 + 4 * u];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[4 * u + r] = t[r];
-          }
-        } else {
-          // ragged: clamped unconditional loads (all 16 in flight), masked afterwards
-#pragma unroll
-          for (int e = 0; e < 16; ++e) v[e] = Xb[(n < N && d0 + e < D) ? (size_t)n * D + d0 + e : 0];
-#pragma unroll
-          for (int e = 0; e < 16; ++e)
-            if (!(n < N && d0 + e < D)) v[e] = 0.f;
-        }
-        if (n_ls == 1) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) v[e] *= inv_l0;
-        } else {
-          float l[16];
-#pragma unroll
-          for (int e = 0; e < 16; ++e) l[e] = hyp[3 + (d0 + e < D ? d0 + e : 0)];
-#pragma unroll
-          for (int e = 0; e < 16; ++e)
-            if (d0 + e < D) v[e] = v[e] / l[e];
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) mx = __builtin_fmaxf(mx, __builtin_fabsf(v[e]));
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          *(f32x4*)&xf[frag_index(n, d0 + 4 * u, NB)] = f32x4{v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]};
+        for (int r = 0; r < 4; ++r) v[4 * u + r] = t[r];
       }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = Xb[(live && n < N && d0 + e < D) ? (size_t)n * D + d0 + e : 0];
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (!(live && n < N && d0 + e < D)) v[e] = 0.f;
     }
+    if (n_ls == 1) {
+      const float inv_l0 = 1.f / hyp[3];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] *= inv_l0;
+    } else {
+      float l[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) l[e] = hyp[3 + (d0 + e < D ? d0 + e : 0)];
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (d0 + e < D) v[e] = v[e] / l[e];
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) mx = __builtin_fmaxf(mx, __builtin_fabsf(v[e]));
     mx = wave_max_dpp(mx);
     if (lane == 0) red[wave] = mx;
-  }
-  barrier_lds();
-  GPK_STAMP(8)  // X loads + fp32 staging + max
-  if (tid == 0) {
-    flag[0] = 0;
-    flag[kFlagT00] = -1;
-    flag[kFlagFact] = -1;
-    for (int q = 3; q < 16; ++q) flag[q] = 0;
-    flag[kFlagHA] = -1;
-    flag[kFlagHB] = -1;
-    flag[kFlagSync] = 0;
-    flag[kFlagTmo] = 0;
-    flag[kFlagInvSigma] = __builtin_bit_cast(int, inv_sigma);  // read back per step (SGPR budget)
-    smem[lay.rbfc + 1] = s2;
-    ((int*)smem)[lay.rbfc + 3] = lay.nrm | (((DC + 1) / 2) << 20);
-    if constexpr (STAMPS) {
-      ((unsigned long long*)(red + 4 * W + 24))[0] = 0;
-      ((unsigned long long*)(red + 4 * W + 26))[0] = 0;
-      ((unsigned long long*)(red + 4 * W + 28))[0] = 0;
-      for (int q = 0; q < 3; ++q) ((unsigned long long*)(red + 4 * W + 32))[q] = 0;
-    }
-  }
-  // ---- 2. centre columns by the mean over the N real rows (GPyTorch _sq_dist)
-  {
-    const int parts = T / DP;
-    const int part = tid / DP, d = tid - part * DP;
-    if (part < parts) {
-      float sacc[4] = {0.f, 0.f, 0.f, 0.f};
-      int n = part;
-      for (; n + 3 * parts < N; n += 4 * parts) {
+    // column sums of this wave's rows: reduce-scatter over lane bits 5, 4, 3, then plain
+    // DPP adds over the lane bits that hold other rows of the same chunk
+    float s8[8], t4[4], u2[2];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) sacc[u] += xf[frag_index(n + u * parts, d, NB)];
+    for (int i = 0; i < 8; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[i]), __builtin_bit_cast(int, v[i + 8]),
+                                                      false, false);
+      s8[i] = __builtin_bit_cast(float, (int)r[0]) + __builtin_bit_cast(float, (int)r[1]);  // col i + 8 b5
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, s8[i]), __builtin_bit_cast(int, s8[i + 4]),
+                                                      false, false);
+      t4[i] = __builtin_bit_cast(float, (int)r[0]) + __builtin_bit_cast(float, (int)r[1]);  // + 4 b4
+    }
+    const bool b3 = (lane >> 3) & 1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float keep = b3 ? t4[i + 2] : t4[i];
+      const float send = b3 ? t4[i] : t4[i + 2];
+      u2[i] = keep + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x128, 0xf, 0xf, false));
+      if (DC == 1)
+        u2[i] += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, u2[i]), 0xB1, 0xf, 0xf, false));
+      if (DC <= 2)
+        u2[i] += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, u2[i]), 0x4E, 0xf, 0xf, false));
+    }
+    // partials: xf[col * 2W + 2 * wave + bit2] (the image area is free until the barrier
+    // after the mean)
+    const bool writer = DC == 1 ? (lane & 3) == 0 : (DC == 2 ? (lane & 2) == 0 : true);
+    if (writer) {
+      const int cc = 2 * ((lane >> 3) & 1) + 4 * ((lane >> 4) & 1) + 8 * ((lane >> 5) & 1);
+      const int col = 16 * (lane & (DC - 1)) + cc;
+      const int slot = 2 * wave + ((lane >> 2) & 1);
+      xf[col * 2 * W + slot] = u2[0];
+      xf[(col + 1) * 2 * W + slot] = u2[1];
+    }
+    barrier_lds();
+    GPK_STAMP(8)
+    if (tid == 0) {
+      flag[0] = 0;
+      flag[kFlagT00] = -1;
+      flag[kFlagFact] = -1;
+      for (int qq = 3; qq < 16; ++qq) flag[qq] = 0;
+      flag[kFlagHA] = -1;
+      flag[kFlagHB] = -1;
+      flag[kFlagSync] = 0;
+      flag[kFlagTmo] = 0;
+      flag[kFlagInvSigma] = __builtin_bit_cast(int, inv_sigma);
+      smem[lay.rbfc + 1] = s2;
+      ((int*)smem)[lay.rbfc + 3] = lay.nrm | (((DC + 1) / 2) << 20);
+      if constexpr (STAMPS) {
+        ((unsigned long long*)(red + 4 * W + 24))[0] = 0;
+        ((unsigned long long*)(red + 4 * W + 26))[0] = 0;
+        ((unsigned long long*)(red + 4 * W + 28))[0] = 0;
+        for (int qq = 0; qq < 3; ++qq) ((unsigned long long*)(red + 4 * W + 32))[qq] = 0;
       }
-      for (; n < N; n += parts) sacc[0] += xf[frag_index(n, d, NB)];
-      cpart[part * DP + d] = (sacc[0] + sacc[1]) + (sacc[2] + sacc[3]);
     }
-    barrier_lds();
-    GPK_STAMP(9)  // column partial sums
     if (tid < DP) {
-      float s = 0.f;
-      for (int p = 0; p < parts; ++p) s += cpart[p * DP + tid];
-      cpart[64 * W + tid] = s / (float)N;
+      float sum = 0.f;
+      for (int w = 0; w < 2 * W; w += 4) {
+        const f32x4 p4 = *(const f32x4*)&xf[tid * 2 * W + w];
+        sum += (p4[0] + p4[1]) + (p4[2] + p4[3]);
+      }
+      cpart[64 * W + tid] = sum / (float)N;
     }
-    barrier_lds();
-    GPK_STAMP(10)  // mean
-  }
-  // ---- 3. subtract the mean, squared norms, residual r = y - c -----------
-  // The centred rows are split into f16 hi + lo parts (x = hi + lo + O(2^-22 x))
-  // for the 3-pass f16 MFMA Gram; the images overwrite the
-  // fp32 staging chunk pair they were read from (read all -> barrier -> write).
-  {
-    const float* cmean_d = cpart + 64 * W;
-    _Float16* xh16 = (_Float16*)(smem + lay.xf);
-    // power-of-two scale 2^a for the f16 images: |x - mean| <= 2 max|x| < 2^(e+1)
-    // -> scaled magnitudes < 2^14 (f16 max 65504), lo parts normal down to 2^-2.
-    // The Gram comes back times 2^(2a) and is rescaled exactly in the RBF.
     int a_sc = 0;
     {
       float m = 0.f;
@@ -977,49 +1244,211 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     }
     const float xsc = __builtin_ldexpf(1.f, a_sc);
     if (tid == 0) smem[lay.rbfc] = __builtin_ldexpf(-2.f, -2 * a_sc);
-    const int DC32 = (DC + 1) / 2;
-    const int n = tid;  // NP <= 256 <= T: one row per thread
-    float s = 0.f;
-    for (int q = 0; q < DC32; ++q) {
-      float v[32];
+    barrier_lds();
+    GPK_STAMP(10)
+    // centre, squared norms, split into f16 hi + lo images (hfrag layout)
+    float sq = 0.f;
+    if (live && n < N) {
+      const float* cm = cpart + 64 * W + d0;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int d0 = 32 * q + 4 * u;
-        f32x4 t = {0.f, 0.f, 0.f, 0.f};
-        if (n < NP && d0 < 16 * DC) {
-          t = *(const f32x4*)&xf[frag_index(n, d0, NB)];
-          if (n < N) {
-            const f32x4 m4 = *(const f32x4*)&cmean_d[d0];
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 m4 = *(const f32x4*)&cm[4 * u];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) t[r] = (d0 + r < D) ? t[r] - m4[r] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[4 * u + r] = t[r];
+        for (int r = 0; r < 4; ++r) v[4 * u + r] = (d0 + 4 * u + r < D) ? v[4 * u + r] - m4[r] : 0.f;
       }
-      barrier_lds();
-      if (n < NP) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          half4_t hi, lo;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float t = v[4 * u + r];
-            s = __builtin_fmaf(t, t, s);
-            const float ts = t * xsc;
-            hi[r] = (_Float16)ts;
-            lo[r] = (_Float16)(ts - (float)hi[r]);
-          }
-          *(half4_t*)&xh16[hfrag_index(n, 32 * q + 4 * u, NB, 0)] = hi;
-          *(half4_t*)&xh16[hfrag_index(n, 32 * q + 4 * u, NB, 1)] = lo;
-        }
-      }
-      barrier_lds();
-      GPK_STAMP(11)  // centre + f16 split (per 32-col chunk)
     }
-    if (n < NP) {
-      nrm[n] = s;
-      rv[n] = (n < N) ? (y[(size_t)b * N + n] - cmean) * sigma : 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sq = __builtin_fmaf(v[e], v[e], sq);
+    if (DC >= 2)
+      sq += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sq), 0xB1, 0xf, 0xf, false));
+    if (DC >= 4)
+      sq += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sq), 0x4E, 0xf, 0xf, false));
+    if (live) {
+      _Float16* xh16 = (_Float16*)(smem + lay.xf);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        half8_t hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float ts = v[8 * h + j] * xsc;
+          hi[j] = (_Float16)ts;
+          lo[j] = (_Float16)(ts - (float)hi[j]);
+        }
+        *(half8_t*)&xh16[hfrag_index(n, d0 + 8 * h, NB, 0)] = hi;
+        *(half8_t*)&xh16[hfrag_index(n, d0 + 8 * h, NB, 1)] = lo;
+        if (DC == 1) {   // columns 16-31 of the 32-column image chunk are padding
+          const half8_t z = {};
+          *(half8_t*)&xh16[hfrag_index(n, 16 + 8 * h, NB, 0)] = z;
+          *(half8_t*)&xh16[hfrag_index(n, 16 + 8 * h, NB, 1)] = z;
+        }
+      }
+      if (dd == 0) {
+        nrm[n] = sq;
+        rv[n] = (n < N) ? (yv - cmean) * sigma : 0.f;
+      }
+    }
+  } else {
+    // ---- 1. stage X / l into LDS in fragment layout (zero padded) ----------
+    // Each thread owns 16-column chunks of rows; all of its global loads are
+    // issued before any is consumed.
+    {
+      const int chunks = NP * DC;  // (row, 16-col chunk) pairs
+      float mx = 0.f;              // max |x / l| (bounds the centred values for the f16 split)
+      // x / l as x * (1 / l): one uniform division (GPyTorch divides; the <= 1 ulp
+      // difference is far inside the 1e-4 parity bound)
+      const float inv_l0 = 1.f / hyp[3];
+      for (int base = 0; base < chunks; base += T) {
+        const int q = base + tid;
+        float v[16];
+        const int n = q / DC, dd = q - n * DC;
+        if (q < chunks) {
+          const int d0 = dd * 16;
+          if (n < N && (D & 3) == 0 && d0 + 16 <= D) {
+  #pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const f32x4 t = *(const f32x4*)&Xb[(size_t)n * D + d0 + 4 * u];
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) v[4 * u + r] = t[r];
+            }
+          } else {
+            // ragged: clamped unconditional loads (all 16 in flight), masked afterwards
+  #pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] = Xb[(n < N && d0 + e < D) ? (size_t)n * D + d0 + e : 0];
+  #pragma unroll
+            for (int e = 0; e < 16; ++e)
+              if (!(n < N && d0 + e < D)) v[e] = 0.f;
+          }
+          if (n_ls == 1) {
+  #pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] *= inv_l0;
+          } else {
+            float l[16];
+  #pragma unroll
+            for (int e = 0; e < 16; ++e) l[e] = hyp[3 + (d0 + e < D ? d0 + e : 0)];
+  #pragma unroll
+            for (int e = 0; e < 16; ++e)
+              if (d0 + e < D) v[e] = v[e] / l[e];
+          }
+  #pragma unroll
+          for (int e = 0; e < 16; ++e) mx = __builtin_fmaxf(mx, __builtin_fabsf(v[e]));
+  #pragma unroll
+          for (int u = 0; u < 4; ++u)
+            *(f32x4*)&xf[frag_index(n, d0 + 4 * u, NB)] = f32x4{v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]};
+        }
+      }
+      mx = wave_max_dpp(mx);
+      if (lane == 0) red[wave] = mx;
+    }
+    barrier_lds();
+    GPK_STAMP(8)  // X loads + fp32 staging + max
+    if (tid == 0) {
+      flag[0] = 0;
+      flag[kFlagT00] = -1;
+      flag[kFlagFact] = -1;
+      for (int q = 3; q < 16; ++q) flag[q] = 0;
+      flag[kFlagHA] = -1;
+      flag[kFlagHB] = -1;
+      flag[kFlagSync] = 0;
+      flag[kFlagTmo] = 0;
+      flag[kFlagInvSigma] = __builtin_bit_cast(int, inv_sigma);  // read back per step (SGPR budget)
+      smem[lay.rbfc + 1] = s2;
+      ((int*)smem)[lay.rbfc + 3] = lay.nrm | (((DC + 1) / 2) << 20);
+      if constexpr (STAMPS) {
+        ((unsigned long long*)(red + 4 * W + 24))[0] = 0;
+        ((unsigned long long*)(red + 4 * W + 26))[0] = 0;
+        ((unsigned long long*)(red + 4 * W + 28))[0] = 0;
+        for (int q = 0; q < 3; ++q) ((unsigned long long*)(red + 4 * W + 32))[q] = 0;
+      }
+    }
+    // ---- 2. centre columns by the mean over the N real rows (GPyTorch _sq_dist)
+    {
+      const int parts = T / DP;
+      const int part = tid / DP, d = tid - part * DP;
+      if (part < parts) {
+        float sacc[4] = {0.f, 0.f, 0.f, 0.f};
+        int n = part;
+        for (; n + 3 * parts < N; n += 4 * parts) {
+  #pragma unroll
+          for (int u = 0; u < 4; ++u) sacc[u] += xf[frag_index(n + u * parts, d, NB)];
+        }
+        for (; n < N; n += parts) sacc[0] += xf[frag_index(n, d, NB)];
+        cpart[part * DP + d] = (sacc[0] + sacc[1]) + (sacc[2] + sacc[3]);
+      }
+      barrier_lds();
+      GPK_STAMP(9)  // column partial sums
+      if (tid < DP) {
+        float s = 0.f;
+        for (int p = 0; p < parts; ++p) s += cpart[p * DP + tid];
+        cpart[64 * W + tid] = s / (float)N;
+      }
+      barrier_lds();
+      GPK_STAMP(10)  // mean
+    }
+    // ---- 3. subtract the mean, squared norms, residual r = y - c -----------
+    // The centred rows are split into f16 hi + lo parts (x = hi + lo + O(2^-22 x))
+    // for the 3-pass f16 MFMA Gram; the images overwrite the
+    // fp32 staging chunk pair they were read from (read all -> barrier -> write).
+    {
+      const float* cmean_d = cpart + 64 * W;
+      _Float16* xh16 = (_Float16*)(smem + lay.xf);
+      // power-of-two scale 2^a for the f16 images: |x - mean| <= 2 max|x| < 2^(e+1)
+      // -> scaled magnitudes < 2^14 (f16 max 65504), lo parts normal down to 2^-2.
+      // The Gram comes back times 2^(2a) and is rescaled exactly in the RBF.
+      int a_sc = 0;
+      {
+        float m = 0.f;
+        for (int w = 0; w < W; ++w) m = __builtin_fmaxf(m, red[w]);
+        int e = 0;
+        if (m > 0.f && m < __builtin_huge_valf()) (void)__builtin_frexpf(m, &e);
+        a_sc = 13 - e;
+        a_sc = a_sc > 100 ? 100 : (a_sc < -100 ? -100 : a_sc);
+      }
+      const float xsc = __builtin_ldexpf(1.f, a_sc);
+      if (tid == 0) smem[lay.rbfc] = __builtin_ldexpf(-2.f, -2 * a_sc);
+      const int DC32 = (DC + 1) / 2;
+      const int n = tid;  // NP <= 256 <= T: one row per thread
+      float s = 0.f;
+      for (int q = 0; q < DC32; ++q) {
+        float v[32];
+  #pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int d0 = 32 * q + 4 * u;
+          f32x4 t = {0.f, 0.f, 0.f, 0.f};
+          if (n < NP && d0 < 16 * DC) {
+            t = *(const f32x4*)&xf[frag_index(n, d0, NB)];
+            if (n < N) {
+              const f32x4 m4 = *(const f32x4*)&cmean_d[d0];
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) t[r] = (d0 + r < D) ? t[r] - m4[r] : 0.f;
+            }
+          }
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) v[4 * u + r] = t[r];
+        }
+        barrier_lds();
+        if (n < NP) {
+  #pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            half4_t hi, lo;
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float t = v[4 * u + r];
+              s = __builtin_fmaf(t, t, s);
+              const float ts = t * xsc;
+              hi[r] = (_Float16)ts;
+              lo[r] = (_Float16)(ts - (float)hi[r]);
+            }
+            *(half4_t*)&xh16[hfrag_index(n, 32 * q + 4 * u, NB, 0)] = hi;
+            *(half4_t*)&xh16[hfrag_index(n, 32 * q + 4 * u, NB, 1)] = lo;
+          }
+        }
+        barrier_lds();
+        GPK_STAMP(11)  // centre + f16 split (per 32-col chunk)
+      }
+      if (n < NP) {
+        nrm[n] = s;
+        rv[n] = (n < N) ? (y[(size_t)b * N + n] - cmean) * sigma : 0.f;
+      }
     }
   }
   barrier_lds();
@@ -1089,7 +1518,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         const f32x4 q = load_w(wb, c, grp);
         const f32x4 ta = *(const f32x4*)&hk[lane * 4];
         f32x4 tb = *(const f32x4*)&hk[256 + lane * 4];
-        tb = pan_self(trsm_tile(q, ta), tb);
+        tb = pan_self(trsm_tile(w_split(q), ta), tb);
         *(f32x4*)&dsc[lane * 4] = tb;
         if constexpr (STAMPS) {
           const unsigned long long hw2 = __builtin_amdgcn_s_memtime();
@@ -1124,7 +1553,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       // right-hand side: this wave's block rows of rw <- -(y - c) (fresh per attempt)
       for (int i = wave; i < NB; i += WK)
         if (lane < 16) rw[16 * i + lane] = -rv[16 * i + lane];
-      // ---- 4. RBF of block rows 0 and 1 (the rest is deferred into the
+      // ---- 4. RBF of block rows 0-2 (the rest is deferred into the
       // factorisation steps); the owners of (0,0), (0,1), (1,1) build and hand
       // those over first, so the diagonal wave starts right away.
       {
@@ -1136,6 +1565,8 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         const RbfK rk = read_rbfk(smem + lay.rbfc);
         constexpr int P0 = plan_P<NB>(0);
         constexpr int P1 = NB > 1 ? plan_P<NB>(1) : 0;
+        // rows 0-2 now and row k+3 at step k (FLOW), rows 0-1 and row k+2 (split order)
+        constexpr int P2 = GPK_EXACT_FLOW ? (NB > 2 ? plan_P<NB>(2) : 0) : P1;
         constexpr int T01 = P0 + 1;
         const int e0 = 32 * attempt;
         if (wv == P0 % WK) {
@@ -1161,7 +1592,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
             if constexpr (NB > 1 && s == T01 / WK) sk = sk || (wv == T01 % WK);
             if constexpr (NB > 1 && s == P1 / WK) sk = sk || (wv == P1 % WK);
             if (!sk) {
-              if (t >= P1) {
+              if (t >= P2) {
                 const int pk = plan_tile<NB, WK * s, WK * s + WK - 1>(t);
                 acc[s] = rbf_tile<NB, FULL>(smem, rk, pk & 255, pk >> 8, lane, N);
               } else {
@@ -1230,22 +1661,43 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   }
 }
 
-template <int NB, bool STAMPS, bool FULL>
-int launch_exact_nb(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
-  constexpr int W = NB >= 12 ? GPK_EXACT_WBIG : (NB >= 6 ? 8 : 4);
+template <int NB, int W, bool STAMPS, bool FULL, int OCC>
+int launch_exact_w(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
   const int DC = (a.D + 15) / 16;
   const ExactLds lay = exact_lds_layout(NB, DC, W);
   const size_t lds = (size_t)lay.total * sizeof(float);
   if (DC * 16 > 64 * W || DC * 16 > 256) return -7;
   if (lds > 160 * 1024) return -7;
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)gpk_exact_kernel<NB, W, STAMPS, FULL>,
+    (void)hipFuncSetAttribute((const void*)gpk_exact_kernel<NB, W, STAMPS, FULL, OCC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((gpk_exact_kernel<NB, W, STAMPS, FULL>), dim3(a.B), dim3(64 * W), lds, stream,
+  hipLaunchKernelGGL((gpk_exact_kernel<NB, W, STAMPS, FULL, OCC>), dim3(a.B), dim3(64 * W), lds, stream,
                      a.X, a.y, a.hyp, a.n_ls, a.N, a.D, DC, a.jitter, a.max_tries,
                      a.L, a.z, a.mll, a.info, stamps);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
+}
+
+// Compute units of the current device (for the small-batch layout choice).
+int device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
+  return n;
+}
+
+template <int NB, bool STAMPS, bool FULL>
+int launch_exact_nb(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
+  constexpr int W = NB >= 12 ? GPK_EXACT_WBIG : (NB >= 6 ? 8 : 4);
+#if GPK_EXACT_SMALLB
+  // Small batches (B <= CUs: BASELINE configs[1], the strong-scaled per-GPU share of
+  // configs[3]): a window's latency IS the launch time, and half the CUs would idle at
+  // two windows per CU; one window per CU with 16 waves gives each window 15 workers.
+  if constexpr (!STAMPS && NB >= 6) {
+    if (a.B <= device_cus()) return launch_exact_w<NB, 16, STAMPS, FULL, 1>(a, stamps, stream);
+  }
+#endif
+  return launch_exact_w<NB, W, STAMPS, FULL, 2>(a, stamps, stream);
 }
 
 template <int NB>

@@ -87,12 +87,20 @@ def traffic_like_frame(n_ids, n_per, nin, seed=0):
     return pd.DataFrame(cols)
 
 
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 class _T:
     def __init__(self, name):
         self.name = name
 
 
-def run(cfg, steps, modes=("eager", "graph"), gps=(True, False)):
+def run(cfg, steps, modes=("eager", "graph", "eager_anomaly"), gps=(True, False)):
     dev = torch.device("cuda:0")
     b, nin = (256, 4) if cfg == "cfg3" else (32, 5)
     n_enc, pred_len, d = 192, 96, 32
@@ -110,8 +118,11 @@ def run(cfg, steps, modes=("eager", "graph"), gps=(True, False)):
             # capturable=True in both modes, so the two time the same Adam arithmetic
             opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.98), eps=1e-9,
                                    capturable=True)
-            with settings.num_likelihood_samples(1):
-                if mode == "eager":
+            # eager_anomaly: the reference's global torch.autograd.set_detect_anomaly(True)
+            # (train.py:18, forecast_denoising.py:11; SURVEY B7 / §8d cfg 3 "off and on")
+            anomaly = torch.autograd.detect_anomaly() if mode == "eager_anomaly" else _Null()
+            with settings.num_likelihood_samples(1), anomaly:
+                if mode in ("eager", "eager_anomaly"):
                     def step(k):
                         enc, dec, y = batches[k % len(batches)]
                         loss = model(enc, dec, y)
@@ -140,7 +151,8 @@ def run(cfg, steps, modes=("eager", "graph"), gps=(True, False)):
         res[mode] = r
     res["config"] = {"cfg": cfg, "b": b, "enc": n_enc, "dec": pred_len, "d_model": d, "M": 256,
                      "backbone": "torch.nn.Transformer stand-in (d 32, 8 heads, d_ff 128, 1 layer)",
-                     "anomaly_mode": False, "input": "GPU-resident window sampler"}
+                     "anomaly_mode": {m: m == "eager_anomaly" for m in modes},
+                     "input": "GPU-resident window sampler"}
     return res
 
 

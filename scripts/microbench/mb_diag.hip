@@ -69,7 +69,8 @@ __global__ void __launch_bounds__(1024) kdiag(const float* in, float* out, unsig
       float w[16];
       for (int i = 0; i < 16; ++i) w[i] = v[i];
       if constexpr (SWEEP == 0) diag_sweep<0>(w);
-      else mbd::dsweep<0>(w);
+      else if constexpr (SWEEP == 1) mbd::dsweep<0>(w);
+      else diag_sweep_dpp(w);
       v[0] += w[15] * 1e-30f;
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -130,8 +131,8 @@ int main() {
   hipMemcpy(din, hin.data(), 1024, hipMemcpyHostToDevice);
   const char* hogn[] = {"none", "mfma", "mfma+lds", "valu-exp"};
   const char* seln[] = {"all", "same-simd", "other-simd"};
-  for (int sweep = 0; sweep < 2; ++sweep) {
-    for (int prio = 0; prio < 2; ++prio) {
+  for (int sweep = 0; sweep < 3; ++sweep) {
+    for (int prio = 0; prio < 1; ++prio) {
       for (int kind = 0; kind < 4; ++kind) {
         for (int sel = 0; sel < 3; ++sel) {
           if (kind == 0 && sel > 0) continue;
@@ -139,15 +140,17 @@ int main() {
           for (int rep = 0; rep < 2; ++rep) {
             if (sweep == 0)
               hipLaunchKernelGGL(kdiag<0>, dim3(BL), dim3(threads), 0, 0, din, dout, dc, dhw, 200, kind, sel, prio);
-            else
+            else if (sweep == 1)
               hipLaunchKernelGGL(kdiag<1>, dim3(BL), dim3(threads), 0, 0, din, dout, dc, dhw, 200, kind, sel, prio);
+            else
+              hipLaunchKernelGGL(kdiag<2>, dim3(BL), dim3(threads), 0, 0, din, dout, dc, dhw, 200, kind, sel, prio);
           }
           hipDeviceSynchronize();
           std::vector<unsigned long long> c(BL);
           hipMemcpy(c.data(), dc, 8 * BL, hipMemcpyDeviceToHost);
           double s = 0;
           for (auto v : c) s += v;
-          printf("sweep=%s prio=%d hog=%-9s sel=%-10s cycles/sweep %.0f\n", sweep ? "dpp" : "readlane", prio,
+          printf("sweep=%d prio=%d hog=%-9s sel=%-10s cycles/sweep %.0f\n", sweep, prio,
                  hogn[kind], seln[sel], s / BL);
         }
       }
@@ -167,13 +170,13 @@ int main() {
   float* o2;
   hipMalloc(&o2, (4096 + BL * 1024) * 4);
   hipLaunchKernelGGL(kdiag<0>, dim3(1), dim3(64), 0, 0, din, dout, dc, dhw, 1, 0, 0, 0);
-  hipLaunchKernelGGL(kdiag<1>, dim3(1), dim3(64), 0, 0, din, o2, dc, dhw, 1, 0, 0, 0);
+  hipLaunchKernelGGL(kdiag<2>, dim3(1), dim3(64), 0, 0, din, o2, dc, dhw, 1, 0, 0, 0);
   hipDeviceSynchronize();
   std::vector<float> r0(64), r1(64);
   hipMemcpy(r0.data(), dout, 256, hipMemcpyDeviceToHost);
   hipMemcpy(r1.data(), o2, 256, hipMemcpyDeviceToHost);
   double md = 0;
   for (int l = 0; l < 32; ++l) md = fmax(md, fabs(r0[l] - r1[l]));
-  printf("readlane vs dpp max |diff| over lanes 0-31: %.3e (lane0 %.6f %.6f)\n", md, r0[0], r1[0]);
+  printf("readlane vs asm-dpp max |diff| over lanes 0-31: %.3e (lane0 %.6f %.6f)\n", md, r0[0], r1[0]);
   return 0;
 }

@@ -31,8 +31,8 @@ print(f"clock GHz (memtime/realtime): {np.mean(s[:, 8] / (s[:, 9] / 100e6)) / 1e
 for i, n in enumerate(names):
     print(f"  {n:22s} {s[:, i].mean():10.0f}  ({100 * s[:, i].mean() / tot.mean():5.1f}%)")
 for i, n in [(24, "pro: X loads+staging+max"), (25, "pro: column partials"), (26, "pro: mean"),
-             (27, "pro: centre+split"), (18, "w0: trailing upd"), (19, "w0: deferred RBF"), (20, "w0: TRSM"), (21, "w0: worker barrier"),
-             (22, "w0: zero-L + RHS"), (23, "w0: wait R_kk^-T"), (2, "diag: tile load"), (3, "diag: sweep"), (4, "diag: publish"), (13, "diag: factor"), (14, "diag: wait look-ahead tiles"), (15, "diag: look-ahead compute")]:
+             (27, "pro: centre+split"), (18, "w0: trailing upd"), (19, "w0: RHS+zeroL+RBF"), (20, "w0: TRSM"), (21, "w0: step counter"),
+             (22, "w0: hand-over"), (23, "w0: wait R_kk^-T"), (2, "diag: tile load"), (3, "diag: sweep"), (4, "diag: publish"), (13, "diag: factor"), (14, "diag: wait look-ahead tiles"), (15, "diag: look-ahead compute")]:
     print(f"  {n:28s} {s[:, i].mean():10.0f}  ({100 * s[:, i].mean() / tot.mean():5.1f}%)")
 
 hw = s[:, 10].astype(np.int64)
@@ -59,13 +59,14 @@ rel = np.where(valid, tl - base[:, None, None, None], -1).astype(np.float64)
 rel[~valid] = np.nan
 m = np.nanmean(rel, axis=0)  # (16 steps, 8 waves, 8 events)
 print("per-step timeline (cycles from the window's first timeline event, mean over windows)")
-print(" k | diag: fac0  fac1  LAin  LAdone | workers (mean over waves): start  trail  zRHS   rbf   wait  trsm  barr | max-wave barr")
+print(" k | diag: fac0  fac1  LAin  LAdone | workers (mean over waves): start  waitW  trsm  count  hand  trail  rest | max-wave rest")
 for k in range(16):
     d = m[k, 7]
     w = np.nanmean(m[k, :7], axis=0)
     wb = np.nanmax(m[k, :7, 6])
     print(f"{k:2d} | {d[0]:6.0f} {d[1]:6.0f} {d[2]:6.0f} {d[3]:6.0f} | " + " ".join(f"{v:6.0f}" for v in w[:7]) + f" | {wb:6.0f}")
-print("per-wave trailing+rbf+trsm busy cycles at k=1..3:")
+print("per-wave busy cycles (trsm + hand + trail + rest) and waits (W + counter) at k=1,2,3,8:")
 for k in (1, 2, 3, 8):
-    busy = (m[k, :7, 1] - m[k, :7, 0]) + (m[k, :7, 3] - m[k, :7, 2]) + (m[k, :7, 5] - m[k, :7, 4])
-    print(k, " ".join(f"{v:5.0f}" for v in busy), " wait:", " ".join(f"{v:5.0f}" for v in (m[k, :7, 4] - m[k, :7, 3])))
+    busy = (m[k, :7, 2] - m[k, :7, 1]) + (m[k, :7, 6] - m[k, :7, 3])
+    wait = (m[k, :7, 1] - m[k, :7, 0]) + (m[k, :7, 3] - m[k, :7, 2])
+    print(k, " ".join(f"{v:5.0f}" for v in busy), " wait:", " ".join(f"{v:5.0f}" for v in wait))
