@@ -47,9 +47,6 @@
 #ifndef GPK_EXACT_FLOW
 #define GPK_EXACT_FLOW 0  // 1: dataflow step order (TRSM -> counter -> hand-over -> bulk); 0: round-2 order
 #endif
-#ifndef GPK_EXACT32
-#define GPK_EXACT32 0        // 1: N % 32 == 0 and D <= 32 use 32-column steps (gpk_exact32.inc; measured no faster)
-#endif
 #ifndef GPK_EXACT_SMALLB
 #define GPK_EXACT_SMALLB 1   // B <= CUs: one window per CU with 16 waves (launch_exact_nb)
 #endif
@@ -1709,36 +1706,15 @@ int launch_exact_any(const GpkExactArgs& a, hipStream_t stream) {
                           : launch_exact_nb<NB, false, false>(a, nullptr, stream);
 }
 
-#include "gpk_exact32.inc"
-
 }  // namespace
 
 int gpk_launch_exact_stamps(const GpkExactArgs& a, unsigned long long* stamps, hipStream_t stream) {
   if (a.N != 256) return -6;
-#if GPK_EXACT32
-  if (a.D <= 32) return launch_exact32_w<8, 8, 2, true>(a, stream, stamps);
-#endif
   return launch_exact_nb<16, true, true>(a, stamps, stream);
 }
 
 int gpk_launch_exact(const GpkExactArgs& a, hipStream_t stream) {
   const int NB = (a.N + 15) / 16;
-#if GPK_EXACT32
-  // 32-column steps (gpk_exact32.inc): N a multiple of 32, D <= 32
-  if (a.N % 32 == 0 && a.D <= 32 && a.D >= 1) {
-    switch (a.N / 32) {
-#define GPK_CASE32(ns) case ns: return launch_exact32<ns>(a, stream);
-#if GPK_EXACT_DEV
-      GPK_CASE32(8)
-#else
-      GPK_CASE32(1) GPK_CASE32(2) GPK_CASE32(3) GPK_CASE32(4)
-      GPK_CASE32(5) GPK_CASE32(6) GPK_CASE32(7) GPK_CASE32(8)
-#endif
-#undef GPK_CASE32
-      default: break;
-    }
-  }
-#endif
   switch (NB) {
 #define GPK_CASE(nb) case nb: return launch_exact_any<nb>(a, stream);
 #if GPK_EXACT_DEV  // development A/B builds: the N=256 instantiation only (fast compile)

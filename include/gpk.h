@@ -111,7 +111,9 @@ int gpk_exact_posterior_f32(const float* X, const float* L, const float* z, cons
  *   Linv = L^{-1}
  * K_ZZ = s2 * exp(-0.5 ||(z_i - z_j)/l||^2) with ARD lengthscales (GPyTorch's centred
  * GEMM-form squared distance, diagonal not zeroed: Z requires grad in the reference).
- * One workgroup, blocked (32-column) elimination of [A | I] in fp64.
+ * Factor: ONE workgroup (fp64 MFMA rank-4 right-looking steps on register tiles, the
+ * fp64 ladder restarted in-kernel); inverse: one workgroup per 16-column block column
+ * (block forward substitution on fp64 MFMA), the block columns on different CUs.
  *
  * Replaces (reference): the per-window (b-fold redundant) fp64 Cholesky that
  * VariationalStrategy._cholesky_factor runs for ToyDeepGPHiddenLayer

@@ -14,9 +14,10 @@ reference's own Transformer (modules/transformer.py:9-43) for
 
 from synthetic z-scored inputs ~N(0, 1) (the datasets need the network), the
 enc/dec embeddings nn.Linear(input, d_model) as at forecast_denoising.py:65-66, seed
-1234 (train.py:254). ``WINDOWS`` distinct windows are stored as float16 (the values are
-inputs; both the HIP path and the oracle read the same float32 up-cast) with targets
-y ~ N(0, 1) of shape (windows, 96, 1). Tests tile them to the batch size.
+1234 (train.py:254). ``WINDOWS[cfg]`` distinct windows (cfg1: all 32 of its batch; cfg3:
+128, half of its batch of 256) are stored as float16 (the values are inputs; both the HIP
+path and the oracle read the same float32 up-cast) with targets y ~ N(0, 1) of shape
+(windows, 96, 1). Tests tile them to the batch size.
 
     PYTHONDONTWRITEBYTECODE=1 python -B tests/golden/make_backbone_fixtures.py
 """
@@ -30,7 +31,7 @@ import torch.nn as nn
 
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
-WINDOWS = 32
+WINDOWS = {"cfg1_solar_autoformer": 32, "cfg3_traffic_ata": 128}
 ENC, DEC, D, HEADS, SEED = 192, 96, 32, 8, 1234
 
 
@@ -49,9 +50,10 @@ def main():
                             attn_type=attn, seed=SEED)
         enc_emb, dec_emb = nn.Linear(nin, D), nn.Linear(nin, D)
         g = torch.Generator().manual_seed(SEED + 1)
-        enc_in = torch.randn(WINDOWS, ENC, nin, generator=g)
-        dec_in = torch.randn(WINDOWS, DEC, nin, generator=g)
-        y = torch.randn(WINDOWS, DEC, 1, generator=g)
+        nw = WINDOWS[name]
+        enc_in = torch.randn(nw, ENC, nin, generator=g)
+        dec_in = torch.randn(nw, DEC, nin, generator=g)
+        y = torch.randn(nw, DEC, 1, generator=g)
         with torch.no_grad():
             enc_out, dec_out = model(enc_emb(enc_in), dec_emb(dec_in))
         path = os.path.join(OUT, f"backbone_{name}.npz")

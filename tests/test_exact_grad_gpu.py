@@ -128,3 +128,31 @@ def test_exact_grad_native_kernel_loaded(cuda_device):
     assert rc == 0
     torch.cuda.synchronize()
     assert torch.isfinite(dh).all()
+
+
+def test_exact_grad_full_bench_batch(cuda_device):
+    """The backward at the bench / BASELINE configs[3] batch (B=512, N=256, D=32: the
+    launch the bench times), checked per window on a sample of 8 windows spread over the
+    batch: dX, dy and the per-window hyper-parameter rows vs the fp64 oracle (1e-4)."""
+    from fine_grained_gaussian_process_forcasting_amd import ops
+    B, N, D = 512, 256, 32
+    g = torch.Generator().manual_seed(512)
+    X = torch.randn(B, N, D, generator=g) / np.sqrt(D)
+    y = torch.randn(B, N, generator=g)
+    s2, c, noise = LN2, 0.0, NOISE0
+    gout = torch.rand(B, generator=g) + 0.5
+    dev = cuda_device
+    hyper = ops.pack_exact_hyper(s2, noise, c, LN2, dev)
+    fw = ops.exact_mll(X.to(dev), y.to(dev), None, None, None, None, hyper=hyper, want_L=True, want_z=True)
+    assert (fw.info.cpu() == 0).all()
+    gr = ops.exact_mll_grad(X.to(dev), fw.L, fw.z, hyper, gout.to(dev))
+    torch.cuda.synchronize()
+    dX, dy, dh = gr.dX.cpu().numpy(), gr.dy.cpu().numpy(), gr.dhyp.cpu().double().numpy()
+    for w in np.linspace(0, B - 1, 8).astype(int):
+        ref = O.exact_mll_grads(X[w:w + 1].double().numpy(), y[w:w + 1].double().numpy(), LN2, s2, c, noise,
+                                gout=gout[w:w + 1].double().numpy())
+        got = {"X": dX[w:w + 1], "y": dy[w:w + 1], "outputscale": dh[w, 0], "noise": dh[w, 1],
+               "mean_constant": dh[w, 2], "lengthscale": dh[w, 3]}
+        for k in got:
+            e = _rel(got[k], ref[k])
+            assert e <= TOL, (w, k, e)
