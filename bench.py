@@ -168,7 +168,7 @@ def load_traffic(key):
         return None
 
 
-def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
+def variational_leg(dev, B, N, M, D, steps, warmup, world, seed, label="BASELINE configs[4]"):
     """BASELINE configs[4] per GPU: forward (K_ZZ factor + predictive mean / var / ELL)
     and the fused backward, each timed over back-to-back launches (time_launches)."""
     g = torch.Generator().manual_seed(seed)
@@ -208,12 +208,13 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed):
     t_fwd_s = ms["fwd"] * 1e-3
     achieved = (f32 + f64) * B / t_fwd_s
     return {
-        "workload": f"DeepGP variational (BASELINE configs[4]): B={B} N={N} M={M} D={D} per GPU",
+        "workload": f"DeepGP variational ({label}): B={B} N={N} M={M} D={D} per GPU",
         "windows_per_s_fwd": B * world / ((ms["kzz"] + ms["fwd"]) * 1e-3),
         "windows_per_s_train_step": B * world / ((ms["kzz"] + ms["fwd"] + ms["bwd"]) * 1e-3),
         "kernel_ms": {"gpk_kzz_chol_f64": ms["kzz"], "gpk_variational_f32": ms["fwd"],
                       "gpk_variational_adjoint_f32": ms["bwd"]},
-        "roofline": {"kernel": "gpk_var_fwd_kernel", "bound": "mfma",
+        "roofline": {"kernel": "gpk_var_fwd_r_kernel" if (M <= 64 and D <= 32) else "gpk_var_fwd_l_kernel",
+                     "bound": "mfma",
                      "achieved": achieved / 1e12, "peak": (f32 + f64) / roof_s / 1e12,
                      "unit": "TFLOP/s", "frac": roof_s * B / t_fwd_s,
                      "flops_per_window": {"fp32": f32, "fp64": f64},
@@ -276,6 +277,7 @@ def main():
     ap.add_argument("--var-N", type=int, default=256)
     ap.add_argument("--var-M", type=int, default=64)
     ap.add_argument("--no-var", action="store_true", help="skip the variational side leg")
+    ap.add_argument("--no-var3", action="store_true", help="skip the cfg-3 (M=256) variational legs")
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grad", action="store_true", help="skip the backward side measurement")
@@ -395,6 +397,13 @@ def main():
         var = variational_leg(dev, args.var_B, args.var_N, args.var_M, D, max(5, args.steps // 5),
                               3, world, seed=7 + rank)
 
+    # the cfg-3 GP shape the reference trains (DeepGP default M=256; enc N=192, dec N=96, b=256)
+    var3 = None
+    if rank == 0 and not args.no_var3:
+        var3 = {f"N{n}": variational_leg(dev, 256, n, 256, D, 10, 3, 1, seed=13 + n,
+                                         label=f"cfg-3 GP shape, {'enc' if n == 192 else 'dec'}")
+                for n in (192, 96)}
+
     if rank == 0:
         value = B_total * args.steps / elapsed
         bpw, fpw = bytes_per_window(N, D), flops_per_window(N, D)
@@ -443,6 +452,8 @@ def main():
         if var is not None:
             line["variational"] = var
             line["elbo_rel_err_vs_fp64_oracle"] = var["elbo_rel_err_vs_fp64_oracle"]
+        if var3 is not None:
+            line["variational_cfg3"] = var3
         if rank == 0 and strong_share is not None:
             line["strong_share"] = strong_share
         if world == 1 and not args.no_e2e:

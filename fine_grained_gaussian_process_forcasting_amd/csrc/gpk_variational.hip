@@ -59,6 +59,15 @@ GPK_DEVICE float row16_sum_f(float v) {
   return v;
 }
 
+// Per-chunk LDS base the compiler must treat as new on every iteration: the staged
+// operands (L^{-1}, zs, norms) and their per-lane addresses would otherwise be hoisted out of the chunk loop as
+// loop-invariant loads and pinned in (hundreds of) registers.
+GPK_DEVICE const float* fresh_lds(const float* p) {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return p + z;
+}
+
 // ---------------------------------------------------------------------------
 // K_ZZ factorisation on fp64 MFMA tiles (one workgroup of KT = 512 threads).
 // The lower triangle (M padded to Mp = multiple of 16, identity padding) is held as
@@ -785,6 +794,304 @@ gpk_var_ell_kernel(const float* __restrict__ mean, const float* __restrict__ var
 }
 
 // ---------------------------------------------------------------------------
+// Forward for M > 64 (cfg-3 shape M = 256): L^{-1} held in REGISTERS for the whole launch.
+// A persistent workgroup of NWV = ceil(MB/2) waves; wave w owns the row tiles rA = w and
+// rB = MB-1-w, i.e. MB+1 16x16 blocks of the lower triangle of L^{-1} (the same count for
+// every wave: balanced), loaded once as f64 MFMA A operands: slot s holds, on lane (c, g)
+// at MFMA step u, L^{-1}[16 rt + c][16 kb + 4 g + u]. Per 32-point chunk:
+//   stage   xs = x/l - mean(Z/l), |xs|^2 and x.w (16 threads per point, DPP row sums);
+//   Gram    the K_ZX tiles of the wave's own row tiles on f32 MFMA -- the f32 C layout
+//           (reg r <-> row 4g + r) IS the f64 B-operand layout of step u = r, so each tile is
+//           one b128 LDS store, read back by every wave as one b128 per (kb, column tile);
+//   GEMM    A[rt] += L^{-1}[rt, kb] K_ZX[kb] over the wave's MB+1 blocks (fp64 MFMA);
+//   reduce  per-wave partials of sum_m A m and sum_m A^2 (s^2 - 1) -> LDS, one wave finishes
+//           mean / variance while the others stage the next chunk (its points were loaded
+//           into registers during this chunk's GEMM).
+// The LDS-tiled kernel above re-read the L^{-1} triangle (272 KB) from L2 for every chunk.
+// ---------------------------------------------------------------------------
+constexpr int LTW = 32;   // points per chunk (2 column tiles)
+
+// A[rA] / A[rB] of one chunk for the wave with rA = RA: slots 0..RA are blocks (RA, s),
+// slots RA+1..MB blocks (MB-1-RA, s-RA-1). The next slot's K_ZX operands (one b128 per
+// column tile) are read while this slot's 8 MFMAs run; a scheduling fence per slot keeps
+// the reads from all being hoisted.
+template <int MB, int RA>
+GPK_DEVICE void lreg_gemm(const double (&Lr)[MB + 1][4], const float* Kl, int lane,
+                          f64x4 (&aA)[2], f64x4 (&aB)[2]) {
+  constexpr int RB = MB - 1 - RA;
+  constexpr int NS = RB == RA ? RA + 1 : MB + 1;
+  f64x4 acc[2] = {f64x4{0.0, 0.0, 0.0, 0.0}, f64x4{0.0, 0.0, 0.0, 0.0}};
+  f32x4 k0 = *(const f32x4*)(Kl + (0 * 64 + lane) * 4);
+  f32x4 k1 = *(const f32x4*)(Kl + (1 * 64 + lane) * 4);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s == RA + 1) {
+      aA[0] = acc[0];
+      aA[1] = acc[1];
+      acc[0] = acc[1] = f64x4{0.0, 0.0, 0.0, 0.0};
+    }
+    f32x4 n0 = k0, n1 = k1;
+    if (s + 1 < NS) {
+      const int kbn = s + 1 <= RA ? s + 1 : s - RA;
+      n0 = *(const f32x4*)(Kl + ((kbn * 2 + 0) * 64 + lane) * 4);
+      n1 = *(const f32x4*)(Kl + ((kbn * 2 + 1) * 64 + lane) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[0] = mfma64(Lr[s][u], (double)k0[u], acc[0]);
+      acc[1] = mfma64(Lr[s][u], (double)k1[u], acc[1]);
+    }
+    k0 = n0;
+    k1 = n1;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (RB == RA) {
+    aA[0] = acc[0];
+    aA[1] = acc[1];
+    aB[0] = aB[1] = f64x4{0.0, 0.0, 0.0, 0.0};
+  } else {
+    aB[0] = acc[0];
+    aB[1] = acc[1];
+  }
+}
+template <int MB, int RA>
+GPK_DEVICE void lreg_gemm_for(int wave, const double (&Lr)[MB + 1][4], const float* Kl, int lane,
+                              f64x4 (&aA)[2], f64x4 (&aB)[2]) {
+  if constexpr (RA < (MB + 1) / 2) {
+    if (wave == RA) lreg_gemm<MB, RA>(Lr, Kl, lane, aA, aB);
+    else lreg_gemm_for<MB, RA + 1>(wave, Lr, Kl, lane, aA, aB);
+  }
+}
+
+template <int MB, int DQ>
+struct LGeo {
+  static constexpr int NWV = (MB + 1) / 2;              // waves
+  static constexpr int NT = 64 * NWV;
+  static constexpr int MP = 16 * MB;
+  static constexpr int DS = DQ + 2;                     // zs / xs row stride (floats)
+  static constexpr int NPASS = (LTW * 16 + NT - 1) / NT; // point-staging passes (16 thr / point)
+  static constexpr int DV = DQ / 16;                    // dims per staging thread
+  // LDS (floats): Kl first (b128 aligned)
+  static constexpr int oKl = 0;                          // MB x 2 tiles x 64 lanes x 4
+  static constexpr int oRed = oKl + MP * LTW;            // NWV x 2 x LTW
+  static constexpr int oZs = oRed + NWV * 2 * LTW;       // MP x DS
+  static constexpr int oZn = oZs + MP * DS;
+  static constexpr int oVm = oZn + MP;
+  static constexpr int oSm1 = oVm + MP;
+  static constexpr int oCm = oSm1 + MP;                  // DQ
+  static constexpr int oXs = oCm + DQ;                   // LTW x DS
+  static constexpr int oXn = oXs + LTW * DS;             // LTW
+  static constexpr int oLin = oXn + LTW;                 // 2 x LTW (chunk parity)
+  static constexpr int total = oLin + 2 * LTW;
+};
+
+template <int MB, int DQ>
+__global__ void __launch_bounds__(64 * ((MB + 1) / 2), 2)
+gpk_var_fwd_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                     const double* __restrict__ Linv, const float* __restrict__ vmean,
+                     const float* __restrict__ vstd, const float* __restrict__ hyp, int N, int M,
+                     int D, int nchunks, float* __restrict__ mean_out, float* __restrict__ var_out,
+                     int* __restrict__ flags) {
+  using G = LGeo<MB, DQ>;
+  constexpr int NWV = G::NWV, NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV;
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4, sub = tid & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rA = wave, rB = MB - 1 - wave;   // rB == rA: the middle wave of an odd MB
+  // hyp: [s2, noise, jitter, b0, w[D], ls[D]]
+  const float s2 = hyp[0], jit = hyp[2], b0 = hyp[3];
+  const float* w = hyp + 4;
+  const float* ls = hyp + 4 + D;
+  const int nch = (N + LTW - 1) / LTW;
+
+  // the wave's L^{-1} blocks -> registers. M % 16 == 0: two row bases, every slot one
+  // 32-byte run at an immediate offset (no per-load address registers or masks -- with
+  // them the 68 loads in flight at M = 256 overflowed the register file); otherwise
+  // masked loads from clamped addresses, 4 slots in flight at a time.
+  double Lr[MB + 1][4];
+  if ((M & 15) == 0) {
+    const double* baseA = Linv + (size_t)(16 * rA + c) * M + 4 * g;
+    const double* baseB = Linv + (size_t)(16 * rB + c) * M + 4 * g - 16 * (rA + 1);
+#pragma unroll
+    for (int s = 0; s <= MB; ++s) {
+      const bool isA = s <= rA;
+      if (isA || rB != rA) {
+        const double* src = (isA ? baseA : baseB) + 16 * s;
+        const double2 v0 = *(const double2*)src, v1 = *(const double2*)(src + 2);
+        Lr[s][0] = v0.x; Lr[s][1] = v0.y; Lr[s][2] = v1.x; Lr[s][3] = v1.y;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Lr[s][u] = 0.0;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s <= MB; ++s) {
+      const bool isA = s <= rA;
+      const int rt = isA ? rA : rB, kb = isA ? s : s - rA - 1;
+      const bool ok = isA || rB != rA;
+      const int m = 16 * rt + c;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = 16 * kb + 4 * g + u;
+        const bool in = ok && m < M && p < M;
+        const double v = Linv[in ? (size_t)m * M + p : 0];
+        Lr[s][u] = in ? v : 0.0;
+      }
+      if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // per-thread staging constants: dims d = sub + 16 v
+  float lsr[DV], wr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) {
+    const int d = sub + 16 * v;
+    lsr[v] = ls[d < D ? d : 0];
+    wr[v] = d < D ? w[d] : 0.f;
+  }
+  float xr[NPASS][DV];
+  auto load_x = [&](int t) {
+    const int b = t / nch, i0 = (t - b * nch) * LTW;
+#pragma unroll
+    for (int q = 0; q < NPASS; ++q) {
+      const int j = (tid >> 4) + q * (NT / 16), i = i0 + j;
+      const bool ok = t < nchunks && j < LTW && i < N;
+#pragma unroll
+      for (int v = 0; v < DV; ++v) {
+        const int d = sub + 16 * v;
+        const bool okd = ok && d < D;
+        const float x = X[okd ? ((size_t)b * N + i) * D + d : 0];
+        xr[q][v] = okd ? x : 0.f;
+      }
+    }
+  };
+  load_x(blockIdx.x);
+  stage_inducing(Z, ls, vmean, vstd, M, D, G::MP, DQ, DS, vsm + G::oZs, vsm + G::oZn, vsm + G::oCm,
+                 vsm + G::oVm, vsm + G::oSm1);
+  lds_barrier();
+  float cmr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) cmr[v] = vsm[G::oCm + sub + 16 * v];
+  int clamped = 0, par = 0;
+
+  for (int t = blockIdx.x; t < nchunks; t += gridDim.x, par ^= 1) {
+    const int b = t / nch, i0 = (t - b * nch) * LTW;
+    const int nvalid = N - i0 < LTW ? N - i0 : LTW;
+    // every LDS address re-derived per chunk (hoisted, they pinned ~100 registers)
+    float* sm = (float*)fresh_lds(vsm);
+    float* Kl = sm + G::oKl;
+    float* red = sm + G::oRed;
+    const float* zs = sm + G::oZs;
+    const float* zn = sm + G::oZn;
+    const float* vm = sm + G::oVm;
+    const float* sm1 = sm + G::oSm1;
+    float* xs = sm + G::oXs;
+    float* xn = sm + G::oXn;
+    float* lin = sm + G::oLin + par * LTW;
+    // stage the chunk's points (xs of the previous chunk was last read by its Gram, before
+    // the previous GEMM barrier; lin is double-buffered against the finishing wave)
+#pragma unroll
+    for (int q = 0; q < NPASS; ++q) {
+      const int j = (tid >> 4) + q * (NT / 16);
+      float nrm = 0.f, lp = 0.f;
+      const bool okj = j < nvalid;
+#pragma unroll
+      for (int v = 0; v < DV; ++v) {
+        const int d = sub + 16 * v;
+        const float xv = (okj && d < D) ? xr[q][v] / lsr[v] - cmr[v] : 0.f;
+        nrm = __builtin_fmaf(xv, xv, nrm);
+        lp = __builtin_fmaf(xr[q][v], wr[v], lp);
+        if (j < LTW) xs[j * DS + d] = xv;
+      }
+      nrm = row16_sum_f(nrm);
+      lp = row16_sum_f(lp);
+      if (sub == 0 && j < LTW) {    // (row16_sum_f leaves the sum on all 16 lanes)
+        xn[j] = nrm;
+        lin[j] = lp;
+      }
+    }
+    lds_barrier();
+    // K_ZX tiles of the wave's row tiles
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rt = h == 0 ? rA : rB;
+      if (h == 1 && rB == rA) break;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const float* za = zs + (16 * rt + c) * DS + g;
+        const float* xb = xs + (16 * ct + c) * DS + g;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < DQ / 4; ++k) acc = mfma32(za[4 * k], xb[4 * k], acc);
+        const int col = 16 * ct + c;
+        const float xnc = xn[col];
+        f32x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * rt + 4 * g + r;
+          float dist = zn[p] + xnc - 2.f * acc[r];
+          dist = dist < 0.f ? 0.f : dist;
+          o[r] = (p < M && col < nvalid) ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * dist) : 0.f;
+        }
+        *(f32x4*)(Kl + ((rt * 2 + ct) * 64 + lane) * 4) = o;
+      }
+    }
+    if (t + (int)gridDim.x < nchunks) load_x(t + gridDim.x);   // next chunk's points
+    lds_barrier();
+    // A = L^{-1} K_ZX on the wave's row tiles (code specialised per wave: the slot -> row
+    // tile switch at rA is then static -- as a runtime test it was if-converted into
+    // selects that doubled the accumulators)
+    f64x4 aA[2], aB[2];
+    lreg_gemm_for<MB, 0>(wave, Lr, Kl, lane, aA, aB);
+    // partials over the wave's rows (A cast to fp32 as the reference does)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      float mp = 0.f, vp = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rowA = 16 * rA + g + 4 * r;
+        const float a = (float)aA[ct][r];
+        mp = __builtin_fmaf(a, vm[rowA], mp);
+        vp = __builtin_fmaf(a * a, sm1[rowA], vp);
+      }
+      if (rB != rA) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rowB = 16 * rB + g + 4 * r;
+          const float a = (float)aB[ct][r];
+          mp = __builtin_fmaf(a, vm[rowB], mp);
+          vp = __builtin_fmaf(a * a, sm1[rowB], vp);
+        }
+      }
+      mp += __shfl_xor(mp, 16, 64);
+      mp += __shfl_xor(mp, 32, 64);
+      vp += __shfl_xor(vp, 16, 64);
+      vp += __shfl_xor(vp, 32, 64);
+      if (g == 0) {
+        red[(wave * 2 + 0) * LTW + 16 * ct + c] = mp;
+        red[(wave * 2 + 1) * LTW + 16 * ct + c] = vp;
+      }
+    }
+    lds_barrier();
+    if (tid < nvalid) {
+      float mm = 0.f, vv = 0.f;
+#pragma unroll
+      for (int q = 0; q < NWV; ++q) {
+        mm += red[(q * 2 + 0) * LTW + tid];
+        vv += red[(q * 2 + 1) * LTW + tid];
+      }
+      const float mean_i = mm + (lin[tid] + b0);
+      float var_i = s2 + jit + vv;
+      if (var_i < 1e-6f) { var_i = 1e-6f; clamped = 1; }  // MVN.variance clamp (fp32)
+      mean_out[(size_t)b * N + i0 + tid] = mean_i;
+      var_out[(size_t)b * N + i0 + tid] = var_i;
+    }
+  }
+  if (flags != nullptr && clamped)
+    (void)__hip_atomic_fetch_or(flags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
 // Adjoint of the forward for the objective sum(gmean * mean) + sum(gvar * var).
 // Per chunk (same tiling as the forward):
 //   K_ZX (LDS), A = L^{-1} K_ZX (fp64 MFMA), var -> clamp mask on gvar,
@@ -1385,14 +1692,6 @@ GPK_DEVICE void stage_reg(const float* Z, const float* ls, const float* vmean, c
 
 GPK_DEVICE int pi_row(int x) { return (x >> 2) + 4 * (x & 3); }
 
-// Per-chunk LDS base the compiler must treat as new on every iteration: the staged
-// operands (L^{-1}, zs, norms) would otherwise be hoisted out of the chunk loop as
-// loop-invariant loads and pinned in (hundreds of) registers.
-GPK_DEVICE const float* fresh_lds(const float* p) {
-  int z = 0;
-  asm volatile("" : "+s"(z));
-  return p + z;
-}
 
 // Points i0 + 16q + c of window b: Gram B operands xb[q][s] = xs[i][4s + g], squared
 // norms (full, every lane), and optionally x . w (full).
@@ -1953,6 +2252,32 @@ int launch_var_fwd(const GpkVarArgs& a, int* flags, hipStream_t stream) {
   return e == hipSuccess ? 0 : (int)e;
 }
 
+template <int MB, int DQ>
+int launch_var_fwd_l(const GpkVarArgs& a, int* flags, hipStream_t stream) {
+  using G = LGeo<MB, DQ>;
+  const size_t lds = (size_t)G::total * sizeof(float);
+  if (lds > 160 * 1024) return -11;
+  set_lds_once<gpk_var_fwd_l_kernel<MB, DQ>>();
+  const long long nch = (long long)a.B * ((a.N + LTW - 1) / LTW);
+  if (nch > 0x7fffffffLL) return -8;
+  const int per_cu = G::NWV <= 4 ? 2 : 1;   // <= 2 waves per SIMD (256 VGPRs: L^{-1} resident)
+  hipLaunchKernelGGL((gpk_var_fwd_l_kernel<MB, DQ>), dim3(chunk_grid(nch, per_cu)), dim3(G::NT), lds,
+                     stream, a.X, a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.N, a.M, a.D, (int)nch,
+                     a.mean, a.var, flags);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  if (a.ell != nullptr) {
+    hipLaunchKernelGGL(gpk_var_ell_kernel, dim3(a.B), dim3(256), 0, stream, a.mean, a.var, a.y,
+                       a.hyp, a.N, a.ell);
+    e = hipGetLastError();
+  }
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+#ifndef GPK_VAR_LREG
+#define GPK_VAR_LREG 1   // 0: A/B builds with the LDS-tiled forward for M > 64
+#endif
+
 struct AdjPlan {
   int nchunks, nwg, P, ntiles, nsplit;
   long long BN, cols_per_split;
@@ -2130,6 +2455,19 @@ int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream) {
   }
   if (var_reg_path(a.M, a.D)) return a.D <= 16 ? launch_var_fwd_r<16>(a, flags, stream)
                                                : launch_var_fwd_r<32>(a, flags, stream);
+  if (GPK_VAR_LREG && a.M > 64) {
+#define GPK_CALL_FWDL(mb)                                                     \
+  if (a.D <= 16) return launch_var_fwd_l<mb, 16>(a, flags, stream);           \
+  if (a.D <= 32) return launch_var_fwd_l<mb, 32>(a, flags, stream);           \
+  return launch_var_fwd_l<mb, 64>(a, flags, stream);
+    const int mb = (a.M + 15) / 16;
+    if (mb <= 6) { GPK_CALL_FWDL(6) }
+    if (mb <= 8) { GPK_CALL_FWDL(8) }
+    if (mb <= 12) { GPK_CALL_FWDL(12) }
+    if (mb <= 16) { GPK_CALL_FWDL(16) }
+#undef GPK_CALL_FWDL
+    return -10;
+  }
 #define GPK_CALL_FWD(mb) return launch_var_fwd<mb>(a, flags, stream);
   GPK_MB_SWITCH((a.M + 15) / 16, GPK_CALL_FWD)
 #undef GPK_CALL_FWD
