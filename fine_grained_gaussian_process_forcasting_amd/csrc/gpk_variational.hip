@@ -37,6 +37,7 @@
 #define GPK_VAR_SKIP 0
 #endif
 
+
 namespace {
 
 constexpr float kLog2PiF = 1.8378770664093453f;
@@ -66,6 +67,12 @@ GPK_DEVICE const float* fresh_lds(const float* p) {
   int z = 0;
   asm volatile("" : "+s"(z));
   return p + z;
+}
+// The same for a global pointer whose per-lane addresses would be loop-invariant.
+template <typename T>
+GPK_DEVICE const T* fresh_ptr(const T* p) {
+  asm volatile("" : "+s"(p));
+  return p;
 }
 
 // ---------------------------------------------------------------------------
@@ -515,12 +522,37 @@ struct VarGeo {
 // D padded to a power of two >= 16 (<= 64): MFMA k-steps and d-tiles, and 256 % Dq == 0.
 GPK_HOST_DEVICE_INLINE int dq_of(int D) { return D <= 16 ? 16 : (D <= 32 ? 32 : 64); }
 
+// Column means of zs (rows 0..M-1, columns 0..Dq-1, row stride ds) in ONE fixed order for
+// every kernel that centres the inducing points (stage_inducing, gpk_var_fin_kernel): 8
+// partial sums per column over the rows m = k (mod 8), ascending, then k = 0..7 (a serial
+// sum over all M rows per column was ~20K cycles of dependent LDS reads at M = 256).
+// scr: >= 8 Dq floats of free LDS. Ends with a barrier.
+constexpr int kCmParts = 8;
+GPK_DEVICE void col_means(const float* zs, int M, int D, int Dq, int ds, float* scr, float* cm) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  for (int e = tid; e < kCmParts * Dq; e += T) {
+    const int d = e % Dq, k = e / Dq;
+    float a = 0.f;
+    for (int m = k; m < M; m += kCmParts) a += zs[m * ds + d];
+    scr[e] = a;
+  }
+  lds_barrier();
+  for (int d = tid; d < Dq; d += T) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < kCmParts; ++k) a += scr[k * Dq + d];
+    cm[d] = d < D ? a / (float)M : 0.f;   // GPyTorch _sq_dist centres by x1 = Z
+  }
+  lds_barrier();
+}
+
 // Stage the centred, scaled inducing points zs = Z/l - mean(Z/l) (rows >= M and
-// columns >= D zero), their squared norms, the q(u) mean and s^2 - 1.
+// columns >= D zero), their squared norms, the q(u) mean and s^2 - 1. scr: >= 8 Dq floats
+// of LDS that is free during the staging.
 GPK_DEVICE void stage_inducing(const float* __restrict__ Z, const float* __restrict__ ls,
                                const float* __restrict__ vmean, const float* __restrict__ vstd,
                                int M, int D, int MP, int Dq, int ds, float* zs, float* zn, float* cm,
-                               float* vm, float* sm1) {
+                               float* vm, float* sm1, float* scr) {
   const int tid = threadIdx.x, T = blockDim.x;
   // 8 unconditional loads (clamped addresses) in flight per thread, then the stores:
   // a predicated load per loop iteration costs one full memory latency each
@@ -545,12 +577,7 @@ GPK_DEVICE void stage_inducing(const float* __restrict__ Z, const float* __restr
     sm1[m] = sd * sd - 1.f;
   }
   lds_barrier();
-  for (int d = tid; d < Dq; d += T) {
-    float s = 0.f;
-    for (int m = 0; m < M; ++m) s += zs[m * ds + d];
-    cm[d] = d < D ? s / (float)M : 0.f;  // GPyTorch _sq_dist centres by x1 = Z
-  }
-  lds_barrier();
+  col_means(zs, M, D, Dq, ds, scr, cm);
   for (int e = tid; e < M * Dq; e += T) {
     const int m = e / Dq, d = e - m * Dq;
     zs[m * ds + d] -= cm[d];
@@ -710,7 +737,7 @@ gpk_var_fwd_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   const float* w = hyp + 4;
   const float* ls = hyp + 4 + D;
 
-  stage_inducing(Z, ls, vmean, vstd, M, D, MP, Dq, ds, zs, zn, cm, vm, sm1);
+  stage_inducing(Z, ls, vmean, vstd, M, D, MP, Dq, ds, zs, zn, cm, vm, sm1, Kl);
   const int nch = (N + TW - 1) / TW;
   int clamped = 0;
   // grid-stride over (window, chunk) pairs: the inducing-point staging is paid once
@@ -967,7 +994,7 @@ gpk_var_fwd_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   };
   load_x(blockIdx.x);
   stage_inducing(Z, ls, vmean, vstd, M, D, G::MP, DQ, DS, vsm + G::oZs, vsm + G::oZn, vsm + G::oCm,
-                 vsm + G::oVm, vsm + G::oSm1);
+                 vsm + G::oVm, vsm + G::oSm1, vsm + G::oKl);
   lds_barrier();
   float cmr[DV];
 #pragma unroll
@@ -1141,7 +1168,7 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   const float* w = hyp + 4;
   const float* ls = hyp + 4 + D;
 
-  stage_inducing(Z, ls, vmean, vstd, M, D, MP, Dq, ds, zs, zn, cm, vm, sm1);
+  stage_inducing(Z, ls, vmean, vstd, M, D, MP, Dq, ds, zs, zn, cm, vm, sm1, Kl);
   for (int m = tid; m < MP; m += blockDim.x) {
     qacc[m] = 0.f;
     for (int q = 0; q < G::WC; ++q) { dvma[q * MP + m] = 0.f; dsma[q * MP + m] = 0.f; }
@@ -1429,6 +1456,626 @@ gpk_var_adj_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 }
 
 // ---------------------------------------------------------------------------
+// Adjoint for M > 64 (cfg-3 shape M = 256) in the forward's register-resident layout
+// (gpk_var_fwd_l_kernel), split in two persistent kernels over the same chunk list:
+//   gpk_var_adja_l_kernel  wave w holds the L^{-1} ROW blocks of row tiles rA = w,
+//                          rB = MB-1-w: K (Gram), A = L^{-1} K, the variance clamp mask,
+//                          dA = gmean m + 2 gvar (s^2 - 1) A -> the workspace with K (for
+//                          dL^{-1} = sum dA K^T, gpk_dlinv_kernel, and for the next kernel);
+//                          dvmean / dvstd row sums.
+//   gpk_var_adjk_l_kernel  wave w holds the L^{-1} COLUMN blocks of block rows pA = w,
+//                          pB = MB-1-w: dK = L^{-T} dA from the chunk's dA / K tiles (LDS),
+//                          Q = dK o K, q_p, r_i, Q^T zs, QX += Q xs, dX.
+// (Both layouts at once would need 272 of the 256 registers; one fused kernel streaming the
+// column blocks from L2 spilled heavily.) k-order of every contraction over inducing
+// points: m = g + 4u, the f64 C layout, so accumulator tiles are the next product's B
+// operands directly; the Gram feeds the zs rows in the order pi(c) = (c >> 2) + 4 (c & 3)
+// to land in it. LDS tiles of K / dA: one b128 per lane, (rt, ct) tile at ((rt*2+ct)*64 +
+// lane)*4, element u <-> row 16 rt + g + 4u, point 16 ct + c.
+// Both kernels write disjoint fields of the same per-workgroup partial rows (the same grid).
+// ---------------------------------------------------------------------------
+GPK_DEVICE int pi16(int c) { return (c >> 2) + 4 * (c & 3); }
+
+// Buffer descriptors for the (M x BN) workspace arrays: a 32-bit lane offset plus a
+// wave-uniform SGPR offset per row step, where flat addressing pinned a 64-bit address per
+// load in flight (the host keeps M BN 4 < 2^31 on this path).
+GPK_DEVICE __amdgpu_buffer_rsrc_t ws_rsrc(const float* p, long long elems) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)(elems * 4), 0x00020000);
+}
+GPK_DEVICE float buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+GPK_DEVICE void buf_st(float v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+}
+
+template <int MB, int DQ>
+struct LAdjGeo {
+  static constexpr int NWV = (MB + 1) / 2, NT = 64 * NWV, MP = 16 * MB, DS = DQ + 2;
+  static constexpr int NPASS = (LTW * 16 + NT - 1) / NT, DV = DQ / 16, NDT = DQ / 16;
+  // gpk_var_adja_l_kernel
+  static constexpr int aKl = 0;                          // MP x LTW
+  static constexpr int aRed = aKl + MP * LTW;            // NWV x LTW
+  static constexpr int aZs = aRed + NWV * LTW;           // MP x DS
+  static constexpr int aZn = aZs + MP * DS;
+  static constexpr int aVm = aZn + MP;
+  static constexpr int aSm1 = aVm + MP;
+  static constexpr int aCm = aSm1 + MP;                  // DQ
+  static constexpr int aRows = aCm + DQ;                 // 2 x MP: dvm | dsm
+  static constexpr int aXs = aRows + 2 * MP;             // LTW x DS
+  static constexpr int aXn = aXs + LTW * DS;             // LTW
+  static constexpr int aGm = aXn + LTW;                  // 2 x LTW (chunk parity)
+  static constexpr int aGv = aGm + 2 * LTW;              // 2 x LTW
+  static constexpr int a_total = aGv + 2 * LTW;
+  // gpk_var_adjk_l_kernel
+  static constexpr int kKl = 0;                          // MP x LTW
+  static constexpr int kdA = kKl + MP * LTW;             // MP x LTW
+  static constexpr int kXz = kdA + MP * LTW;             // NWV x LTW x DQ  Q^T zs partials
+  static constexpr int kRed = kXz + NWV * LTW * DQ;      // NWV x LTW       r partials
+  static constexpr int kZs = kRed + NWV * LTW;           // MP x DS
+  static constexpr int kZn = kZs + MP * DS;
+  static constexpr int kVm = kZn + MP;
+  static constexpr int kSm1 = kVm + MP;
+  static constexpr int kCm = kSm1 + MP;                  // DQ
+  static constexpr int kQ = kCm + DQ;                    // MP  q_p
+  static constexpr int kScr = kQ + MP;                   // NWV x 320 transpose scratch
+  static constexpr int kXs = kScr + NWV * 320;           // 2 x LTW x DS (chunk parity)
+  static constexpr int kGm = kXs + 2 * LTW * DS;         // 2 x LTW
+  static constexpr int kMisc = kGm + 2 * LTW;            // 2 NT + NWV
+  static constexpr int k_total = kMisc + 2 * NT + NWV;
+  static constexpr bool fits = (size_t)a_total * 4 <= 160 * 1024 && (size_t)k_total * 4 <= 160 * 1024;
+};
+
+// dK of the wave with pA = RA from its column-block registers: slots 0..NA-1 are blocks
+// (rt = RA + s, RA), the rest (rt = RB + s - NA, RB); B operands dA[rt] from LDS.
+template <int MB, int RA>
+GPK_DEVICE void lcol_gemm(const double (&Lc)[MB + 1][4], const float* dAl, int lane,
+                          f64x4 (&dKa)[2], f64x4 (&dKb)[2]) {
+  constexpr int RB = MB - 1 - RA;
+  constexpr int NA = MB - RA;
+  constexpr int NS = RB == RA ? NA : MB + 1;
+  f64x4 acc[2] = {f64x4{0.0, 0.0, 0.0, 0.0}, f64x4{0.0, 0.0, 0.0, 0.0}};
+  f32x4 k0 = *(const f32x4*)(dAl + ((RA * 2 + 0) * 64 + lane) * 4);
+  f32x4 k1 = *(const f32x4*)(dAl + ((RA * 2 + 1) * 64 + lane) * 4);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s == NA) {
+      dKa[0] = acc[0];
+      dKa[1] = acc[1];
+      acc[0] = acc[1] = f64x4{0.0, 0.0, 0.0, 0.0};
+    }
+    f32x4 n0 = k0, n1 = k1;
+    if (s + 1 < NS) {
+      const int rtn = s + 1 < NA ? RA + s + 1 : RB + (s + 1 - NA);
+      n0 = *(const f32x4*)(dAl + ((rtn * 2 + 0) * 64 + lane) * 4);
+      n1 = *(const f32x4*)(dAl + ((rtn * 2 + 1) * 64 + lane) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[0] = mfma64(Lc[s][u], (double)k0[u], acc[0]);
+      acc[1] = mfma64(Lc[s][u], (double)k1[u], acc[1]);
+    }
+    k0 = n0;
+    k1 = n1;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (RB == RA) {
+    dKa[0] = acc[0];
+    dKa[1] = acc[1];
+    dKb[0] = dKb[1] = f64x4{0.0, 0.0, 0.0, 0.0};
+  } else {
+    dKb[0] = acc[0];
+    dKb[1] = acc[1];
+  }
+}
+template <int MB, int RA>
+GPK_DEVICE void lcol_gemm_for(int wave, const double (&Lc)[MB + 1][4], const float* dAl, int lane,
+                              f64x4 (&dKa)[2], f64x4 (&dKb)[2]) {
+  if constexpr (RA < (MB + 1) / 2) {
+    if (wave == RA) lcol_gemm<MB, RA>(Lc, dAl, lane, dKa, dKb);
+    else lcol_gemm_for<MB, RA + 1>(wave, Lc, dAl, lane, dKa, dKb);
+  }
+}
+
+// The chunk's points (16 threads per point, dims sub + 16 v) -> xs (and |xs|^2 -> xn if given).
+template <int NPASS, int DV, int NT, int DS>
+GPK_DEVICE void lstage_points(const float (&xr)[NPASS][DV], const float (&lsr)[DV], const float (&cmr)[DV],
+                              int D, int nvalid, float* xs, float* xn) {
+  const int tid = threadIdx.x, sub = tid & 15;
+#pragma unroll
+  for (int q = 0; q < NPASS; ++q) {
+    const int j = (tid >> 4) + q * (NT / 16);
+    float nrm = 0.f;
+    const bool okj = j < nvalid;
+#pragma unroll
+    for (int v = 0; v < DV; ++v) {
+      const int d = sub + 16 * v;
+      const float xv = (okj && d < D) ? xr[q][v] / lsr[v] - cmr[v] : 0.f;
+      nrm = __builtin_fmaf(xv, xv, nrm);
+      if (j < LTW) xs[j * DS + d] = xv;
+    }
+    if (xn != nullptr) {
+      nrm = row16_sum_f(nrm);
+      if (sub == 0 && j < LTW) xn[j] = nrm;
+    }
+  }
+}
+template <int NPASS, int DV, int NT>
+GPK_DEVICE void lload_points(const float* X, int t, int nchunks, int nch, int N, int D, float (&xr)[NPASS][DV]) {
+  const int tid = threadIdx.x, sub = tid & 15;
+  const int b = t / nch, i0 = (t - b * nch) * LTW;
+#pragma unroll
+  for (int q = 0; q < NPASS; ++q) {
+    const int j = (tid >> 4) + q * (NT / 16), i = i0 + j;
+    const bool ok = t < nchunks && j < LTW && i < N;
+#pragma unroll
+    for (int v = 0; v < DV; ++v) {
+      const int d = sub + 16 * v;
+      const bool okd = ok && d < D;
+      const float x = X[okd ? ((size_t)b * N + i) * D + d : 0];
+      xr[q][v] = okd ? x : 0.f;
+    }
+  }
+}
+
+template <int MB, int DQ>
+__global__ void __launch_bounds__(64 * ((MB + 1) / 2), 2)
+gpk_var_adja_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                      const double* __restrict__ Linv, const float* __restrict__ vmean,
+                      const float* __restrict__ vstd, const float* __restrict__ hyp,
+                      const float* __restrict__ gmean, const float* __restrict__ gvar, int N, int M,
+                      int D, int nchunks, long long BN, float* __restrict__ wsdA,
+                      float* __restrict__ wsK, float* __restrict__ wspart) {
+  using G = LAdjGeo<MB, DQ>;
+  constexpr int NWV = G::NWV, NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV;
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4, sub = tid & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rA = wave, rB = MB - 1 - wave;
+  const bool two = rB != rA;
+  const float s2 = hyp[0], jit = hyp[2];
+  const float* ls = hyp + 4 + D;
+  const int nch = (N + LTW - 1) / LTW;
+
+  // L^{-1} row blocks, k-order g + 4u: Lr[s][u] = L^{-1}[16 rt + c][16 kb + g + 4u]
+  double Lr[MB + 1][4];
+  {
+    const bool full = (M & 15) == 0;
+#pragma unroll
+    for (int s = 0; s <= MB; ++s) {
+      const bool isA = s <= rA;
+      const int rt = isA ? rA : rB, kb = isA ? s : s - rA - 1;
+      const bool ok = isA || two;
+      const int m = 16 * rt + c;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = 16 * kb + g + 4 * u;
+        const bool in = ok && (full || (m < M && p < M));
+        const double v = Linv[in ? (size_t)m * M + p : 0];
+        Lr[s][u] = in ? v : 0.0;
+      }
+      if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float lsr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) lsr[v] = ls[sub + 16 * v < D ? sub + 16 * v : 0];
+  float xr[NPASS][DV];
+  lload_points<NPASS, DV, NT>(X, blockIdx.x, nchunks, nch, N, D, xr);
+  stage_inducing(Z, ls, vmean, vstd, M, D, G::MP, DQ, DS, vsm + G::aZs, vsm + G::aZn, vsm + G::aCm,
+                 vsm + G::aVm, vsm + G::aSm1, vsm + G::aKl);
+  for (int e = tid; e < 2 * G::MP; e += NT) vsm[G::aRows + e] = 0.f;
+  lds_barrier();
+  float cmr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) cmr[v] = vsm[G::aCm + sub + 16 * v];
+  float sumgv = 0.f;
+  int par = 0;
+  const __amdgpu_buffer_rsrc_t rdA = ws_rsrc(wsdA, (long long)M * BN), rK = ws_rsrc(wsK, (long long)M * BN);
+
+  for (int t = blockIdx.x; t < nchunks; t += gridDim.x, par ^= 1) {
+    const int b = t / nch, i0 = (t - b * nch) * LTW;
+    const int nvalid = N - i0 < LTW ? N - i0 : LTW;
+    const long long col0 = (long long)b * N + i0;
+    float* sm = (float*)fresh_lds(vsm);
+    float* Kl = sm + G::aKl;
+    float* red = sm + G::aRed;
+    const float* zs = sm + G::aZs;
+    const float* zn = sm + G::aZn;
+    const float* vm = sm + G::aVm;
+    const float* sm1 = sm + G::aSm1;
+    float* rows = sm + G::aRows;
+    float* xs = sm + G::aXs;
+    float* xn = sm + G::aXn;
+    float* gmc = sm + G::aGm + par * LTW;
+    float* gvc = sm + G::aGv + par * LTW;
+    lstage_points<NPASS, DV, NT, DS>(xr, lsr, cmr, D, nvalid, xs, xn);
+    if (tid < LTW) {
+      const bool ok = tid < nvalid;
+      const float gm = gmean[ok ? col0 + tid : 0], gv = gvar[ok ? col0 + tid : 0];
+      gmc[tid] = ok ? gm : 0.f;
+      gvc[tid] = ok ? gv : 0.f;
+    }
+    lds_barrier();
+    // K tiles of the wave's rows (rows fed in the order pi: acc row g + 4r)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rt = h == 0 ? rA : rB;
+      if (h == 1 && !two) break;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const float* za = zs + (16 * rt + pi16(c)) * DS + g;
+        const float* xb = xs + (16 * ct + c) * DS + g;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < DQ / 4; ++k) acc = mfma32(za[4 * k], xb[4 * k], acc);
+        const int col = 16 * ct + c;
+        const float xnc = xn[col];
+        f32x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * rt + g + 4 * r;
+          float dist = zn[p] + xnc - 2.f * acc[r];
+          dist = dist < 0.f ? 0.f : dist;
+          o[r] = (p < M && col < nvalid) ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * dist) : 0.f;
+        }
+        *(f32x4*)(Kl + ((rt * 2 + ct) * 64 + lane) * 4) = o;
+      }
+    }
+    if (t + (int)gridDim.x < nchunks) lload_points<NPASS, DV, NT>(X, t + gridDim.x, nchunks, nch, N, D, xr);
+    lds_barrier();
+    f32x4 Af[2][2];
+    {
+      f64x4 aA[2], aB[2];
+      lreg_gemm_for<MB, 0>(wave, Lr, Kl, lane, aA, aB);
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          Af[0][ct][r] = (float)aA[ct][r];
+          Af[1][ct][r] = (float)aB[ct][r];
+        }
+    }
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      float vp = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const int rt = h == 0 ? rA : rB;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vp = __builtin_fmaf(Af[h][ct][r] * Af[h][ct][r], sm1[16 * rt + g + 4 * r], vp);
+      }
+      vp += __shfl_xor(vp, 16, 64);
+      vp += __shfl_xor(vp, 32, 64);
+      if (g == 0) red[wave * LTW + 16 * ct + c] = vp;
+    }
+    lds_barrier();
+    // clamp mask (the same fixed-order total on every wave), dA, row sums, workspace
+    float gmq[2], gvq[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int col = 16 * ct + c;
+      float vv = 0.f;
+#pragma unroll
+      for (int q = 0; q < NWV; ++q) vv += red[q * LTW + col];
+      gmq[ct] = gmc[col];
+      gvq[ct] = (s2 + jit + vv < 1e-6f) ? 0.f : gvc[col];   // clamp_min(1e-6): gradient masked
+      if (wave == 0 && g == 0) sumgv += gvq[ct];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int rt = h == 0 ? rA : rB;
+      const int voff = (int)(((long long)(16 * rt + g) * BN + col0 + c) * 4);
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const f32x4 kv = *(const f32x4*)(Kl + ((rt * 2 + ct) * 64 + lane) * 4);
+        const bool okc = 16 * ct + c < nvalid;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * rt + g + 4 * r;
+          const float da = gmq[ct] * vm[p] + 2.f * gvq[ct] * sm1[p] * Af[h][ct][r];
+          if (p < M && okc) {
+            buf_st(da, rdA, voff + 64 * ct, (int)(16 * r * BN));
+            buf_st(kv[r], rK, voff + 64 * ct, (int)(16 * r * BN));
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pm = 0.f, ps = 0.f;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          pm = __builtin_fmaf(gmq[ct], Af[h][ct][r], pm);
+          ps = __builtin_fmaf(gvq[ct], Af[h][ct][r] * Af[h][ct][r], ps);
+        }
+        pm = row16_sum_f(pm);
+        ps = row16_sum_f(ps);
+        if (c == 0) {
+          const int p = 16 * rt + g + 4 * r;
+          rows[p] += pm;
+          rows[G::MP + p] += ps;
+        }
+      }
+    }
+  }
+  lds_barrier();
+  // partial fields of this kernel: dvm (M) | dsm (M) | sumgv
+  const int P = M * D + 3 * M + 2 * D + 3;
+  float* po = wspart + (size_t)blockIdx.x * P;
+  for (int m = tid; m < M; m += NT) {
+    po[M * D + M + m] = vsm[G::aRows + m];
+    po[M * D + 2 * M + m] = vsm[G::aRows + G::MP + m];
+  }
+  if (wave == 0) {
+    const float v = row16_sum_f(sumgv);   // accumulated on lanes 0..15 only
+    if (lane == 0) po[M * D + 3 * M + D + 1] = v;
+  }
+}
+
+template <int MB, int DQ>
+__global__ void __launch_bounds__(64 * ((MB + 1) / 2), 2)
+gpk_var_adjk_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                      const double* __restrict__ Linv, const float* __restrict__ vmean,
+                      const float* __restrict__ vstd, const float* __restrict__ hyp,
+                      const float* __restrict__ gmean, int N, int M, int D, int nchunks,
+                      long long BN, const float* __restrict__ wsdA, const float* __restrict__ wsK,
+                      float* __restrict__ wspart, float* __restrict__ dX) {
+  using G = LAdjGeo<MB, DQ>;
+  constexpr int NWV = G::NWV, NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV, NDT = G::NDT;
+  constexpr int NLD = G::MP * LTW / NT;   // workspace elements per thread per array
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4, sub = tid & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pA = wave, pB = MB - 1 - wave;
+  const bool two = pB != pA;
+  const float* w = hyp + 4;
+  const float* ls = hyp + 4 + D;
+  const int nch = (N + LTW - 1) / LTW;
+
+  // L^{-1} column blocks, k-order g + 4u: slot s < MB - pA: (rt = pA + s, P = pA), then
+  // (rt = pB + s', P = pB);  Lc[s][u] = L^{-1}[16 rt + g + 4u][16 P + c]
+  double Lc[MB + 1][4];
+  {
+    const bool full = (M & 15) == 0;
+    const int NA = MB - pA;
+#pragma unroll
+    for (int s = 0; s <= MB; ++s) {
+      const bool isA = s < NA;
+      const int P = isA ? pA : pB, rt = isA ? pA + s : pB + (s - NA);
+      const bool ok = isA || (two && rt < MB);
+      const int col = 16 * P + c;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = 16 * rt + g + 4 * u;
+        const bool in = ok && (full || (row < M && col < M));
+        const double v = Linv[in ? (size_t)row * M + col : 0];
+        Lc[s][u] = in ? v : 0.0;
+      }
+      if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float lsr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) lsr[v] = ls[sub + 16 * v < D ? sub + 16 * v : 0];
+  float xr[NPASS][DV];
+  lload_points<NPASS, DV, NT>(X, blockIdx.x, nchunks, nch, N, D, xr);
+  stage_inducing(Z, ls, vmean, vstd, M, D, G::MP, DQ, DS, vsm + G::kZs, vsm + G::kZn, vsm + G::kCm,
+                 vsm + G::kVm, vsm + G::kSm1, vsm + G::kKl);
+  for (int e = tid; e < G::MP; e += NT) vsm[G::kQ + e] = 0.f;
+  lds_barrier();
+  float cmr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) cmr[v] = vsm[G::kCm + sub + 16 * v];
+  const __amdgpu_buffer_rsrc_t rdA = ws_rsrc(wsdA, (long long)M * BN), rK = ws_rsrc(wsK, (long long)M * BN);
+  const int dd = tid % DQ;   // the dX phase's dim for this thread (NT % DQ == 0)
+  const float il_dd = dd < D ? 1.f / ls[dd < D ? dd : 0] : 0.f;
+  const float w_dd = dd < D ? w[dd < D ? dd : 0] : 0.f;
+  float rx2 = 0.f, gxa = 0.f, sumQ = 0.f, sumgm = 0.f;
+  f32x4 qx[2][NDT];   // QX rows of the wave's blocks (p = 16 blk + 4g + r, d = 16 dt + c)
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) qx[h][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int par = 0;
+
+  for (int t = blockIdx.x; t < nchunks; t += gridDim.x, par ^= 1) {
+    const int b = t / nch, i0 = (t - b * nch) * LTW;
+    const int nvalid = N - i0 < LTW ? N - i0 : LTW;
+    const long long col0 = (long long)b * N + i0;
+    float* sm = (float*)fresh_lds(vsm);
+    float* Kl = sm + G::kKl;
+    float* dAl = sm + G::kdA;
+    float* xzl = sm + G::kXz;
+    float* red = sm + G::kRed;
+    const float* zs = sm + G::kZs;
+    float* qrow = sm + G::kQ;
+    float* scr = sm + G::kScr + wave * 320;
+    float* xs = sm + G::kXs + par * LTW * DS;
+    float* gmc = sm + G::kGm + par * LTW;
+    // ---- the chunk's dA / K rows (coalesced along points) -> LDS tiles; points; gmean
+    {
+      // thread -> point j = tid % 32 of rows m = tid / 32 + q NT / 32: one lane offset, the
+      // row step in the SGPR offset (rows >= M read past the array: zero by the bounds check)
+      // (two halves: 16 values per array in flight at most)
+      constexpr int NH = NLD > 8 ? 2 : 1, NQ = NLD / NH;
+      const int j = tid & (LTW - 1);
+      const int voff = (int)(((long long)(tid / LTW) * BN + col0 + j) * 4);
+#pragma unroll
+      for (int hh = 0; hh < NH; ++hh) {
+        float va[NQ], vk[NQ];
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          const int so = (int)((long long)(hh * NQ + qq) * (NT / LTW) * BN * 4);
+          va[qq] = buf_ld(rdA, voff, so);
+          vk[qq] = buf_ld(rK, voff, so);
+        }
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          const int q = hh * NQ + qq;
+          const int m = tid / LTW + q * (NT / LTW);
+          const bool ok = m < M && j < nvalid;
+          const int rt = m >> 4, mm = m & 15, ct = j >> 4, cc = j & 15;
+          const int o = ((rt * 2 + ct) * 64 + (mm & 3) * 16 + cc) * 4 + (mm >> 2);
+          dAl[o] = ok ? va[qq] : 0.f;
+          Kl[o] = ok ? vk[qq] : 0.f;
+        }
+      }
+    }
+    lstage_points<NPASS, DV, NT, DS>(xr, lsr, cmr, D, nvalid, xs, nullptr);
+    if (tid < LTW) {
+      const bool ok = tid < nvalid;
+      const float gm = gmean[ok ? col0 + tid : 0];
+      gmc[tid] = ok ? gm : 0.f;
+      sumgm += ok ? gm : 0.f;
+    }
+    if (t + (int)gridDim.x < nchunks) lload_points<NPASS, DV, NT>(X, t + gridDim.x, nchunks, nch, N, D, xr);
+    lds_barrier();
+    // ---- dK = L^{-T} dA on the wave's block rows; Q = dK o K
+    f32x4 Qt[2][2];
+    {
+      f64x4 dK[2][2];
+      lcol_gemm_for<MB, 0>(wave, Lc, dAl, lane, dK[0], dK[1]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rt = h == 0 ? pA : pB;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const f32x4 kv = *(const f32x4*)(Kl + ((rt * 2 + ct) * 64 + lane) * 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Qt[h][ct][r] = (h == 1 && !two) ? 0.f : (float)dK[h][ct][r] * kv[r];
+        }
+      }
+    }
+    // q_p row sums (rows owned by this wave), r_i partials, sum Q
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int rt = h == 0 ? pA : pB;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = row16_sum_f(Qt[h][0][r] + Qt[h][1][r]);
+        if (c == 0) qrow[16 * rt + g + 4 * r] += v;
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      float v = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) v += (Qt[h][ct][0] + Qt[h][ct][1]) + (Qt[h][ct][2] + Qt[h][ct][3]);
+      sumQ += v;
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) red[wave * LTW + 16 * ct + c] = v;
+    }
+    // Q^T zs (k = p, rows g + 4r): xz[ct][dt][r'] = sum_p Q[p][16 ct + 4g + r'] zs[p][16 dt + c]
+    {
+      f32x4 xz[2][NDT];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) xz[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const int rt = h == 0 ? pA : pB;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const float zb = zs[(16 * rt + g + 4 * r) * DS + 16 * dt + c];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) xz[ct][dt] = mfma32(Qt[h][ct][r], zb, xz[ct][dt]);
+          }
+      }
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            xzl[(wave * LTW + 16 * ct + 4 * g + r) * DQ + 16 * dt + c] = xz[ct][dt][r];
+    }
+    // QX_p += sum_i Q_pi xs_i: each Q tile transposed through the wave's scratch (k = point)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = Qt[h][ct][r];
+        wave_lds_sync();
+        float aq[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) aq[s] = scr[((c & 3) * 16 + 4 * s + g) * 5 + (c >> 2)];
+        wave_lds_sync();   // the next tile overwrites scr
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            qx[h][dt] = mfma32(aq[s], xs[(16 * ct + 4 * s + g) * DS + 16 * dt + c], qx[h][dt]);
+      }
+    }
+    lds_barrier();   // Q^T zs and r partials complete
+    // ---- dX_i = ((Q^T zs)_i - xs_i r_i) / l + gmean_i w; sum_i r_i xs_i^2, gmean_i xs_i
+    for (int e = tid; e < LTW * DQ; e += NT) {
+      const int col = e / DQ;
+      float v = 0.f, r = 0.f;
+#pragma unroll
+      for (int q = 0; q < NWV; ++q) {
+        v += xzl[(q * LTW + col) * DQ + dd];
+        r += red[q * LTW + col];
+      }
+      const float xv = xs[col * DS + dd];
+      if (col < nvalid && dd < D) {
+        dX[(col0 + col) * D + dd] = (v - xv * r) * il_dd + gmc[col] * w_dd;
+        rx2 = __builtin_fmaf(r * xv, xv, rx2);
+        gxa = __builtin_fmaf(gmc[col], xv, gxa);
+      }
+    }
+  }
+  lds_barrier();
+  // partial fields of this kernel: QX (M x D) | q (M) | rx2 (D) | sumQ | gx (D) | sumgm
+  const int P = M * D + 3 * M + 2 * D + 3;
+  float* po = wspart + (size_t)blockIdx.x * P;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 1 && !two) break;
+    const int rt = h == 0 ? pA : pB;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = 16 * rt + 4 * g + r, d = 16 * dt + c;
+        if (p < M && d < D) po[p * D + d] = qx[h][dt][r];
+      }
+  }
+  for (int m = tid; m < M; m += NT) po[M * D + m] = vsm[G::kQ + m];
+  float* misc = vsm + G::kMisc;
+  misc[tid] = rx2;
+  misc[NT + tid] = gxa;
+  sumQ = wave_sum(sumQ);
+  if (lane == 0) misc[2 * NT + wave] = sumQ;
+  lds_barrier();
+  for (int d = tid; d < D; d += NT) {
+    float v = 0.f, u = 0.f;
+    for (int q = d; q < NT; q += DQ) { v += misc[q]; u += misc[NT + q]; }
+    po[M * D + 3 * M + d] = v;
+    po[M * D + 3 * M + D + 2 + d] = u;
+  }
+  if (tid == 0) {
+    float v = 0.f;
+    for (int q = 0; q < NWV; ++q) v += misc[2 * NT + q];
+    po[M * D + 3 * M + D] = v;
+  }
+  if (wave == 0) {
+    const float u = wave_sum(sumgm);   // accumulated on lanes 0..LTW-1
+    if (lane == 0) po[M * D + 3 * M + 2 * D + 2] = u;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // dL^{-1} = sum_cols dA[:, col] K[:, col]^T (lower part): split-K fp64-MFMA GEMM.
 // Workgroup = one 64 x 64 lower output tile (ti >= tj) x one split of the columns;
 // 4 waves, each a 32 x 32 quadrant (2 x 2 MFMA tiles). fp32 operands are exact in fp64.
@@ -1586,14 +2233,10 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
   const int tid = threadIdx.x;
   const float s2 = hyp[0];
   const float* ls = hyp + 4 + D;
+  __shared__ float cms[kCmParts * 64];
   for (int e = tid; e < M * D; e += 256) fzs[e] = Z[e] / ls[e % D];
   lds_barrier();
-  for (int d = tid; d < D; d += 256) {
-    float sm = 0.f;  // the same fp32 sum as stage_inducing: the identical centre
-    for (int m = 0; m < M; ++m) sm += fzs[m * D + d];
-    cmf[d] = sm / (float)M;
-  }
-  lds_barrier();
+  col_means(fzs, M, D, D, D, cms, cmf);   // the same fp32 sums as stage_inducing: the identical centre
   for (int e = tid; e < M * D; e += 256) fzs[e] -= cmf[e % D];
   lds_barrier();
   const double* QX = tot;
@@ -1672,7 +2315,7 @@ GPK_DEVICE void stage_reg(const float* Z, const float* ls, const float* vmean, c
                           const double* Linv, int M, int D, float* sm) {
   using L = RegLds<DQ>;
   stage_inducing(Z, ls, vmean, vstd, M, D, 64, DQ, L::ZS, sm + L::zs, sm + L::zn, sm + L::cm,
-                 sm + L::vm, sm + L::sm1);
+                 sm + L::vm, sm + L::sm1, sm + L::li);   // (L^{-1} is staged afterwards)
   double* li = (double*)(sm + L::li);
   for (int base = 0; base < 64 * 64; base += 8 * (int)blockDim.x) {   // 8 loads in flight
     double v[8];
@@ -2294,10 +2937,27 @@ GPK_HOST_DEVICE_INLINE bool var_reg_path(int M, int D) { return GPK_VAR_REG && M
 
 AdjPlan adj_plan_common(AdjPlan p, int B, int N, int M, int D);
 
+template <int MB, int DQ>
+constexpr bool var_adj_lreg_fits() {
+  if constexpr (MB >= 5) return LAdjGeo<MB, DQ>::fits;
+  return false;
+}
+GPK_HOST_DEVICE_INLINE int adj_dq(int D) { return D <= 32 ? 32 : 64; }
+
 template <int MB>
 AdjPlan adj_plan(int B, int N, int M, int D) {
   using G = VarGeo<MB>;
   AdjPlan p{};
+  if constexpr (MB >= 5) {
+    const bool fits = adj_dq(D) == 32 ? var_adj_lreg_fits<MB, 32>() : var_adj_lreg_fits<MB, 64>();
+    const bool small_ws = (long long)M * B * N * 4 < (1LL << 31);   // 32-bit buffer offsets
+    if (GPK_VAR_LREG && M > 64 && fits && small_ws) {   // persistent, <= 2 waves / SIMD
+      const long long nch = (long long)B * ((N + LTW - 1) / LTW);
+      p.nchunks = (int)nch;
+      p.nwg = chunk_grid(nch, LAdjGeo<MB, 32>::NWV <= 4 ? 2 : 1);
+      return adj_plan_common(p, B, N, M, D);
+    }
+  }
   if (var_reg_path(M, D)) {
     const long long nch = (long long)B * ((N + 31) / 32);
     p.nchunks = (int)nch;
@@ -2370,6 +3030,26 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     return launch_var_adj_tail(a, p, stream);
+  }
+  if constexpr (var_adj_lreg_fits<MB, DQ>()) {
+    if (GPK_VAR_LREG && a.M > 64 && (long long)a.M * p.BN * 4 < (1LL << 31)) {
+      using LG = LAdjGeo<MB, DQ>;
+      set_lds_once<gpk_var_adja_l_kernel<MB, DQ>>();
+      set_lds_once<gpk_var_adjk_l_kernel<MB, DQ>>();
+      hipLaunchKernelGGL((gpk_var_adja_l_kernel<MB, DQ>), dim3(p.nwg), dim3(LG::NT),
+                         (size_t)LG::a_total * sizeof(float), stream, a.X, a.Z, a.Linv, a.vmean,
+                         a.vstd, a.hyp, a.gmean, a.gvar, a.N, a.M, a.D, p.nchunks, p.BN, wsdA, wsK,
+                         wspart);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return (int)e;
+      hipLaunchKernelGGL((gpk_var_adjk_l_kernel<MB, DQ>), dim3(p.nwg), dim3(LG::NT),
+                         (size_t)LG::k_total * sizeof(float), stream, a.X, a.Z, a.Linv, a.vmean,
+                         a.vstd, a.hyp, a.gmean, a.N, a.M, a.D, p.nchunks, p.BN, wsdA, wsK, wspart,
+                         a.dX);
+      e = hipGetLastError();
+      if (e != hipSuccess) return (int)e;
+      return launch_var_adj_tail(a, p, stream);
+    }
   }
   const size_t lds = var_adj_lds<MB, DQ>();
   if (lds > 160 * 1024) return -12;

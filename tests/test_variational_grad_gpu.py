@@ -100,7 +100,11 @@ def test_variance_clamp_gradient_mask(cuda_device):
         assert e <= TOL, (k, e)
 
 
-@pytest.mark.parametrize("B,N,M,D", [(8, 192, 256, 32), (16, 256, 64, 32), (5, 96, 256, 16)])
+@pytest.mark.parametrize("B,N,M,D", [(8, 192, 256, 32), (16, 256, 64, 32), (5, 96, 256, 16),
+                                     # M > 64 register-resident adjoint: every row-block
+                                     # count, ragged M / N, D up to the DQ = 64 variant
+                                     (3, 70, 100, 7), (2, 50, 96, 20), (2, 33, 180, 30),
+                                     (2, 41, 250, 32), (2, 45, 90, 40), (2, 30, 120, 64)])
 def test_variational_grads_reference_shapes(cuda_device, B, N, M, D):
     """The backward at the reference's GP shapes (M=256 default, DeepGP.py:15; cfg 5's
     M=64) on a window sample, every gradient block vs the fp64 oracle."""
