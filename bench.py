@@ -290,7 +290,10 @@ def main():
         raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # under torchrun the process group is created even at world size 1, so the RCCL
+    # init / barrier / MAX all-reduce path of the timed region runs on a one-GPU box too
+    pg = world > 1 or "RANK" in os.environ
+    if pg:
         dist.init_process_group("nccl", device_id=dev)
 
     N, D = args.N, args.D
@@ -324,7 +327,7 @@ def main():
     # launch adds 4-12 us of event overhead per 70 us kernel, and the same to the timed loop)
     acc = ObjectiveAccumulator(args.steps, dev, width=B)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -334,13 +337,13 @@ def main():
     ev1.record()
     totals, work = acc.reduce()
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     ops.check_cholesky_info(info, 1e-6, inputs=(X,))
-    if world > 1:
+    if pg:
         t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = (float(v) for v in t.tolist())
@@ -425,7 +428,8 @@ def main():
                                    "Cholesky + forward solve + MLL, L written; MLL partials "
                                    "all-reduced once per timed region",
                        "windows_per_gpu": B, "N": N, "D": D, "global_batch": B_total,
-                       "parallelism": f"window-sharded x{world}", "kernel": "gpk_exact_mll_f32"},
+                       "parallelism": f"window-sharded x{world}", "kernel": "gpk_exact_mll_f32",
+                       "process_group": "nccl" if pg else None},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": load_traffic(f"exact_B{B}_N{N}_D{D}"),
@@ -479,7 +483,7 @@ def main():
                     "sample": f"{sv} through oracle.variational_forward_torch_cpu (the reference's "
                               f"per-window fp64 K_ZZ Cholesky + TRSM), forward only"}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

@@ -34,6 +34,21 @@ def headers():
     return sorted(hs)
 
 
+def included(path, seen=None):
+    """Local headers a source pulls in (quoted #include, transitively): the object digest
+    covers exactly these, so editing one kernel's header does not rebuild every kernel."""
+    import re
+    seen = set() if seen is None else seen
+    base = os.path.dirname(path)
+    with open(path) as f:
+        for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+            h = os.path.normpath(os.path.join(base, m.group(1)))
+            if os.path.exists(h) and h not in seen:
+                seen.add(h)
+                included(h, seen)
+    return seen
+
+
 def _digest(paths, extra=""):
     h = hashlib.sha256(extra.encode())
     for p in paths:
@@ -49,13 +64,13 @@ def build(force: bool = False, verbose: bool = True, defines=(), out_dir: str = 
     os.makedirs(out_dir, exist_ok=True)
     lib_path = os.path.join(out_dir, "libgpk.so")
     flags = FLAGS + [f"-D{d}" for d in defines]
-    hdr_digest = _digest(headers(), " ".join(flags))
+    flag_str = " ".join(flags)
     objs = []
     jobs = []
     for src in sources():
         obj = os.path.join(out_dir, os.path.basename(src) + ".o")
         stamp = obj + ".sha"
-        dig = _digest([src], hdr_digest)
+        dig = _digest([src] + sorted(included(src)), flag_str)
         objs.append(obj)
         if not force and os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == dig:
             continue

@@ -38,6 +38,15 @@ SIGNATURES = {
                                         c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "gpk_kzz_chol_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_float, c_double, c_int,
                                  c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gpk_kzz_backward_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "gpk_kzz_backward_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                     c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gpk_gauss_ell_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                  c_void_p]),
+    "gpk_gauss_ell_grad_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gpk_meanfield_kl_f32": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
     "gpk_variational_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),

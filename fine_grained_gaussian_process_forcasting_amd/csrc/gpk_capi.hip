@@ -2,6 +2,8 @@
 // Declarations and the reference interfaces each entry point replaces: include/gpk.h.
 #include "../../include/gpk.h"
 #include "gpk_internal.h"
+#include "gpk_elbo.h"
+#include "gpk_kzz.h"
 
 extern "C" {
 
@@ -97,7 +99,67 @@ int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitte
   if (Linv == nullptr) return -9;
   if (info == nullptr) return -10;
   GpkKzzArgs a{Z, hyp, M, D, jitter, chol_jitter, max_tries, L, Linv, info};
-  return gpk_launch_kzz(a, (hipStream_t)stream);
+  return gpk_launch_kzz16(a, (hipStream_t)stream);
+}
+
+size_t gpk_kzz_backward_workspace_bytes(int M, int D) {
+  if (M < 1 || M > 256 || D < 1 || D > 64) return 0;
+  return gpk_kzz_grad_ws_bytes(M, D);
+}
+
+int gpk_kzz_backward_f64(const double* dLinv, const double* L, const double* Linv, const float* Z,
+                         const float* hyp, int M, int D, void* workspace, float* dZ, float* dhyp,
+                         void* stream) {
+  if (dLinv == nullptr) return -1;
+  if (L == nullptr) return -2;
+  if (Linv == nullptr) return -3;
+  if (Z == nullptr) return -4;
+  if (hyp == nullptr) return -5;
+  if (M < 1 || M > 256) return -6;
+  if (D < 1 || D > 64) return -7;
+  if (workspace == nullptr) return -8;
+  if (dZ == nullptr) return -9;
+  if (dhyp == nullptr) return -10;
+  GpkKzzGradArgs a{dLinv, L, Linv, Z, hyp, M, D, workspace, dZ, dhyp};
+  return gpk_launch_kzz_grad(a, (hipStream_t)stream);
+}
+
+int gpk_gauss_ell_f32(const float* y, const float* mean, const float* var, const float* noise, int R,
+                      int N, float* ell, void* stream) {
+  if (y == nullptr) return -1;
+  if (mean == nullptr) return -2;
+  if (var == nullptr) return -3;
+  if (noise == nullptr) return -4;
+  if (R < 0) return -5;
+  if (N < 1) return -6;
+  if (ell == nullptr) return -7;
+  if (R == 0) return 0;
+  return gpk_launch_ell(y, mean, var, noise, R, N, ell, (hipStream_t)stream);
+}
+
+int gpk_gauss_ell_grad_f32(const float* y, const float* mean, const float* var, const float* noise,
+                           const float* gell, int R, int N, float* dy, float* dmean, float* dvar,
+                           float* dnoise_part, void* stream) {
+  if (y == nullptr) return -1;
+  if (mean == nullptr) return -2;
+  if (var == nullptr) return -3;
+  if (noise == nullptr) return -4;
+  if (gell == nullptr) return -5;
+  if (R < 0) return -6;
+  if (N < 1) return -7;
+  if (R == 0) return 0;
+  return gpk_launch_ell_grad(y, mean, var, noise, gell, R, N, dy, dmean, dvar, dnoise_part,
+                             (hipStream_t)stream);
+}
+
+int gpk_meanfield_kl_f32(const float* m, const float* s, int M, float* kl, const float* gkl,
+                         float* dm, float* ds, void* stream) {
+  if (m == nullptr) return -1;
+  if (s == nullptr) return -2;
+  if (M < 1) return -3;
+  if (gkl == nullptr && kl == nullptr) return -4;
+  if (gkl != nullptr && (dm == nullptr || ds == nullptr)) return -6;
+  return gpk_launch_kl(m, s, M, kl, gkl, dm, ds, (hipStream_t)stream);
 }
 
 int gpk_variational_f32(const float* X, const float* Z, const double* Linv, const float* vmean,

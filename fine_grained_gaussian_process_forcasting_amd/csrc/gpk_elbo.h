@@ -1,0 +1,11 @@
+// Launchers of gpk_elbo.hip (the ELBO terms), for the C-ABI shim.
+#pragma once
+#include <hip/hip_runtime.h>
+
+int gpk_launch_ell(const float* y, const float* mean, const float* var, const float* noise, int R,
+                   int N, float* ell, hipStream_t stream);
+int gpk_launch_ell_grad(const float* y, const float* mean, const float* var, const float* noise,
+                        const float* gell, int R, int N, float* dy, float* dmean, float* dvar,
+                        float* dnoise_part, hipStream_t stream);
+int gpk_launch_kl(const float* m, const float* s, int M, float* kl, const float* gkl, float* dm,
+                  float* ds, hipStream_t stream);

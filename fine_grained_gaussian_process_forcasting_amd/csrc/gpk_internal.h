@@ -80,6 +80,21 @@ struct GpkVarAdjArgs {
 };
 
 int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream);
+struct GpkKzzGradArgs {
+  const double* dLinv; // (M, M) lower: dObjective/dLinv summed over the calls sharing the factor
+  const double* L;     // (M, M) gpk_kzz_chol_f64 factor (lower, zero upper)
+  const double* Linv;  // (M, M) its inverse (lower, zero upper)
+  const float* Z;      // (M, D)
+  const float* hyp;    // device: [outputscale, lengthscale[D]]
+  int M, D;
+  void* ws;            // gpk_kzz_grad_ws_bytes(M, D) bytes
+  float* dZ;           // (M, D) out
+  float* dhyp;         // (1 + D) out: {ds2, dlengthscale[D]}
+};
+
+size_t gpk_kzz_grad_ws_bytes(int M, int D);
+int gpk_launch_kzz_grad(const GpkKzzGradArgs& a, hipStream_t stream);
+
 size_t gpk_var_adjoint_ws_bytes(int B, int N, int M, int D);
 int gpk_launch_var_adjoint(const GpkVarAdjArgs& a, hipStream_t stream);
 int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream);

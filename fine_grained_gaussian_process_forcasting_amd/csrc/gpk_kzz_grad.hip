@@ -1,0 +1,253 @@
+// Adjoint of the shared K_ZZ factor (fp64), once per optimizer step.
+//
+// Reference: the autograd backward that train.py:166 runs through GPyTorch's
+// VariationalStrategy._cholesky_factor (psd_safe_cholesky of K_ZZ + jitter in fp64) and
+// the triangular solve L^{-1} K_ZX (denoising_model/DeepGP.py:33-38 via upstream
+// variational_strategy.py); oracle/gp_oracle.py restates the forward.
+//
+// Given G = dObjective/dLinv (lower, summed over every GP call that used the factor):
+//   T1   = G Linv^T                      (full)
+//   Lbar = -tril(Linv^T T1)              (= dObjective/dL)
+//   P    = Phi(L^T Lbar)                 (tril, diagonal halved)
+//   U    = P Linv                        (lower)
+//   S    = Linv^T U                      (full; Kbar = (S + S^T) / 2)
+//   W    = Kbar o s2 exp(-d2/2),  w1 = W 1,  Wz = W zs  (zs = Z / l, fp64)
+//   dZ   = 2 (Wz - zs o w1) / l,  dl_d = 2 (sum_i w1_i zs_id^2 - Wz_id zs_id) / l_d,
+//   ds2  = sum W / s2.
+// Kernels: gpk_kzzg_gemm_kernel<MODE> (one wave per 16 x 16 output tile, fp64 MFMA,
+// operands straight from L2 with a one-k-block register prefetch; triangular k-ranges),
+// gpk_kzzg_rbf_kernel (one wave per 16 x 16 tile of W: partial w1 / Wz per row and
+// column block), gpk_kzzg_fin_kernel (fixed-order sums -> dZ, ds2, dl: deterministic).
+#include "gpk_common.h"
+#include "gpk_internal.h"
+
+#include <mutex>
+
+namespace {
+
+GPK_DEVICE f64x4 mfma64(double a, double b, f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// lower tiles row-major: tile t -> (it, jt), jt <= it
+GPK_DEVICE void tri_tile(int t, int& it, int& jt) {
+  int r = (int)((__builtin_sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  while (r * (r + 1) / 2 > t) --r;
+  it = r;
+  jt = t - r * (r + 1) / 2;
+}
+
+// MODE 1: C = G Linv^T        A(i,k) = G[i][k] (k <= i)   B(k,j) = Linv[j][k]   kb in [0, min(ib, jb)]  full
+// MODE 2: C = -tril(Linv^T T1) A(i,k) = -Linv[k][i]        B(k,j) = T1[k][j]     kb in [ib, T)           lower
+// MODE 3: C = Phi(L^T Lbar)   A(i,k) = L[k][i]             B(k,j) = Lbar[k][j]   kb in [ib, T)           lower, diag / 2
+// MODE 4: C = P Linv          A(i,k) = P[i][k]             B(k,j) = Linv[k][j]   kb in [jb, ib]          lower
+// MODE 5: C = Linv^T U        A(i,k) = Linv[k][i]          B(k,j) = U[k][j]      kb in [max(ib,jb), T)   full
+template <int MODE>
+struct KzzGemm {
+  static constexpr bool kFull = MODE == 1 || MODE == 5;
+  static constexpr bool kTA = MODE == 2 || MODE == 3 || MODE == 5;   // A(i,k) read as X[k][i]
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(256)
+gpk_kzzg_gemm_kernel(const double* __restrict__ Am, const double* __restrict__ Bm, int M,
+                     double* __restrict__ C) {
+  using G = KzzGemm<MODE>;
+  const int T = (M + 15) >> 4;
+  const int ntile = G::kFull ? T * T : T * (T + 1) / 2;
+  const int t = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (t >= ntile) return;
+  int ib, jb;
+  if (G::kFull) {
+    ib = t / T;
+    jb = t - ib * T;
+  } else {
+    tri_tile(t, ib, jb);
+  }
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  int k_lo, k_hi;   // k-blocks [k_lo, k_hi]
+  if (MODE == 1) { k_lo = 0; k_hi = ib < jb ? ib : jb; }
+  else if (MODE == 4) { k_lo = jb; k_hi = ib; }
+  else { k_lo = ib > jb ? ib : jb; k_hi = T - 1; }
+  const int i = 16 * ib + c;          // A row of this lane
+  const int j = 16 * jb + c;          // B column of this lane
+  const bool iok = i < M, jok = j < M;
+
+  // operands of one 16-wide k-block: step s uses k = 16 kb + 4 s + g
+  auto load = [&](int kb, double (&a)[4], double (&b)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 16 * kb + 4 * s + g;
+      const bool kok = k < M;
+      const int kc = kok ? k : 0, ic = iok ? i : 0, jc = jok ? j : 0;
+      double av = G::kTA ? Am[(size_t)kc * M + ic] : Am[(size_t)ic * M + kc];
+      double bv = MODE == 1 ? Bm[(size_t)jc * M + kc] : Bm[(size_t)kc * M + jc];
+      if (MODE == 1 && k > i) av = 0.0;          // G = tril(dLinv)
+      a[s] = (iok && kok) ? (MODE == 2 ? -av : av) : 0.0;
+      b[s] = (jok && kok) ? bv : 0.0;
+    }
+  };
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  double a0[4], b0[4], a1[4], b1[4];
+  load(k_lo, a0, b0);
+  for (int kb = k_lo; kb <= k_hi; kb += 2) {
+    if (kb + 1 <= k_hi) load(kb + 1, a1, b1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma64(a0[s], b0[s], acc);
+    if (kb + 1 > k_hi) break;
+    if (kb + 2 <= k_hi) load(kb + 2, a0, b0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma64(a1[s], b1[s], acc);
+  }
+  // lane (c, g), reg r <-> C[16 ib + g + 4 r][16 jb + c]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ii = 16 * ib + g + 4 * r;
+    if (ii >= M || !jok) continue;
+    double v = acc[r];
+    if (!G::kFull && ib == jb) {
+      if (j > ii) v = 0.0;
+      if (MODE == 3 && j == ii) v *= 0.5;
+    }
+    C[(size_t)ii * M + j] = v;
+  }
+}
+
+// W tile (ib, jb): W_ij = (S_ij + S_ji)/2 * s2 exp(-d2_ij / 2). Per row i of the tile the
+// partial sums over j of this column block: part[(jb * M + i) * (D + 1) + {0: w1, 1 + d: Wz_d}].
+// One wave per tile; zs rows of both blocks staged in LDS as fp64.
+constexpr int kRbfMaxD = 64;
+__global__ void __launch_bounds__(64)
+gpk_kzzg_rbf_kernel(const double* __restrict__ S, const float* __restrict__ Z,
+                    const float* __restrict__ hyp, int M, int D, double* __restrict__ part) {
+  __shared__ double zi[16][kRbfMaxD + 1];
+  __shared__ double zj[16][kRbfMaxD + 1];
+  __shared__ double w[16][17];
+  const int T = (M + 15) >> 4;
+  const int ib = blockIdx.x / T, jb = blockIdx.x - (blockIdx.x / T) * T;
+  const int lane = threadIdx.x;
+  const double s2 = (double)hyp[0];
+  for (int e = lane; e < 16 * D; e += 64) {
+    const int r = e / D, d = e - r * D;
+    const int ii = 16 * ib + r, jj = 16 * jb + r;
+    const double l = (double)hyp[1 + d];
+    zi[r][d] = ii < M ? (double)Z[(size_t)ii * D + d] / l : 0.0;
+    zj[r][d] = jj < M ? (double)Z[(size_t)jj * D + d] / l : 0.0;
+  }
+  __syncthreads();
+  // 256 entries, 4 per lane: row r = lane >> 2 ... (entry e = lane + 64 q)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = lane + 64 * q, r = e >> 4, cc = e & 15;
+    const int ii = 16 * ib + r, jj = 16 * jb + cc;
+    double v = 0.0;
+    if (ii < M && jj < M) {
+      double d2 = 0.0;
+      for (int d = 0; d < D; ++d) {
+        const double df = zi[r][d] - zj[cc][d];
+        d2 = __builtin_fma(df, df, d2);
+      }
+      const double kbar = 0.5 * (S[(size_t)ii * M + jj] + S[(size_t)jj * M + ii]);
+      v = kbar * s2 * exp(-0.5 * d2);
+    }
+    w[r][cc] = v;
+  }
+  __syncthreads();
+  // row r = lane & 15, dims d = (lane >> 4) + 4 u
+  const int r = lane & 15, q4 = lane >> 4;
+  const int ii = 16 * ib + r;
+  if (ii >= M) return;
+  double* out = part + ((size_t)jb * M + ii) * (D + 1);
+  if (q4 == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) s += w[r][cc];
+    out[0] = s;
+  }
+  for (int d = q4; d < D; d += 4) {
+    double s = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) s = __builtin_fma(w[r][cc], zj[cc][d], s);
+    out[1 + d] = s;
+  }
+}
+
+// Fixed-order sums over the column blocks, then over the rows: dZ (M, D) float,
+// dhyp = {ds2, dl[D]} float. One workgroup, thread = row.
+__global__ void __launch_bounds__(256)
+gpk_kzzg_fin_kernel(const double* __restrict__ part, const float* __restrict__ Z,
+                    const float* __restrict__ hyp, int M, int D, float* __restrict__ dZ,
+                    float* __restrict__ dhyp) {
+  extern __shared__ double fsm[];   // (M) w1 | (M x D) row terms of dl
+  double* w1s = fsm;
+  double* rt = fsm + M;
+  const int T = (M + 15) >> 4;
+  for (int i = threadIdx.x; i < M; i += 256) {
+    double w1 = 0.0;
+    for (int jb = 0; jb < T; ++jb) w1 += part[((size_t)jb * M + i) * (D + 1)];
+    w1s[i] = w1;
+    for (int d = 0; d < D; ++d) {
+      double wz = 0.0;
+      for (int jb = 0; jb < T; ++jb) wz += part[((size_t)jb * M + i) * (D + 1) + 1 + d];
+      const double l = (double)hyp[1 + d];
+      const double z = (double)Z[(size_t)i * D + d] / l;
+      dZ[(size_t)i * D + d] = (float)(2.0 * (wz - z * w1) / l);
+      rt[(size_t)i * D + d] = w1 * z * z - wz * z;
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < D) {
+    const int d = threadIdx.x;
+    double s = 0.0;
+    for (int i = 0; i < M; ++i) s += rt[(size_t)i * D + d];
+    dhyp[1 + d] = (float)(2.0 * s / (double)hyp[1 + d]);
+  }
+  if (threadIdx.x == 64) {
+    double s = 0.0;
+    for (int i = 0; i < M; ++i) s += w1s[i];
+    dhyp[0] = (float)(s / (double)hyp[0]);
+  }
+}
+
+template <int MODE>
+hipError_t launch_gemm(const double* A, const double* B, int M, double* C, hipStream_t stream) {
+  const int T = (M + 15) >> 4;
+  const int ntile = KzzGemm<MODE>::kFull ? T * T : T * (T + 1) / 2;
+  hipLaunchKernelGGL((gpk_kzzg_gemm_kernel<MODE>), dim3((ntile + 3) / 4), dim3(256), 0, stream, A, B,
+                     M, C);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t gpk_kzz_grad_ws_bytes(int M, int D) {
+  const int T = (M + 15) >> 4;
+  return (2 * (size_t)M * M + (size_t)T * M * (D + 1)) * sizeof(double);
+}
+
+int gpk_launch_kzz_grad(const GpkKzzGradArgs& a, hipStream_t stream) {
+  const int M = a.M, D = a.D;
+  double* b0 = (double*)a.ws;
+  double* b1 = b0 + (size_t)M * M;
+  double* part = b1 + (size_t)M * M;
+  hipError_t e;
+  if ((e = launch_gemm<1>(a.dLinv, a.Linv, M, b0, stream)) != hipSuccess) return (int)e;   // T1
+  if ((e = launch_gemm<2>(a.Linv, b0, M, b1, stream)) != hipSuccess) return (int)e;        // Lbar
+  if ((e = launch_gemm<3>(a.L, b1, M, b0, stream)) != hipSuccess) return (int)e;           // P
+  if ((e = launch_gemm<4>(b0, a.Linv, M, b1, stream)) != hipSuccess) return (int)e;        // U
+  if ((e = launch_gemm<5>(a.Linv, b1, M, b0, stream)) != hipSuccess) return (int)e;        // S
+  const int T = (M + 15) >> 4;
+  hipLaunchKernelGGL(gpk_kzzg_rbf_kernel, dim3(T * T), dim3(64), 0, stream, b0, a.Z, a.hyp, M, D, part);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  static std::once_flag once;   // fin needs M (D + 1) doubles of LDS (up to 133 KB)
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute((const void*)gpk_kzzg_fin_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();
+  });
+  hipLaunchKernelGGL(gpk_kzzg_fin_kernel, dim3(1), dim3(256), (size_t)M * (D + 1) * sizeof(double), stream,
+                     part, a.Z, a.hyp, M, D, a.dZ, a.dhyp);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}

@@ -2519,7 +2519,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
                      const double* __restrict__ Linv, const float* __restrict__ vmean,
                      const float* __restrict__ vstd, const float* __restrict__ hyp,
                      const float* __restrict__ gmean, const float* __restrict__ gvar, int B, int N,
-                     int M, int D, long long BN, float* __restrict__ wsdA, float* __restrict__ wsK,
+                     int M, int D, long long BN, float* __restrict__ wsgv,
                      float* __restrict__ wspart, float* __restrict__ dX) {
   using L = RegLds<DQ>;
   constexpr int NDT = DQ / 16;
@@ -2616,22 +2616,13 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
           rows[64 + p] += ps;
         }
       }
-    // dA and K_ZX -> workspace (for dL^{-1} = sum dA K^T)
+    // the clamp-masked gvar -> workspace: dL^{-1} = vm u^T + 2 (s^2 - 1) o L^{-1} G with
+    // u = sum gmean K_ZX, G = K_ZX diag(gvar) K_ZX^T (gpk_var_kgram_r_kernel), so neither
+    // dA nor K_ZX makes an HBM round trip
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int i = i0 + 16 * q + c;
-      if (i < N) {
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int p = 16 * rt + g + 4 * r;
-            if (p < M) {
-              wsdA[(size_t)p * BN + col0 + i] = dA[rt][q][r];
-              wsK[(size_t)p * BN + col0 + i] = K[rt][q][r];
-            }
-          }
-      }
+      if (i < N && g == 0) wsgv[col0 + i] = gvq[q];
     }
     // dK = L^{-T} dA (fp64; L^{-T} upper: kb >= rt), then Q = dK o K_ZX (in K's registers)
 #pragma unroll
@@ -2834,6 +2825,162 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 }
 
 // ---------------------------------------------------------------------------
+// dL^{-1} of the register path (M <= 64) without the dA / K_ZX workspace. With
+// dA = gmean m^T-terms + 2 gvar (s^2 - 1) o A and A = L^{-1} K_ZX:
+//   dL^{-1} = sum_i dA_i K_i^T = vm u^T + 2 diag(s^2 - 1) L^{-1} G,
+//   u = sum_i gmean_i K_i,  G = sum_i gvar_i K_i K_i^T     (gvar clamp-masked by the adjoint)
+// so only K_ZX is needed, recomputed here in the TRANSPOSED orientation (points on the
+// rows of each f32 acc tile), which makes sum_s mfma(Q.reg[s], P.reg[s]) = Q^T P the
+// point contraction: the 10 lower 16 x 16 tiles of G accumulate in registers (fp32 per
+// wave, fp64 across waves / workgroups). Partials per workgroup:
+//   [G lower tiles (10 x 256, acc order) | u (64)].
+// ---------------------------------------------------------------------------
+constexpr int kGTiles = 10;                  // lower 16 x 16 tiles of a 64 x 64 G
+constexpr int kGPart = kGTiles * 256 + 64;   // floats per workgroup partial
+
+template <int DQ>
+__global__ void __launch_bounds__(256, 2)
+gpk_var_kgram_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                       const float* __restrict__ vmean, const float* __restrict__ vstd,
+                       const float* __restrict__ hyp, const float* __restrict__ gmean,
+                       const float* __restrict__ wsgv, int B, int N, int M, int D,
+                       float* __restrict__ gpart) {
+  using L = RegLds<DQ>;
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const float s2 = hyp[0];
+  const float* ls = hyp + 4 + D;
+  stage_inducing(Z, ls, vmean, vstd, M, D, 64, DQ, L::ZS, vsm + L::zs, vsm + L::zn, vsm + L::cm,
+                 vsm + L::vm, vsm + L::sm1, vsm + L::li);
+  lds_barrier();
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int wave = tid >> 6;
+  float il[DQ / 4], cmv[DQ / 4], wv[DQ / 4];
+  dim_consts<DQ>(vsm, ls, nullptr, D, il, cmv, wv);
+  f32x4 G[kGTiles];
+#pragma unroll
+  for (int t = 0; t < kGTiles; ++t) G[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float u[4] = {0.f, 0.f, 0.f, 0.f};
+  const int nch = (N + 31) / 32;
+  const long long total = (long long)B * nch;
+  for (long long t = (long long)blockIdx.x * 4 + wave; t < total; t += (long long)gridDim.x * 4) {
+    const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
+    const size_t col0 = (size_t)b * N;
+    const float* sm = fresh_lds(vsm);
+    const float* zs = sm + L::zs;
+    const float* zn = sm + L::zn;
+    RegPoints<DQ> P;
+    load_points<DQ, false>(X, N, D, b, i0, il, cmv, wv, P);
+    // per-register point weights (point 16 q + 4 g + r), requested up front
+    float gvr[2][4], gmr[2][4];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + 16 * q + 4 * g + r;
+        const size_t e = col0 + (i < N ? i : 0);
+        gvr[q][r] = wsgv[e];
+        gmr[q][r] = gmean[e];
+      }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float xn[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xn[r] = __shfl(P.xn[q], 4 * g + r, 64);
+      // K^T tiles: rows = points 16 q + 4 g + r, columns = inducing points 16 rt + c
+      f32x4 KT[4], W[4];
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < DQ / 4; ++s) acc = mfma32(P.xb[q][s], zs[(16 * rt + c) * L::ZS + 4 * s + g], acc);
+        const int p = 16 * rt + c;
+        const float znp = zn[p];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = (i0 + 16 * q + 4 * g + r < N) && p < M;
+          const float d2 = __builtin_fmaxf(znp + xn[r] - 2.f * acc[r], 0.f);
+          const float kv = ok ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * d2) : 0.f;
+          KT[rt][r] = kv;
+          W[rt][r] = kv * gvr[q][r];
+          u[rt] = __builtin_fmaf(gmr[q][r], kv, u[rt]);
+        }
+      }
+      // G(rt, rt') += K_rt diag(gv) K_rt'^T = sum_s mfma(KT_rt.reg[s], W_rt'.reg[s])
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int rp = 0; rp <= rt; ++rp)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            G[rt * (rt + 1) / 2 + rp] = mfma32(KT[rt][s], W[rp][s], G[rt * (rt + 1) / 2 + rp]);
+    }
+  }
+  // workgroup partial: the 4 waves summed in a fixed order through LDS (the staging area is free)
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt) {
+    u[rt] += __shfl_xor(u[rt], 16, 64);
+    u[rt] += __shfl_xor(u[rt], 32, 64);
+  }
+  float* red = vsm;   // kGPart floats
+  for (int wv2 = 0; wv2 < 4; ++wv2) {
+    lds_barrier();
+    if (wave == wv2) {
+#pragma unroll
+      for (int t2 = 0; t2 < kGTiles; ++t2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int e = t2 * 256 + r * 64 + lane;
+          red[e] = (wv2 == 0 ? 0.f : red[e]) + G[t2][r];
+        }
+      if (g == 0) {
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          const int e = kGTiles * 256 + 16 * rt + c;
+          red[e] = (wv2 == 0 ? 0.f : red[e]) + u[rt];
+        }
+      }
+    }
+  }
+  lds_barrier();
+  float* po = gpart + (size_t)blockIdx.x * kGPart;
+  for (int e = tid; e < kGPart; e += 256) po[e] = red[e];
+}
+
+// dL^{-1}[p][k] = vm_p u_k + 2 (s_p^2 - 1) sum_{j <= p} L^{-1}[p][j] G[j][k]  (k <= p < M;
+// upper zero) from the reduced totals (fp64). One workgroup.
+__global__ void __launch_bounds__(256)
+gpk_var_gdl_kernel(const double* __restrict__ gtot, const double* __restrict__ Linv,
+                   const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
+                   double* __restrict__ dLinv) {
+  __shared__ double Gs[64][65];
+  __shared__ double us[64];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < kGTiles * 256; e += 256) {   // acc order: tile, reg r, lane (c, g)
+    const int t2 = e >> 8, r = (e >> 6) & 3, ln = e & 63;
+    int rt = 0;
+    while ((rt + 1) * (rt + 2) / 2 <= t2) ++rt;
+    const int rp = t2 - rt * (rt + 1) / 2;
+    const int row = 16 * rt + 4 * (ln >> 4) + r, col = 16 * rp + (ln & 15);   // f32 acc: row 4g + r
+    if (rt == rp && row < col) continue;   // one writer per element: deterministic
+    Gs[row][col] = gtot[e];
+    Gs[col][row] = gtot[e];
+  }
+  for (int e = tid; e < 64; e += 256) us[e] = gtot[kGTiles * 256 + e];
+  lds_barrier();
+  for (int e = tid; e < M * M; e += 256) {
+    const int p = e / M, k = e - p * M;
+    double v = 0.0;
+    if (k <= p) {
+      double a = 0.0;
+      for (int j = 0; j <= p; ++j) a = __builtin_fma(Linv[(size_t)p * M + j], Gs[j][k], a);
+      const double sd = (double)vstd[p];
+      v = (double)vmean[p] * us[k] + 2.0 * (sd * sd - 1.0) * a;
+    }
+    dLinv[e] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 template <int MB>
@@ -2959,10 +3106,20 @@ AdjPlan adj_plan(int B, int N, int M, int D) {
     }
   }
   if (var_reg_path(M, D)) {
+    // workspace: masked gvar (BN) | K-Gram partials (nwg x kGPart) | their fp64 totals
     const long long nch = (long long)B * ((N + 31) / 32);
     p.nchunks = (int)nch;
     p.nwg = (int)((nch + 3) / 4 < 512 ? (nch + 3) / 4 : 512);
-    return adj_plan_common(p, B, N, M, D);
+    p = adj_plan_common(p, B, N, M, D);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t o = 0;
+    p.off_dA = o; o = al(o + (size_t)p.BN * sizeof(float));
+    p.off_K = o; o = al(o + (size_t)p.nwg * kGPart * sizeof(float));
+    p.off_part = o; o = al(o + (size_t)p.nwg * p.P * sizeof(float));
+    p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
+    p.off_dl = o; o = al(o + (size_t)kGPart * sizeof(double));
+    p.total = o;
+    return p;
   }
   p.nchunks = B * ((N + G::TW - 1) / G::TW);
   p.nwg = chunk_grid(p.nchunks, 2);
@@ -3022,14 +3179,37 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
   float* wspart = (float*)(ws + p.off_part);
   if (var_reg_path(a.M, a.D)) {
     constexpr int RQ = DQ <= 16 ? 16 : 32;
+    float* wsgv = wsdA;
+    float* gpart = wsK;
+    double* gtot = (double*)(ws + p.off_dl);
+    double* tot = (double*)(ws + p.off_tot);
     const size_t lds = (size_t)RegLds<RQ>::adj_total * sizeof(float);
     set_lds_once<gpk_var_adj_r_kernel<RQ>>();
     hipLaunchKernelGGL((gpk_var_adj_r_kernel<RQ>), dim3(p.nwg), dim3(256), lds, stream, a.X, a.Z,
                        a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.B, a.N, a.M, a.D, p.BN,
-                       wsdA, wsK, wspart, a.dX);
-    const hipError_t e = hipGetLastError();
+                       wsgv, wspart, a.dX);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    return launch_var_adj_tail(a, p, stream);
+    set_lds_once<gpk_var_kgram_r_kernel<RQ>>();
+    hipLaunchKernelGGL((gpk_var_kgram_r_kernel<RQ>), dim3(p.nwg), dim3(256),
+                       (size_t)RegLds<RQ>::fwd_total * sizeof(float), stream, a.X, a.Z, a.vmean, a.vstd,
+                       a.hyp, a.gmean, wsgv, a.B, a.N, a.M, a.D, gpart);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    // fixed-order sums: K-Gram partials -> gtot, adjoint partials -> tot (section (a) only)
+    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((kGPart + 31) / 32), dim3(256), 0, stream, gpart, p.nwg,
+                       kGPart, gtot, nullptr, 0, 0, 0, nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.P + 31) / 32), dim3(256), 0, stream, wspart, p.nwg,
+                       p.P, tot, nullptr, 0, 0, 0, nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(gpk_var_gdl_kernel, dim3(1), dim3(256), 0, stream, gtot, a.Linv, a.vmean, a.vstd,
+                       a.M, a.dLinv);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    set_lds_once<gpk_var_fin_kernel, 64 * 1024>();
+    hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(1), dim3(256), p.fin_lds, stream, a.Z, a.vstd, a.hyp,
+                       tot, a.M, a.D, a.dZ, a.dpar);
+    e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
   }
   if constexpr (var_adj_lreg_fits<MB, DQ>()) {
     if (GPK_VAR_LREG && a.M > 64 && (long long)a.M * p.BN * 4 < (1LL << 31)) {

@@ -291,6 +291,20 @@ class GaussianLikelihood(nn.Module):
         res = ((target - mean) ** 2 + variance) / noise + noise.log() + LOG_2PI
         return res.mul(-0.5)
 
+    def expected_log_prob_sum(self, target: torch.Tensor, input: MultivariateNormal) -> torch.Tensor:
+        """expected_log_prob(target, input).sum(-1) -- what VariationalELBO reads -- as ONE
+        gfx950 launch forward and one backward (gpk::gauss_ell) instead of ~10 elementwise
+        kernels each way; the per-point form above stays GPyTorch's API."""
+        mean, variance = input.mean, input.variance
+        if not (mean.is_cuda and mean.dtype == torch.float32 and variance.shape == mean.shape):
+            return self.expected_log_prob(target, input).sum(-1)
+        shape = mean.shape
+        N = shape[-1]
+        y = torch.broadcast_to(target, shape).to(torch.float32)
+        ell = torch.ops.gpk.gauss_ell(y.reshape(-1, N), mean.reshape(-1, N), variance.reshape(-1, N),
+                                      self.noise.reshape(1))
+        return ell.reshape(shape[:-1])
+
 
 # ---------------------------------------------------------------------------
 # variational distribution / strategy (upstream variational/*.py, whitened)
@@ -311,9 +325,13 @@ class MeanFieldVariationalDistribution(nn.Module):
             self._variational_stddev.data.fill_(1.0)
 
     def kl_divergence(self) -> torch.Tensor:
-        """KL(N(m, diag s^2) || N(0, I)) = 1/2 (sum s^2 + sum m^2 - M - sum log s^2)."""
+        """KL(N(m, diag s^2) || N(0, I)) = 1/2 (sum s^2 + sum m^2 - M - sum log s^2)
+        (one gfx950 launch each way, gpk::meanfield_kl, for the unbatched fp32 layer)."""
         m = self.variational_mean
-        s2 = self._variational_stddev.pow(2)
+        s = self._variational_stddev
+        if m.is_cuda and m.dim() == 1 and m.dtype == torch.float32:
+            return torch.ops.gpk.meanfield_kl(m, s).reshape(())
+        s2 = s.pow(2)
         return 0.5 * (s2.sum(-1) + m.pow(2).sum(-1) - m.shape[-1] - s2.log().sum(-1))
 
 
@@ -408,6 +426,8 @@ class _ApproximateMarginalLogLikelihood(nn.Module):
 
 class VariationalELBO(_ApproximateMarginalLogLikelihood):
     def _log_likelihood_term(self, variational_dist_f, target, **kwargs):
+        if hasattr(self.likelihood, "expected_log_prob_sum"):
+            return self.likelihood.expected_log_prob_sum(target, variational_dist_f)
         return self.likelihood.expected_log_prob(target, variational_dist_f).sum(-1)
 
 

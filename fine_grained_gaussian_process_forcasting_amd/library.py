@@ -10,14 +10,16 @@ instead of being opaque Python. Each op is one C-ABI call of include/gpk.h on
   gpk::exact_mll_grad(X, L, z, hyper, gout) -> (dX, dy, dhyp)
   gpk::exact_posterior(X, L, z, hyper, Xs) -> (mean, var)                     [eval only]
   gpk::kzz_factor(Z, s2, ls, jitter, chol_jitter, max_tries) -> (Linv, L, info) [autograd]
-  gpk::variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter) -> (mean, var, flags)
+  gpk::variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter) -> (mean, var, flags, hyper)
                                                                                [autograd]
-  gpk::variational_adj(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter, gmean, gvar)
-      -> (dX, dLinv, dZ, dvmean, dvstd, ds2, dls, dw, db0)
+  gpk::variational_adj(x, Linv, Z, vmean, vstd, hyper, gmean, gvar) -> (dX, dLinv, dZ, dpar)
+  gpk::gauss_ell(y, mean, var, noise) -> ell (R,)                             [autograd]
+  gpk::meanfield_kl(m, s) -> kl (1,)                                          [autograd]
 
 Reference call sites they serve: GPModel.py:10-13 + ExactMarginalLogLikelihood
-(exact_mll), ExactGPModel in eval mode (exact_posterior), DeepGP.py:33-73 VariationalStrategy (kzz_factor, variational_fwd), and
-the backward of train.py:166 (the *_grad / *_adj ops).
+(exact_mll), ExactGPModel in eval mode (exact_posterior), DeepGP.py:33-73 VariationalStrategy (kzz_factor, variational_fwd),
+the ELBO at forecast_denoising.py:86-89 (gauss_ell, meanfield_kl), and the backward of
+train.py:166 (the *_grad / *_adj ops).
 """
 from __future__ import annotations
 
@@ -149,58 +151,134 @@ def _var_hyper(x, s2, ls, w, b0, jitter):
 
 @torch.library.custom_op("gpk::variational_fwd", mutates_args=(), device_types="cuda")
 def variational_fwd(x: Tensor, Linv: Tensor, Z: Tensor, vmean: Tensor, vstd: Tensor, s2: Tensor,
-                    ls: Tensor, w: Tensor, b0: Tensor, jitter: float) -> Tuple[Tensor, Tensor, Tensor]:
-    out = ops.variational_forward(x, Z, Linv, vmean, vstd, hyper=_var_hyper(x, s2, ls, w, b0, jitter))
-    return out.mean, out.var, out.flags
+                    ls: Tensor, w: Tensor, b0: Tensor, jitter: float) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """-> (mean, var, clamp flags, packed hyper vector). The hyper vector is returned so the
+    backward reuses it (one pack per GP call, not one per direction)."""
+    hyper = _var_hyper(x, s2, ls, w, b0, jitter)
+    out = ops.variational_forward(x, Z, Linv, vmean, vstd, hyper=hyper)
+    return out.mean, out.var, out.flags, hyper
 
 
 @variational_fwd.register_fake
 def _(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter):
-    B, N, _ = x.shape
-    return x.new_empty(B, N), x.new_empty(B, N), x.new_empty(1, dtype=torch.int32)
+    B, N, D = x.shape
+    return (x.new_empty(B, N), x.new_empty(B, N), x.new_empty(1, dtype=torch.int32),
+            x.new_empty(4 + 2 * D))
 
 
 @torch.library.custom_op("gpk::variational_adj", mutates_args=(), device_types="cuda")
-def variational_adj(x: Tensor, Linv: Tensor, Z: Tensor, vmean: Tensor, vstd: Tensor, s2: Tensor,
-                    ls: Tensor, w: Tensor, b0: Tensor, jitter: float, gmean: Tensor,
-                    gvar: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor,
-                                           Tensor, Tensor]:
+def variational_adj(x: Tensor, Linv: Tensor, Z: Tensor, vmean: Tensor, vstd: Tensor, hyper: Tensor,
+                    gmean: Tensor, gvar: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """-> (dX, dLinv, dZ (K_ZX part), dpar = [dvmean (M), dvstd (M), ds2, dls (D), dw (D), db0])."""
     B, N, D = x.shape
-    adj = ops.variational_adjoint(x, Z, Linv, vmean, vstd, _var_hyper(x, s2, ls, w, b0, jitter),
-                                  gmean, gvar)
-    dw, db0 = adj.dw, adj.db0                                        # LinearMean (in-kernel)
-    dls = adj.dls.sum().reshape(ls.shape) if ls.numel() == 1 else adj.dls.reshape(ls.shape)
-    return (adj.dX.to(x.dtype), adj.dLinv, adj.dZ.to(Z.dtype),
-            adj.dvmean.reshape(vmean.shape).to(vmean.dtype).clone(),
-            adj.dvstd.reshape(vstd.shape).to(vstd.dtype).clone(),
-            adj.ds2.reshape(s2.shape).to(s2.dtype).clone(), dls.to(ls.dtype).clone(),
-            dw.reshape(w.shape).to(w.dtype).clone(), db0.reshape(b0.shape).to(b0.dtype).clone())
+    M = Z.shape[0]
+    adj = ops.variational_adjoint(x, Z, Linv, vmean, vstd, hyper, gmean, gvar)
+    return adj.dX, adj.dLinv, adj.dZ, adj.dpar
 
 
 @variational_adj.register_fake
-def _(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter, gmean, gvar):
-    return (torch.empty_like(x), torch.empty_like(Linv), torch.empty_like(Z), torch.empty_like(vmean),
-            torch.empty_like(vstd), torch.empty_like(s2), torch.empty_like(ls), torch.empty_like(w),
-            torch.empty_like(b0))
+def _(x, Linv, Z, vmean, vstd, hyper, gmean, gvar):
+    M, D = Z.shape
+    return (torch.empty_like(x), torch.empty_like(Linv), torch.empty_like(Z),
+            x.new_empty(2 * M + 2 * D + 2))
 
 
 def _var_setup(ctx, inputs, output):
     x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter = inputs
-    ctx.jitter = jitter
-    ctx.save_for_backward(x, Linv, Z, vmean, vstd, s2, ls, w, b0)
-    ctx.mark_non_differentiable(output[2])
+    ctx.save_for_backward(x, Linv, Z, vmean, vstd, s2, ls, w, b0, output[3])
+    ctx.mark_non_differentiable(output[2], output[3])
 
 
-def _var_backward(ctx, gmean, gvar, _gflags):
-    x, Linv, Z, vmean, vstd, s2, ls, w, b0 = ctx.saved_tensors
-    B, N, _ = x.shape
+def _var_backward(ctx, gmean, gvar, _gflags, _ghyper):
+    x, Linv, Z, vmean, vstd, s2, ls, w, b0, hyper = ctx.saved_tensors
+    B, N, D = x.shape
+    M = Z.shape[0]
     if gmean is None:
         gmean = x.new_zeros(B, N)
     if gvar is None:
         gvar = x.new_zeros(B, N)
-    grads = torch.ops.gpk.variational_adj(x, Linv, Z, vmean, vstd, s2, ls, w, b0, ctx.jitter,
-                                          gmean.contiguous(), gvar.contiguous())
-    return (*grads, None)
+    dX, dLinv, dZ, dpar = torch.ops.gpk.variational_adj(x, Linv, Z, vmean, vstd, hyper,
+                                                        gmean.contiguous(), gvar.contiguous())
+    dls = dpar[2 * M + 1:2 * M + 1 + D]
+    dls = dls.sum().reshape(ls.shape) if ls.numel() == 1 else dls.reshape(ls.shape)
+    return (dX, dLinv, dZ, dpar[:M].reshape(vmean.shape), dpar[M:2 * M].reshape(vstd.shape),
+            dpar[2 * M].reshape(s2.shape), dls, dpar[2 * M + 1 + D:2 * M + 1 + 2 * D].reshape(w.shape),
+            dpar[2 * M + 1 + 2 * D].reshape(b0.shape), None)
 
 
 variational_fwd.register_autograd(_var_backward, setup_context=_var_setup)
+
+# ---------------------------------------------------------------------------
+# ELBO terms (gpk_gauss_ell_f32 / gpk_meanfield_kl_f32)
+# ---------------------------------------------------------------------------
+
+
+@torch.library.custom_op("gpk::gauss_ell", mutates_args=(), device_types="cuda")
+def gauss_ell(y: Tensor, mean: Tensor, var: Tensor, noise: Tensor) -> Tensor:
+    """(R,) sums over N of GaussianLikelihood.expected_log_prob for (R, N) rows."""
+    return ops.gauss_ell(y.contiguous().float(), mean.contiguous().float(), var.contiguous().float(),
+                         noise.reshape(1).contiguous().float())
+
+
+@gauss_ell.register_fake
+def _(y, mean, var, noise):
+    return mean.new_empty(mean.shape[0])
+
+
+@torch.library.custom_op("gpk::gauss_ell_grad", mutates_args=(), device_types="cuda")
+def gauss_ell_grad(y: Tensor, mean: Tensor, var: Tensor, noise: Tensor,
+                   gell: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    return ops.gauss_ell_grad(y.contiguous().float(), mean.contiguous().float(), var.contiguous().float(),
+                              noise.reshape(1).contiguous().float(), gell.contiguous().float())
+
+
+@gauss_ell_grad.register_fake
+def _(y, mean, var, noise, gell):
+    return (torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean), mean.new_empty(1))
+
+
+def _ell_setup(ctx, inputs, output):
+    ctx.save_for_backward(*inputs)
+
+
+def _ell_backward(ctx, gell):
+    y, mean, var, noise = ctx.saved_tensors
+    dy, dmean, dvar, dnoise = torch.ops.gpk.gauss_ell_grad(y, mean, var, noise, gell.contiguous())
+    return dy, dmean, dvar, dnoise.reshape(noise.shape)
+
+
+gauss_ell.register_autograd(_ell_backward, setup_context=_ell_setup)
+
+
+@torch.library.custom_op("gpk::meanfield_kl", mutates_args=(), device_types="cuda")
+def meanfield_kl(m: Tensor, s: Tensor) -> Tensor:
+    """(1,) KL(N(m, diag s^2) || N(0, I)) of the whitened mean-field q(u)."""
+    return ops.meanfield_kl(m.contiguous().float(), s.contiguous().float())
+
+
+@meanfield_kl.register_fake
+def _(m, s):
+    return m.new_empty(1)
+
+
+@torch.library.custom_op("gpk::meanfield_kl_grad", mutates_args=(), device_types="cuda")
+def meanfield_kl_grad(m: Tensor, s: Tensor, gkl: Tensor) -> Tuple[Tensor, Tensor]:
+    return ops.meanfield_kl_grad(m.contiguous().float(), s.contiguous().float(), gkl.reshape(1).contiguous().float())
+
+
+@meanfield_kl_grad.register_fake
+def _(m, s, gkl):
+    return torch.empty_like(m), torch.empty_like(s)
+
+
+def _kl_setup(ctx, inputs, output):
+    ctx.save_for_backward(*inputs)
+
+
+def _kl_backward(ctx, gkl):
+    m, s = ctx.saved_tensors
+    dm, ds = torch.ops.gpk.meanfield_kl_grad(m, s, gkl)
+    return dm, ds
+
+
+meanfield_kl.register_autograd(_kl_backward, setup_context=_kl_setup)

@@ -369,6 +369,7 @@ def variational_forward(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
 class VariationalAdjoint:
     dX: torch.Tensor      # (B, N, D)
     dLinv: torch.Tensor   # (M, M) float64, lower: sum over points of dA K_ZX^T
+    dpar: torch.Tensor    # (2M + 2D + 2,) the packed parameter gradients below
     dZ: torch.Tensor      # (M, D) the K_ZX part of dZ
     dvmean: torch.Tensor  # (M,)
     dvstd: torch.Tensor   # (M,)
@@ -408,7 +409,7 @@ def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
         hyper.data_ptr(), gmean.data_ptr(), gvar.data_ptr(), B, N, M, D, ws.data_ptr(),
         dX.data_ptr(), dLinv.data_ptr(), dZ.data_ptr(), dpar.data_ptr(), _stream_ptr(dev))
     _native.check(rc, "gpk_variational_adjoint_f32")
-    return VariationalAdjoint(dX, dLinv, dZ, dpar[:M], dpar[M:2 * M], dpar[2 * M],
+    return VariationalAdjoint(dX, dLinv, dpar, dZ, dpar[:M], dpar[M:2 * M], dpar[2 * M],
                               dpar[2 * M + 1:2 * M + 1 + D], dpar[2 * M + 1 + D:2 * M + 1 + 2 * D],
                               dpar[2 * M + 1 + 2 * D])
 
@@ -417,26 +418,73 @@ def kzz_backward(dLinv: torch.Tensor, L: torch.Tensor, Linv: torch.Tensor, Z: to
                  outputscale: torch.Tensor, lengthscale: torch.Tensor):
     """Back-propagate dObjective/dLinv (lower, fp64) through Linv = chol(K_ZZ + jitter)^{-1}
     to (dZ, d outputscale, d lengthscale): once per optimizer step for all GP calls that
-    shared the factor. M x M fp64 GEMMs with the factor the forward produced (no
-    refactorisation): Lbar = -tril(Linv^T G Linv^T); Cholesky adjoint
-    S = Linv^T Phi(L^T Lbar) Linv, Kbar = (S + S^T)/2; RBF adjoint over K_ZZ.
-    Pure torch on the tensors' device (M x M only; the per-point work is in HIP)."""
-    G = dLinv.tril()
-    LinvT = Linv.transpose(0, 1)
-    Lbar = -(LinvT @ G @ LinvT).tril()
-    P = (L.transpose(0, 1) @ Lbar).tril()
-    P.diagonal().mul_(0.5)
-    S = LinvT @ P @ Linv
-    Kbar = 0.5 * (S + S.transpose(0, 1))
-    D = Z.shape[1]
-    ls = lengthscale.detach().double().reshape(-1).expand(D)
-    s2 = outputscale.detach().double().reshape(())
-    zs = Z.detach().double() / ls
-    d2 = (zs.unsqueeze(1) - zs.unsqueeze(0)).pow(2).sum(-1)
-    W = Kbar * (s2 * torch.exp(-0.5 * d2))
-    w1 = W.sum(1)
-    Wz = W @ zs
-    dZ = 2.0 * (Wz - zs * w1.unsqueeze(1)) / ls
-    dls = 2.0 * ((w1.unsqueeze(1) * zs * zs).sum(0) - (Wz * zs).sum(0)) / ls
-    ds2 = W.sum() / s2
-    return dZ, ds2, dls
+    shared the factor (include/gpk.h::gpk_kzz_backward_f64: five fp64-MFMA tile GEMMs
+    Lbar = -tril(Linv^T G Linv^T), S = Linv^T Phi(L^T Lbar) Linv, then the RBF adjoint over
+    K_ZZ with Kbar = (S + S^T)/2). Returns (dZ (M, D) float, ds2 (), dls (D,)) -- dls per
+    dimension even for a shared lengthscale (the caller sums)."""
+    M, D = Z.shape
+    _require_device(dLinv, L, Linv, Z)
+    dev = Z.device
+    ls = lengthscale.detach().reshape(-1).float()
+    hyper = torch.cat([outputscale.detach().reshape(1).float(), ls.expand(D) if ls.numel() == 1 else ls])
+    lib = _native.lib()
+    ws = torch.empty(lib.gpk_kzz_backward_workspace_bytes(M, D), device=dev, dtype=torch.uint8)
+    dZ = torch.empty(M, D, device=dev, dtype=torch.float32)
+    dhyp = torch.empty(1 + D, device=dev, dtype=torch.float32)
+    rc = lib.gpk_kzz_backward_f64(dLinv.detach().contiguous().double().data_ptr(),
+                                  L.detach().contiguous().data_ptr(), Linv.detach().contiguous().data_ptr(),
+                                  Z.detach().contiguous().float().data_ptr(), hyper.data_ptr(), M, D,
+                                  ws.data_ptr(), dZ.data_ptr(), dhyp.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_kzz_backward_f64")
+    return dZ, dhyp[0], dhyp[1:]
+
+
+# ---------------------------------------------------------------------------
+# ELBO terms (gpk_gauss_ell_f32 / gpk_meanfield_kl_f32)
+# ---------------------------------------------------------------------------
+def gauss_ell(y: torch.Tensor, mean: torch.Tensor, var: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
+    """Per-row sum of GaussianLikelihood.expected_log_prob for (R, N) rows (one launch)."""
+    R, N = mean.shape
+    _require_device(y, mean, var, noise)
+    dev = mean.device
+    ell = torch.empty(R, device=dev, dtype=torch.float32)
+    rc = _native.lib().gpk_gauss_ell_f32(y.data_ptr(), mean.data_ptr(), var.data_ptr(), noise.data_ptr(),
+                                         R, N, ell.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_gauss_ell_f32")
+    return ell
+
+
+def gauss_ell_grad(y, mean, var, noise, gell):
+    """(dy, dmean, dvar, dnoise (1,)) of sum_r gell_r ell_r (one launch + one sum)."""
+    R, N = mean.shape
+    _require_device(y, mean, var, noise, gell)
+    dev = mean.device
+    dy = torch.empty(R, N, device=dev, dtype=torch.float32)
+    dmean = torch.empty(R, N, device=dev, dtype=torch.float32)
+    dvar = torch.empty(R, N, device=dev, dtype=torch.float32)
+    part = torch.empty(R, device=dev, dtype=torch.float32)
+    rc = _native.lib().gpk_gauss_ell_grad_f32(y.data_ptr(), mean.data_ptr(), var.data_ptr(), noise.data_ptr(),
+                                              gell.data_ptr(), R, N, dy.data_ptr(), dmean.data_ptr(),
+                                              dvar.data_ptr(), part.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_gauss_ell_grad_f32")
+    return dy, dmean, dvar, part.sum().reshape(1)
+
+
+def meanfield_kl(m: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """KL(N(m, diag s^2) || N(0, I)) as a (1,) tensor (one launch)."""
+    _require_device(m, s)
+    kl = torch.empty(1, device=m.device, dtype=torch.float32)
+    rc = _native.lib().gpk_meanfield_kl_f32(m.data_ptr(), s.data_ptr(), m.numel(), kl.data_ptr(), None,
+                                            None, None, _stream_ptr(m.device))
+    _native.check(rc, "gpk_meanfield_kl_f32")
+    return kl
+
+
+def meanfield_kl_grad(m, s, gkl):
+    _require_device(m, s, gkl)
+    dm = torch.empty_like(m)
+    ds = torch.empty_like(s)
+    rc = _native.lib().gpk_meanfield_kl_f32(m.data_ptr(), s.data_ptr(), m.numel(), None, gkl.data_ptr(),
+                                            dm.data_ptr(), ds.data_ptr(), _stream_ptr(m.device))
+    _native.check(rc, "gpk_meanfield_kl_f32")
+    return dm, ds

@@ -127,6 +127,6 @@ def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module
         cache = KzzCache()
         key_tensors = (Z, s2, ls)
     Linv = cache.factor(Z, s2, ls, jitter, key_tensors)
-    out = torch.ops.gpk.variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, float(jitter))
+    mean, var, flags, _ = torch.ops.gpk.variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, float(jitter))
     cache.check_pending()
-    return out
+    return mean, var, flags

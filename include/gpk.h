@@ -128,6 +128,55 @@ int gpk_kzz_chol_f64(const float* Z, const float* hyp, int M, int D, float jitte
                      void* stream);
 
 /*
+ * Adjoint of gpk_kzz_chol_f64, once per optimizer step for all GP calls that shared the
+ * factor (fp64 throughout):
+ *   Lbar = -tril(Linv^T G Linv^T),  S = Linv^T Phi(L^T Lbar) Linv,  Kbar = (S + S^T)/2
+ *   (Phi = lower triangle with the diagonal halved), then the RBF adjoint over K_ZZ
+ *   (without its jitter): W = Kbar o K, dZ = 2 (W zs - zs o W1)/l, dl, ds2 = sum W / s2.
+ * Five fp64-MFMA tile GEMM launches + a W-tile kernel + one fixed-order reduction
+ * (run-to-run deterministic).
+ *
+ * Replaces (reference): the autograd backward of psd_safe_cholesky + the triangular solve
+ * inside upstream VariationalStrategy (denoising_model/DeepGP.py:33-38) that train.py:166
+ * runs -- b times per GP call in the reference (Z expanded over the batch), once per step
+ * here; SURVEY.md §8f rows 1 and 3.
+ *
+ * dLinv : (M, M) double, lower (G = dObjective/dLinv)   L, Linv : gpk_kzz_chol_f64 outputs
+ * Z : (M, D) float   hyp : device float[1 + D] = {s2, lengthscale[D]} (as gpk_kzz_chol_f64)
+ * workspace : gpk_kzz_backward_workspace_bytes(M, D) bytes of device memory
+ * dZ : (M, D) float out    dhyp : (1 + D) float out = {ds2, dlengthscale[D]}
+ */
+size_t gpk_kzz_backward_workspace_bytes(int M, int D);
+int gpk_kzz_backward_f64(const double* dLinv, const double* L, const double* Linv, const float* Z,
+                         const float* hyp, int M, int D, void* workspace, float* dZ, float* dhyp,
+                         void* stream);
+
+/*
+ * ELBO terms of the variational path, one launch each way (fixed-order sums):
+ *   ell_r = sum_i -0.5 [((y_ri - mean_ri)^2 + var_ri) / noise + log noise + log 2 pi]
+ *   kl    = 0.5 [sum s^2 + sum m^2 - M - sum log s^2]         (whitened mean-field q(u))
+ * gpk_gauss_ell_grad_f32: for the objective sum_r gell_r ell_r -> dy, dmean, dvar (each
+ * (R, N) or NULL) and dnoise_part (R,) per-row partials of d/dnoise (or NULL).
+ * gpk_meanfield_kl_f32: gkl == NULL -> kl (1,) out; else the backward dm = gkl m,
+ * ds = gkl (s - 1/s).
+ *
+ * Replaces (reference): upstream GaussianLikelihood.expected_log_prob (summed over the
+ * points by VariationalELBO._log_likelihood_term) and
+ * MeanFieldVariationalDistribution.kl_divergence, as the ELBO at forecast_denoising.py:86-89
+ * evaluates them, and their autograd backward (train.py:166); SURVEY.md §8a row a14.
+ *
+ * y, mean, var : (R, N) float;  noise : device float[1];  ell, gell : (R,) float
+ * m, s : (M,) float (variational mean / stddev);  kl, gkl : (1,) float
+ */
+int gpk_gauss_ell_f32(const float* y, const float* mean, const float* var, const float* noise, int R,
+                      int N, float* ell, void* stream);
+int gpk_gauss_ell_grad_f32(const float* y, const float* mean, const float* var, const float* noise,
+                           const float* gell, int R, int N, float* dy, float* dmean, float* dvar,
+                           float* dnoise_part, void* stream);
+int gpk_meanfield_kl_f32(const float* m, const float* s, int M, float* kl, const float* gkl,
+                         float* dm, float* ds, void* stream);
+
+/*
  * Batched variational predictive distribution and expected log likelihood:
  *   K_ZX = s2 * exp(-0.5 ||(z_m - x_i)/l||^2)       (fp32, GPyTorch's centred GEMM form)
  *   A    = Linv @ K_ZX                              (fp64, then cast to fp32)

@@ -26,3 +26,22 @@ for M in (64, 256):
     I = torch.eye(M, dtype=torch.float64, device=dev)
     err = float((kz.Linv @ kz.L - I).abs().max())
     print(f"M={M}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per factor+inverse, |Linv L - I|max {err:.2e}, info {int(kz.info[0])}")
+
+# the K_ZZ adjoint (gpk_kzz_backward_f64) on the same factor
+for M in (64, 256):
+    g = torch.Generator().manual_seed(1)
+    Z = (torch.randn(M, 32, generator=g) / math.sqrt(32)).to(dev)
+    s2 = torch.tensor(LN2, device=dev)
+    ls = torch.full((32,), LN2, device=dev)
+    kz = ops.kzz_cholesky(Z, s2, ls, jitter=1e-4)
+    G = torch.randn(M, M, generator=g, dtype=torch.float64).tril().to(dev)
+    for _ in range(3):
+        ops.kzz_backward(G, kz.L, kz.Linv, Z, s2, ls)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        ops.kzz_backward(G, kz.L, kz.Linv, Z, s2, ls)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"M={M}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per K_ZZ adjoint")

@@ -137,11 +137,37 @@ def test_shard_range_partitions():
             assert max(sizes) - min(sizes) <= 1
 
 
+def kzz_backward_torch(dLinv, L, Linv, Z, outputscale, lengthscale):
+    """Plain-torch fp64 statement of the K_ZZ factor adjoint that
+    include/gpk.h::gpk_kzz_backward_f64 implements (the GPU test's reference):
+    Lbar = -tril(Linv^T G Linv^T); S = Linv^T Phi(L^T Lbar) Linv, Kbar = (S + S^T)/2;
+    RBF adjoint over K_ZZ."""
+    G = dLinv.tril()
+    LinvT = Linv.transpose(0, 1)
+    Lbar = -(LinvT @ G @ LinvT).tril()
+    P = (L.transpose(0, 1) @ Lbar).tril()
+    P.diagonal().mul_(0.5)
+    S = LinvT @ P @ Linv
+    Kbar = 0.5 * (S + S.transpose(0, 1))
+    D = Z.shape[1]
+    ls = lengthscale.detach().double().reshape(-1).expand(D)
+    s2 = outputscale.detach().double().reshape(())
+    zs = Z.detach().double() / ls
+    d2 = (zs.unsqueeze(1) - zs.unsqueeze(0)).pow(2).sum(-1)
+    W = Kbar * (s2 * torch.exp(-0.5 * d2))
+    w1 = W.sum(1)
+    Wz = W @ zs
+    dZ = 2.0 * (Wz - zs * w1.unsqueeze(1)) / ls
+    dls = 2.0 * ((w1.unsqueeze(1) * zs * zs).sum(0) - (Wz * zs).sum(0)) / ls
+    ds2 = W.sum() / s2
+    return dZ, ds2, dls
+
+
 def test_kzz_backward_formula_matches_autograd():
-    """ops.kzz_backward (the M x M part of the variational backward, run once per step
-    for the shared K_ZZ factor) against fp64 torch autograd through cholesky + inverse.
-    Pure torch math: checked here on CPU tensors, it runs on the device in the product."""
-    from fine_grained_gaussian_process_forcasting_amd import ops
+    """The K_ZZ adjoint formula (the M x M part of the variational backward, run once per
+    step for the shared factor; HIP kernel gpk_kzz_backward_f64, checked against this
+    formula in tests/test_variational_grad_gpu.py) against fp64 torch autograd through
+    cholesky + inverse."""
     g = torch.Generator().manual_seed(0)
     M, D = 12, 5
     Z = torch.randn(M, D, generator=g, dtype=torch.float64) / 2
@@ -154,7 +180,7 @@ def test_kzz_backward_formula_matches_autograd():
     L = torch.linalg.cholesky(K)
     Linv = torch.linalg.solve_triangular(L, torch.eye(M, dtype=torch.float64), upper=False)
     gZ, gl, gs = torch.autograd.grad((Linv * G).sum(), [Zr, lr, sr])
-    dZ, ds2, dls = ops.kzz_backward(G, L.detach(), Linv.detach(), Z, s2, ls)
+    dZ, ds2, dls = kzz_backward_torch(G, L.detach(), Linv.detach(), Z, s2, ls)
     assert torch.allclose(dZ, gZ, rtol=1e-9, atol=1e-9)
     assert torch.allclose(dls, gl, rtol=1e-9, atol=1e-9)
     assert torch.allclose(ds2, gs, rtol=1e-9, atol=1e-9)

@@ -134,10 +134,11 @@ def test_custom_ops_registered_with_fake_and_autograd():
         Z = torch.empty(8, 4)
         Linv, Lz, inf = torch.ops.gpk.kzz_factor(Z, torch.empty(()), torch.empty(4), 1e-4, 1e-8, 3)
         assert Linv.shape == (8, 8) and Linv.dtype == torch.float64
-        mean, var, flags = torch.ops.gpk.variational_fwd(X, Linv, Z, torch.empty(8), torch.empty(8),
-                                                         torch.empty(()), torch.empty(4), torch.empty(4),
-                                                         torch.empty(()), 1e-4)
+        mean, var, flags, hyp = torch.ops.gpk.variational_fwd(X, Linv, Z, torch.empty(8), torch.empty(8),
+                                                              torch.empty(()), torch.empty(4), torch.empty(4),
+                                                              torch.empty(()), 1e-4)
         assert mean.shape == (3, 16) and var.shape == (3, 16) and flags.shape == (1,)
+        assert hyp.shape == (4 + 2 * 4,)
 
 
 def test_posterior_entry_validation_without_device():

@@ -126,3 +126,25 @@ def test_variational_grads_reference_shapes(cuda_device, B, N, M, D):
         e = _rel(v.detach().cpu().numpy(), ref[k])
         print(f"B={B} N={N} M={M} D={D} {k:12s} {e:.2e}")
         assert e <= TOL, (k, e)
+
+
+@pytest.mark.parametrize("M,D", [(12, 5), (64, 32), (100, 7), (256, 32), (250, 64)])
+def test_kzz_backward_kernel_vs_torch_fp64(cuda_device, M, D):
+    """gpk_kzz_backward_f64 (five fp64-MFMA tile GEMMs + the RBF adjoint) against the
+    plain-torch fp64 statement of the same formula (itself checked against autograd
+    through cholesky + inverse in tests/test_host_logic.py), on a real K_ZZ factor."""
+    from fine_grained_gaussian_process_forcasting_amd import ops
+    from tests.test_host_logic import kzz_backward_torch
+    dev = cuda_device
+    g = torch.Generator().manual_seed(M + D)
+    Z = (torch.randn(M, D, generator=g) / np.sqrt(D)).to(dev)
+    ls = torch.linspace(0.6, 1.4, D).to(dev)
+    s2 = torch.tensor(0.9, device=dev)
+    f = ops.kzz_cholesky(Z, s2, ls, jitter=1e-4)
+    G = torch.randn(M, M, generator=g, dtype=torch.float64).tril().to(dev)
+    dZ, ds2, dls = ops.kzz_backward(G, f.L, f.Linv, Z, s2, ls)
+    rZ, rs2, rls = kzz_backward_torch(G, f.L, f.Linv, Z, s2, ls)
+    for name, a, b in (("dZ", dZ, rZ), ("ds2", ds2, rs2), ("dls", dls, rls)):
+        e = _rel(a.double().cpu().numpy(), b.double().cpu().numpy())
+        print(f"M={M} D={D} {name} {e:.2e}")
+        assert e <= 1e-6, (name, e)     # fp32 outputs of an fp64 computation
