@@ -79,7 +79,7 @@ struct GpkVarAdjArgs {
   float* dpar;         // (2M + 2D + 2) out: dvmean, dvstd, ds2, dlengthscale, dweights, dbias
 };
 
-int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream);
+
 struct GpkKzzGradArgs {
   const double* dLinv; // (M, M) lower: dObjective/dLinv summed over the calls sharing the factor
   const double* L;     // (M, M) gpk_kzz_chol_f64 factor (lower, zero upper)

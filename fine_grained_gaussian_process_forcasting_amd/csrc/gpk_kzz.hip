@@ -8,19 +8,22 @@
 //
 // gpk_kzz16_kernel<NS>: ONE workgroup of 8 waves; the UPPER triangle of K_ZZ (padded to
 // T 16-blocks, identity padding) is held as 16 x 16 fp64 tiles in v_mfma_f64_16x16x4f64
-// accumulators (acc layout: lane (c, g), reg r <-> row g + 4r, column c), NS tiles per
-// wave, for the whole factorisation. Blocked right-looking Cholesky of R = L^T in 16-column
-// steps (T steps instead of the 4-column kernel's 4T):
-//   diag   the owner wave of tile (k,k) factors it in ONE readlane-broadcast sweep of the
+// accumulators (acc layout: lane (c, g), reg r <-> row g + 4r, column c) for the whole
+// factorisation, wave w owning block columns w and T - 1 - w (T + 1 tiles). Blocked
+// right-looking Cholesky of R = L^T in 16-column steps (T steps instead of the 4-column
+// kernel's 4T):
+//   diag   the owner wave of column k factors T'_kk in ONE readlane-broadcast sweep of the
 //          augmented [T_kk | I] (lanes 0-15: columns of T_kk -> rows of L_kk, lanes 16-31:
-//          identity columns -> columns of L_kk^{-1}); L_kk^{-1} -> LDS;
+//          identity columns -> columns of L_kk^{-1}) -- LOOK-AHEAD: during step k - 1's
+//          update, right after its own T'_kk is updated, while the other waves update;
 //   TRSM   owners of block row k: R_kj = L_kk^{-1} T'_kj (4 f64 MFMAs, the register tile is
 //          the B operand) -> LDS panel + L's block (j, k);
 //   update every tile (i, j), k < i <= j: T'_ij -= R_ki^T R_kj (4 f64 MFMAs, both operands
-//          read from the LDS panel in acc layout: conflict-free).
+//          read from the LDS panel in acc layout: conflict-free; R_kj once per column).
 // Two workgroup barriers per step. GPyTorch's fp64 ladder restarts in-kernel (info = -t).
 // gpk_kzz_inv_kernel: L^{-1}, one workgroup per 16-column block column (block forward
-// substitution on fp64 MFMA), the block columns on different CUs.
+// substitution on fp64 MFMA; the diagonal-block inverses come from the factor kernel, which
+// forms each L_kk^{-1} anyway), the block columns on different CUs.
 #include "gpk_common.h"
 #include "gpk_internal.h"
 #include "gpk_kzz.h"
@@ -54,22 +57,148 @@ GPK_DEVICE double readlane_d(double v, int lane) {
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
-constexpr int KT = 512;   // 8 waves
+#ifndef GPK_KZZ_WAVES
+#define GPK_KZZ_WAVES 8
+#endif
+#ifndef GPK_KZZ_OPAQUE
+#define GPK_KZZ_OPAQUE 1   // per-step opaque tile coordinates (A/B switch)
+#endif
+#ifndef GPK_KZZ_STAMPS
+#define GPK_KZZ_STAMPS 0   // debug: per-step phase clocks into info[1..] (results still valid)
+#endif
+constexpr int KW = GPK_KZZ_WAVES;
+constexpr int KT = 64 * KW;
 __host__ __device__ inline int kzz_zstride(int D) { return ((D + 15) & ~15) + 4; }
 constexpr int kLinvStride = 17;   // L_kk^{-1} rows in LDS (odd: conflict-free column reads)
 
+// The owner wave factors the (updated) diagonal tile t = T'_kk held in its registers:
+// one readlane-broadcast sweep of the augmented [T_kk | I] (lanes 0-15: columns of T_kk
+// -> rows of L_kk, lanes 16-31: identity columns -> columns of L_kk^{-1}). Results: lkk
+// (16 x 17, row-major L_kk), linv (16 x 17, L_kk^{-1}) in LDS; status = failed column + 1.
+GPK_DEVICE void factor_diag(const f64x4 t, int k, double* dbuf, double* lkk, double* linv,
+                            int* status) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dbuf[(g + 4 * r) * 16 + c] = t[r];
+  wave_lds_sync();
+  double v[16];
+  const bool left = lane < 16;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const double x = dbuf[i * 16 + c];   // unconditional read, then select
+    v[i] = left ? x : ((lane - 16 == i) ? 1.0 : 0.0);
+  }
+  int bad = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const double p = readlane_d(v[q], q);
+    if (!(p > 0.0) && bad == 0) bad = q + 1;
+    const double s = rsq64(p > 0.0 ? p : 1.0);
+    const double vq = v[q];
+    const double t = (s * s) * vq;   // row q's multiple: the multipliers stay SGPR operands
+    v[q] = vq * s;
+#pragma unroll
+    for (int i = q + 1; i < 16; ++i) v[i] = __builtin_fma(-readlane_d(v[i], q), t, v[i]);
+  }
+  // lanes 0-15: v[i] = L_kk[c][i] (i <= c); lanes 16-31: v[i] = L_kk^{-1}[i][c - 16]
+  if (left) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lkk[c * kLinvStride + i] = i <= c ? v[i] : 0.0;
+  } else if (lane < 32) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) linv[i * kLinvStride + c] = v[i];
+  }
+  if (lane == 0) status[0] = bad == 0 ? 0 : 16 * k + bad;
+}
+
+// LDS flag words of the factor kernel (volatile, LDS address space: ds_read / ds_write only)
+enum KzzFlag { kKfTile = 0, kKfTmo = 1, kKfStatus = 2 };
+constexpr int kKzzTimeout = 1 << 20;   // info code of an expired spin-wait (never NotPSD)
+
+GPK_DEVICE void kzz_spin_until(lds_vint* f, int target) {
+  int n = 0;
+  while (f[kKfTile] != target) {
+    if (++n > (1 << 20)) {   // bounded: a logic error ends as info = 1 << 20, never a hang
+      f[kKfTmo] = 1;
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// K_ZZ tile (it, jt) of the padded matrix + jitter (+ ladder) into an fp64 acc tile: fp32 Gram
+// on MFMA (A rows fed in the order pi(x) = (x >> 2) + 4 (x & 3) so the fp32 accumulator lands
+// in the fp64 acc layout), the fp32 kernel and jitter as the reference, then fp64.
+GPK_DEVICE f64x4 kzz_tile(const float* zt, const float* zn, int ZS, int D16, int M, int T, int it,
+                          int jt, float s2, float jitter_var, double ladder) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int j = 16 * jt + c;
+  f32x4 gram = {0.f, 0.f, 0.f, 0.f};
+  const int ia = 16 * it + (c >> 2) + 4 * (c & 3);
+  const float* za = zt + (ia < M ? ia : 0) * ZS + 4 * g;
+  const float* zb = zt + (j < M ? j : 0) * ZS + 4 * g;
+  for (int d0 = 0; d0 < D16; d0 += 16) {
+    const float4 av = *(const float4*)(za + d0);
+    const float4 bv = *(const float4*)(zb + d0);
+    gram = mfma32(av.x, bv.x, gram);
+    gram = mfma32(av.y, bv.y, gram);
+    gram = mfma32(av.z, bv.z, gram);
+    gram = mfma32(av.w, bv.w, gram);
+  }
+  f64x4 t;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 16 * it + g + 4 * r;
+    double v = (i == j) ? 1.0 : 0.0;
+    if (i < M && j < M) {
+      float dist = zn[i] + zn[j] - 2.f * gram[r];
+      dist = dist < 0.f ? 0.f : dist;
+      float kv = s2 * __expf(-0.5f * dist);
+      if (i == j) kv = kv + jitter_var;
+      v = (double)kv;
+      if (i == j) v += ladder;
+    }
+    t[r] = v;
+  }
+  return t;
+}
+
+GPK_DEVICE double ladder_of(int attempt, double jitter_chol) {   // GPyTorch: cumulative increments
+  double ladder = 0.0, prev = 0.0, p10 = 1.0;
+  for (int q = 0; q < attempt; ++q) {
+    const double jn = jitter_chol * p10;
+    ladder += jn - prev;
+    prev = jn;
+    p10 *= 10.0;
+  }
+  return ladder;
+}
+
+// Waves 0 .. KW-2 are WORKERS holding the upper triangle's tiles (whole block columns, greedy
+// balanced: columns T-1 .. 0 each to the least-loaded worker); wave KW-1 is the DIAGONAL wave
+// and holds no tile. Per step k:
+//   [A] barrier: L_kk, L_kk^{-1} (LDS) and the step's status are out;
+//   [B] workers: TRSM of block row k -> LDS panel + L; diagonal wave: the diagonal blocks of
+//       L and L^{-1} to HBM; barrier;
+//   [C] the owner of column k+1 updates T'_{k+1,k+1} FIRST and hands it over (LDS + flag),
+//       then its other tiles; the diagonal wave factors it meanwhile (look-ahead), so the
+//       sequential 16-column sweeps overlap the trailing updates.
+// The diagonal wave's registers are disjoint from the workers' (separate loops), so the
+// tiles (NS per worker) and the sweep do not compete for the 256-VGPR budget.
 template <int NS>
 __global__ void __launch_bounds__(KT, 1)
 gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
                  float jitter_var, double jitter_chol, int max_tries, double* __restrict__ L,
-                 int* __restrict__ info) {
+                 double* __restrict__ Linv, int* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) double dsm[];
-  const int T = (M + 15) >> 4, Mp = 16 * T;
+  const int T = (M + 15) >> 4;
   double* panel = dsm;                 // (T - 1) tiles x 256, [slot][reg][lane]
-  double* dbuf = panel + (size_t)(T > 1 ? T - 1 : 1) * 256;   // 256: the diagonal tile
+  double* dbuf = panel + (size_t)(T > 1 ? T - 1 : 1) * 256;   // 256: the hand-over tile
   double* linv = dbuf + 256;           // 16 x 17: L_kk^{-1}
-  int* status = (int*)(linv + 16 * kLinvStride);              // [0]: failed column + 1
-  float* zt = (float*)(status + 4);    // M x ZS  Z / l, centred (zero padded)
+  double* lkk = linv + 16 * kLinvStride;                      // 16 x 17: L_kk
+  int* flagw = (int*)(lkk + 16 * kLinvStride);                // KzzFlag words
+  lds_vint* fl = as_lds_flags(flagw);
+  float* zt = (float*)(flagw + 4);     // M x ZS  Z / l, centred (zero padded)
   const int ZS = kzz_zstride(D);
   const int D16 = (D + 15) & ~15;
   float* zn = zt + M * ZS;             // M
@@ -94,9 +223,9 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
       if (e < M * ZS) zt[e] = d < D ? v[u] / l[u] : 0.f;
     }
   }
+  if (tid < 4) flagw[tid] = tid == kKfTile ? -1 : 0;
   lds_barrier();
-  // column means in a fixed order: 8 partial sums per column (one per wave), then 8 -> 1
-  for (int d = wave; d < D; d += KT / 64) {
+  for (int d = wave; d < D; d += KT / 64) {   // column means: one wave per column
     float sm = 0.f;
     for (int m = lane; m < M; m += 64) sm += zt[m * ZS + d];
     sm = wave_sum(sm);
@@ -115,155 +244,165 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
   }
   lds_barrier();
 
-  // upper tiles (it <= jt), column-major t = jt (jt + 1) / 2 + it, dealt round-robin
-  const int ntile = T * (T + 1) / 2;
-  int its[NS], jts[NS];
-#pragma unroll
-  for (int q = 0; q < NS; ++q) {
-    const int t = wave + 8 * q;
-    int it = T, jt = T;   // no tile: coordinates past the end (skipped everywhere)
-    if (t < ntile) tile_of(t, T, it, jt);
-    its[q] = __builtin_amdgcn_readfirstlane(it);
-    jts[q] = __builtin_amdgcn_readfirstlane(jt);
-  }
-  f64x4 acc[NS];
+  constexpr int NWK = KW - 1;          // workers
   int result = 0;
-  for (int attempt = 0; attempt <= max_tries; ++attempt) {
-    double ladder = 0.0;  // GPyTorch adds (jitter_new - jitter_prev) cumulatively
+  if (wave == NWK) {
+    // ================= diagonal wave =================
+    for (int attempt = 0; attempt <= max_tries; ++attempt) {
+      int failed = 0;
+      for (int k = -1; k < T; ++k) {
+        if (k >= 0) {
+          lds_barrier();   // [A]
+          failed = fl[kKfStatus];
+          if (fl[kKfTmo]) failed = kKzzTimeout;
+          if (failed) break;
+          // [B] diagonal blocks of L and L^{-1}
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int e = lane + 64 * u, which = e >> 8, r = (e >> 4) & 15, cc = e & 15;
+            const int row = 16 * k + r, col = 16 * k + cc;
+            if (row < M && col < M) {
+              if (which == 0) L[(size_t)row * M + col] = lkk[r * kLinvStride + cc];
+              else Linv[(size_t)row * M + col] = linv[r * kLinvStride + cc];
+            }
+          }
+          lds_barrier();
+        }
+        if (k + 1 < T) {   // [C] look-ahead: factor T'_{k+1,k+1} once it is handed over
+          kzz_spin_until(fl, attempt * (T + 1) + k + 1);
+          f64x4 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[r] = dbuf[r * 64 + lane];
+          factor_diag(t, k + 1, dbuf, lkk, linv, flagw + kKfStatus);
+        }
+      }
+      if (!failed) {
+        result = attempt > 0 ? -attempt : 0;
+        break;
+      }
+      result = failed;
+      lds_barrier();
+      if (failed == kKzzTimeout) break;
+      if (lane == 0) fl[kKfStatus] = 0;
+      lds_barrier();
+    }
+  } else {
+    // ================= workers =================
+    // greedy balanced block-column assignment (identical on every wave)
+    int its[NS], jts[NS];
     {
-      double prev = 0.0, p10 = 1.0;
-      for (int q = 0; q < attempt; ++q) {
-        const double jn = jitter_chol * p10;
-        ladder += jn - prev;
-        prev = jn;
-        p10 *= 10.0;
-      }
-    }
-    // K_ZZ tiles: fp32 Gram on MFMA (A rows fed in the order pi(x) = (x >> 2) + 4 (x & 3) so the
-    // fp32 accumulator lands in the fp64 acc layout), fp32 kernel + jitter, -> fp64 + ladder
+      int load[NWK];
 #pragma unroll
-    for (int q = 0; q < NS; ++q) {
-      asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
-      const int j = 16 * jts[q] + c;
-      f32x4 gram = {0.f, 0.f, 0.f, 0.f};
-      if (its[q] < T) {
-        const int ia = 16 * its[q] + (c >> 2) + 4 * (c & 3);
-        const float* za = zt + (ia < M ? ia : 0) * ZS + 4 * g;
-        const float* zb = zt + (j < M ? j : 0) * ZS + 4 * g;
-        for (int d0 = 0; d0 < D16; d0 += 16) {
-          const float4 av = *(const float4*)(za + d0);
-          const float4 bv = *(const float4*)(zb + d0);
-          gram = mfma32(av.x, bv.x, gram);
-          gram = mfma32(av.y, bv.y, gram);
-          gram = mfma32(av.z, bv.z, gram);
-          gram = mfma32(av.w, bv.w, gram);
+      for (int w = 0; w < NWK; ++w) load[w] = 0;
+      int n = 0;
+#pragma unroll
+      for (int q = 0; q < NS; ++q) { its[q] = T; jts[q] = T; }
+      for (int col = T - 1; col >= 0; --col) {
+        int best = 0;
+#pragma unroll
+        for (int w = 1; w < NWK; ++w) best = load[w] < load[best] ? w : best;
+#pragma unroll
+        for (int w = 0; w < NWK; ++w) load[w] += (w == best) ? col + 1 : 0;
+        if (best == wave) {
+          for (int r0 = 0; r0 <= col; ++r0) {
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+              if (q == n) { its[q] = r0; jts[q] = col; }
+            }
+            ++n;
+          }
         }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * its[q] + g + 4 * r;
-        double v = (i == j) ? 1.0 : 0.0;
-        if (its[q] < T && i < M && j < M) {
-          float dist = zn[i] + zn[j] - 2.f * gram[r];
-          dist = dist < 0.f ? 0.f : dist;
-          float kv = s2 * __expf(-0.5f * dist);
-          if (i == j) kv = kv + jitter_var;
-          v = (double)kv;
-          if (i == j) v += ladder;
-        }
-        acc[q][r] = v;
+      for (int q = 0; q < NS; ++q) {
+        its[q] = __builtin_amdgcn_readfirstlane(its[q]);
+        jts[q] = __builtin_amdgcn_readfirstlane(jts[q]);
       }
     }
-    if (tid == 0) status[0] = 0;
-    int failed = 0;
-    for (int k = 0; k < T; ++k) {
+    f64x4 acc[NS];
+    for (int attempt = 0; attempt <= max_tries; ++attempt) {
+      const double ladder = ladder_of(attempt, jitter_chol);
 #pragma unroll
-      for (int q = 0; q < NS; ++q) asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
-      // ---- diagonal block: the owner wave of tile (k, k) ----
-      const int tkk = k * (k + 1) / 2 + k;
-      if (wave == (tkk & 7)) {
+      for (int q = 0; q < NS; ++q) {
+        asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
+        if (its[q] < T) acc[q] = kzz_tile(zt, zn, ZS, D16, M, T, its[q], jts[q], s2, jitter_var, ladder);
+        if (its[q] == 0 && jts[q] == 0) {   // hand tile (0, 0) to the diagonal wave
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dbuf[r * 64 + lane] = acc[q][r];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+          if (lane == 0) fl[kKfTile] = attempt * (T + 1);
+        }
+      }
+      int failed = 0;
+      for (int k = 0; k < T; ++k) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
+#if GPK_KZZ_STAMPS
+        if (tid == 0 && attempt == 0) info[1 + 3 * k] = (int)__builtin_amdgcn_s_memtime();
+#endif
+        lds_barrier();   // [A]
+#if GPK_KZZ_STAMPS
+        if (tid == 0 && attempt == 0) info[2 + 3 * k] = (int)__builtin_amdgcn_s_memtime();
+#endif
+        failed = fl[kKfStatus];
+        if (fl[kKfTmo]) failed = kKzzTimeout;
+        if (failed) break;
+        // [B] TRSM of block row k: R_kj = L_kk^{-1} T'_kj -> registers, LDS panel, L
+        double la[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) la[kk] = linv[c * kLinvStride + g + 4 * kk];
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
-          if (its[q] == k && jts[q] == k) {
+          if (its[q] == k && jts[q] > k && jts[q] < T) {
+            f64x4 x = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dbuf[(g + 4 * r) * 16 + c] = acc[q][r];
+            for (int kk = 0; kk < 4; ++kk) x = mfma64(la[kk], acc[q][kk], x);
+            acc[q] = x;
+            double* pt = panel + (size_t)(jts[q] - k - 1) * 256;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pt[r * 64 + lane] = x[r];
+            const int row = 16 * jts[q] + c;   // L block (j, k) = R_kj^T
+            if (row < M) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) L[(size_t)row * M + 16 * k + g + 4 * r] = x[r];
+            }
           }
         }
-        wave_lds_sync();
-        // augmented [T_kk | I]: lane c < 16 holds column c of T_kk, lane 16 + c column c of I
-        double v[16];
-        const bool left = lane < 16;
+        lds_barrier();
+#if GPK_KZZ_STAMPS
+        if (tid == 0 && attempt == 0) info[3 + 3 * k] = (int)__builtin_amdgcn_s_memtime();
+#endif
+        // [C] the hand-over tile first, then the rest of the trailing update
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = left ? dbuf[i * 16 + c] : ((lane - 16 == i) ? 1.0 : 0.0);
-        int bad = 0;
+        for (int q = 0; q < NS; ++q) {
+          if (its[q] == k + 1 && jts[q] == k + 1) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const double p = readlane_d(v[q], q);
-          if (!(p > 0.0) && bad == 0) bad = q + 1;
-          const double s = rsq64(p > 0.0 ? p : 1.0);
-          const double sq = s * s;
-          const double vq = v[q];
-          v[q] = vq * s;
+            for (int kk = 0; kk < 4; ++kk) acc[q] = mfma64(-panel[kk * 64 + lane], panel[kk * 64 + lane], acc[q]);
 #pragma unroll
-          for (int i = q + 1; i < 16; ++i) v[i] = __builtin_fma(-readlane_d(v[i], q) * sq, vq, v[i]);
-        }
-        // lanes 0-15: v[i] = L_kk[c][i] (i <= c); lanes 16-31: v[i] = L_kk^{-1}[i][c]
-        const int row = 16 * k + c;
-        if (left) {
-          if (row < M) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-              if (i <= c) L[(size_t)row * M + 16 * k + i] = v[i];
+            for (int r = 0; r < 4; ++r) dbuf[r * 64 + lane] = acc[q][r];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (lane == 0) fl[kKfTile] = attempt * (T + 1) + k + 1;
           }
-        } else if (lane < 32) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) linv[i * kLinvStride + (lane - 16)] = v[i];
         }
-        if (lane == 0) status[0] = bad == 0 ? 0 : 16 * k + bad;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+          if (its[q] > k && its[q] < T && !(its[q] == k + 1 && jts[q] == k + 1)) {
+            const double* pa = panel + (size_t)(its[q] - k - 1) * 256;
+            const double* pb = panel + (size_t)(jts[q] - k - 1) * 256;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) acc[q] = mfma64(-pa[kk * 64 + lane], pb[kk * 64 + lane], acc[q]);
+          }
+        }
       }
+      if (!failed) {
+        result = attempt > 0 ? -attempt : 0;
+        break;
+      }
+      result = failed;
       lds_barrier();
-      failed = status[0];
-      if (failed) break;
-      // ---- TRSM of block row k: R_kj = L_kk^{-1} T'_kj -> registers, LDS panel, L ----
-      double la[4];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) la[kk] = linv[c * kLinvStride + g + 4 * kk];
-#pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        if (its[q] == k && jts[q] > k && jts[q] < T) {
-          f64x4 x = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) x = mfma64(la[kk], acc[q][kk], x);
-          acc[q] = x;
-          double* pt = panel + (size_t)(jts[q] - k - 1) * 256;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pt[r * 64 + lane] = x[r];
-          // L block (j, k) = R_kj^T: L[16 j + c][16 k + g + 4 r] = R_kj[g + 4 r][c]
-          const int row = 16 * jts[q] + c;
-          if (row < M) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) L[(size_t)row * M + 16 * k + g + 4 * r] = x[r];
-          }
-        }
-      }
-      lds_barrier();
-      // ---- trailing update: T'_ij -= R_ki^T R_kj for k < i <= j ----
-#pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        if (its[q] > k && its[q] < T) {
-          const double* pa = panel + (size_t)(its[q] - k - 1) * 256;
-          const double* pb = panel + (size_t)(jts[q] - k - 1) * 256;
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) acc[q] = mfma64(-pa[kk * 64 + lane], pb[kk * 64 + lane], acc[q]);
-        }
-      }
+      if (failed == kKzzTimeout) break;
+      lds_barrier();   // (the diagonal wave resets the status between these two)
     }
-    if (!failed) {
-      result = attempt > 0 ? -attempt : 0;
-      break;
-    }
-    result = failed;
-    lds_barrier();
   }
   for (int i = wave; i < M; i += KT / 64) {   // strict upper triangle of L: one row per wave
     for (int j = i + 1 + lane; j < M; j += 64) L[(size_t)i * M + j] = 0.0;
@@ -274,7 +413,7 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
 // L^{-1} of the K_ZZ factor: one workgroup per 16-column block column jb (grid T16), so
 // the block columns run concurrently on different CUs. Block forward substitution,
 // right-looking, on fp64 MFMA:
-//   T_u = L_uu^{-1} (the diagonal blocks the column needs, formed in the workgroup),
+//   T_u = L_uu^{-1} (the diagonal blocks of Linv, written by gpk_kzz16_kernel),
 //   X_jb = T_jb;  for k = jb ..: S_u += -L_uk X_k (u > k), X_{k+1} = T_{k+1} S_{k+1}.
 // k-order of every MFMA: q = g + 4 kk, so a tile held in acc layout (reg r <-> row g + 4r)
 // is the B operand of k-step kk straight from register kk. S tiles dealt over the 4 waves
@@ -300,25 +439,12 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
     const int i = e >> 4, j = 16 * jb + (e & 15);
     if (i < M && j < M) Linv[(size_t)i * M + j] = 0.0;
   }
-  // diagonal-block inverses: lane group g of wave w takes block u = 4 w + g (+ 16 ...),
-  // lane c its column c by forward substitution
-  for (int u = 4 * wave + g; u < nb; u += 16) {
-    const int b0 = 16 * (jb + u);
-    double lr[16][16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-#pragma unroll
-      for (int q = 0; q <= r; ++q) lr[r][q] = Lat(b0 + r, b0 + q);
-    double x[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      double v = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-      for (int q = 0; q < r; ++q) v = __builtin_fma(-lr[r][q], x[q], v);
-      x[r] = (r >= c) ? v * rcp64(lr[r][r]) : 0.0;
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Tv[u * 256 + r * 16 + c] = x[r];
+  // diagonal-block inverses T_u = L_uu^{-1}: the factor kernel stored them as the diagonal
+  // blocks of Linv (identity padding beyond M)
+  for (int e = tid; e < nb * 256; e += KIT) {
+    const int u = e >> 8, r = (e >> 4) & 15, q = e & 15;
+    const int i = 16 * (jb + u) + r, j = 16 * (jb + u) + q;
+    Tv[e] = (i < M && j < M) ? Linv[(size_t)i * M + j] : (i == j ? 1.0 : 0.0);
   }
   lds_barrier();
   for (int e = tid; e < 256; e += KIT) {      // X_jb = T_jb
@@ -392,12 +518,12 @@ void set_lds_once() {
 template <int NS>
 int launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
   const int T = (a.M + 15) >> 4;
-  const size_t lds = (size_t)((T > 1 ? T - 1 : 1) * 256 + 256 + 16 * kLinvStride) * sizeof(double) +
+  const size_t lds = (size_t)((T > 1 ? T - 1 : 1) * 256 + 256 + 2 * 16 * kLinvStride) * sizeof(double) +
                      4 * sizeof(int) + (size_t)(a.M * kzz_zstride(a.D) + a.M + a.D) * sizeof(float);
   if (lds > 160 * 1024) return -4;
   set_lds_once<gpk_kzz16_kernel<NS>>();
   hipLaunchKernelGGL((gpk_kzz16_kernel<NS>), dim3(1), dim3(KT), lds, stream, a.Z, a.hyp, a.M, a.D,
-                     a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.info);
+                     a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.Linv, a.info);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   set_lds_once<gpk_kzz_inv_kernel>();
@@ -411,10 +537,18 @@ int launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
 
 int gpk_launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
   const int T = (a.M + 15) >> 4;
-  const int ns = (T * (T + 1) / 2 + 7) / 8;   // tiles per wave
-  if (ns <= 2) return launch_kzz16<2>(a, stream);
-  if (ns <= 5) return launch_kzz16<5>(a, stream);
-  if (ns <= 10) return launch_kzz16<10>(a, stream);
-  if (ns <= 17) return launch_kzz16<17>(a, stream);
+  // tiles per worker: whole block columns, greedily balanced over KW - 1 workers
+  int load[32] = {0}, ns = 0;
+  for (int col = T - 1; col >= 0; --col) {
+    int best = 0;
+    for (int w = 1; w < KW - 1; ++w) best = load[w] < load[best] ? w : best;
+    load[best] += col + 1;
+    ns = load[best] > ns ? load[best] : ns;
+  }
+  if (ns <= 4) return launch_kzz16<4>(a, stream);
+  if (ns <= 8) return launch_kzz16<8>(a, stream);
+  if (ns <= 12) return launch_kzz16<12>(a, stream);
+  if (ns <= 16) return launch_kzz16<16>(a, stream);
+  if (ns <= 21) return launch_kzz16<21>(a, stream);
   return -3;
 }

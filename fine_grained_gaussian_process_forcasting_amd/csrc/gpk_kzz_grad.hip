@@ -14,14 +14,14 @@
 //   W    = Kbar o s2 exp(-d2/2),  w1 = W 1,  Wz = W zs  (zs = Z / l, fp64)
 //   dZ   = 2 (Wz - zs o w1) / l,  dl_d = 2 (sum_i w1_i zs_id^2 - Wz_id zs_id) / l_d,
 //   ds2  = sum W / s2.
-// Kernels: gpk_kzzg_gemm_kernel<MODE> (one wave per 16 x 16 output tile, fp64 MFMA,
-// operands straight from L2 with a one-k-block register prefetch; triangular k-ranges),
-// gpk_kzzg_rbf_kernel (one wave per 16 x 16 tile of W: partial w1 / Wz per row and
-// column block), gpk_kzzg_fin_kernel (fixed-order sums -> dZ, ds2, dl: deterministic).
+// Kernels: gpk_kzzg_gemm_kernel<MODE> (one workgroup per 16 x 16 output tile, its k-blocks
+// split over the 4 waves, all operands requested up front from L2, fp64 MFMA; triangular
+// k-ranges), gpk_kzzg_rbf_kernel (one wave per 16 x 16 tile of W: partial w1 / Wz per row
+// and column block), gpk_kzzg_sum_kernel + gpk_kzzg_fin_kernel (fixed-order sums -> dZ,
+// ds2, dl: deterministic).
 #include "gpk_common.h"
 #include "gpk_internal.h"
 
-#include <mutex>
 
 namespace {
 
@@ -49,15 +49,18 @@ struct KzzGemm {
   static constexpr bool kTA = MODE == 2 || MODE == 3 || MODE == 5;   // A(i,k) read as X[k][i]
 };
 
+// One workgroup per output tile; its k-blocks are dealt to the 4 waves (kb = k_lo + w,
+// + 4, ...), every wave requests ALL its operands up front (<= 4 k-blocks at M = 256: one
+// L2 latency instead of one per k-block), and the 4 partial tiles are summed in LDS in a
+// fixed order.
 template <int MODE>
 __global__ void __launch_bounds__(256)
 gpk_kzzg_gemm_kernel(const double* __restrict__ Am, const double* __restrict__ Bm, int M,
                      double* __restrict__ C) {
   using G = KzzGemm<MODE>;
+  __shared__ double red[3][256];
   const int T = (M + 15) >> 4;
-  const int ntile = G::kFull ? T * T : T * (T + 1) / 2;
-  const int t = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (t >= ntile) return;
+  const int t = blockIdx.x;
   int ib, jb;
   if (G::kFull) {
     ib = t / T;
@@ -66,6 +69,7 @@ gpk_kzzg_gemm_kernel(const double* __restrict__ Am, const double* __restrict__ B
     tri_tile(t, ib, jb);
   }
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int k_lo, k_hi;   // k-blocks [k_lo, k_hi]
   if (MODE == 1) { k_lo = 0; k_hi = ib < jb ? ib : jb; }
   else if (MODE == 4) { k_lo = jb; k_hi = ib; }
@@ -73,39 +77,46 @@ gpk_kzzg_gemm_kernel(const double* __restrict__ Am, const double* __restrict__ B
   const int i = 16 * ib + c;          // A row of this lane
   const int j = 16 * jb + c;          // B column of this lane
   const bool iok = i < M, jok = j < M;
-
-  // operands of one 16-wide k-block: step s uses k = 16 kb + 4 s + g
-  auto load = [&](int kb, double (&a)[4], double (&b)[4]) {
+  constexpr int KPW = 4;              // k-blocks per wave (T <= 16)
+  double a[KPW][4], b[KPW][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+  for (int u = 0; u < KPW; ++u) {
+    const int kb = k_lo + wave + 4 * u;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {     // step s of k-block kb uses k = 16 kb + 4 s + g
       const int k = 16 * kb + 4 * s + g;
-      const bool kok = k < M;
+      const bool kok = kb <= k_hi && k < M;
       const int kc = kok ? k : 0, ic = iok ? i : 0, jc = jok ? j : 0;
       double av = G::kTA ? Am[(size_t)kc * M + ic] : Am[(size_t)ic * M + kc];
       double bv = MODE == 1 ? Bm[(size_t)jc * M + kc] : Bm[(size_t)kc * M + jc];
       if (MODE == 1 && k > i) av = 0.0;          // G = tril(dLinv)
-      a[s] = (iok && kok) ? (MODE == 2 ? -av : av) : 0.0;
-      b[s] = (jok && kok) ? bv : 0.0;
+      a[u][s] = (iok && kok) ? (MODE == 2 ? -av : av) : 0.0;
+      b[u][s] = (jok && kok) ? bv : 0.0;
     }
-  };
-  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-  double a0[4], b0[4], a1[4], b1[4];
-  load(k_lo, a0, b0);
-  for (int kb = k_lo; kb <= k_hi; kb += 2) {
-    if (kb + 1 <= k_hi) load(kb + 1, a1, b1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma64(a0[s], b0[s], acc);
-    if (kb + 1 > k_hi) break;
-    if (kb + 2 <= k_hi) load(kb + 2, a0, b0);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma64(a1[s], b1[s], acc);
   }
+  // every operand in registers before the first MFMA: the loads above are all in flight
+  // together (the scheduler would otherwise interleave them with the MFMA chain)
+#pragma unroll
+  for (int u = 0; u < KPW; ++u)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) asm volatile("" : "+v"(a[u][s]), "+v"(b[u][s]));
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int u = 0; u < KPW; ++u)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma64(a[u][s], b[u][s], acc);
+  if (wave > 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave - 1][r * 64 + lane] = acc[r];
+  }
+  __syncthreads();
+  if (wave != 0) return;
   // lane (c, g), reg r <-> C[16 ib + g + 4 r][16 jb + c]
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int ii = 16 * ib + g + 4 * r;
     if (ii >= M || !jok) continue;
-    double v = acc[r];
+    double v = ((acc[r] + red[0][r * 64 + lane]) + red[1][r * 64 + lane]) + red[2][r * 64 + lane];
     if (!G::kFull && ib == jb) {
       if (j > ii) v = 0.0;
       if (MODE == 3 && j == ii) v *= 0.5;
@@ -173,49 +184,68 @@ gpk_kzzg_rbf_kernel(const double* __restrict__ S, const float* __restrict__ Z,
   }
 }
 
-// Fixed-order sums over the column blocks, then over the rows: dZ (M, D) float,
-// dhyp = {ds2, dl[D]} float. One workgroup, thread = row.
+// Fixed-order sums over the column blocks: tot[i][0] = w1_i, tot[i][1 + d] = Wz_id
+// (one thread per output, many workgroups).
 __global__ void __launch_bounds__(256)
-gpk_kzzg_fin_kernel(const double* __restrict__ part, const float* __restrict__ Z,
+gpk_kzzg_sum_kernel(const double* __restrict__ part, int M, int D, double* __restrict__ tot) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= M * (D + 1)) return;
+  const int T = (M + 15) >> 4;
+  double v[16];
+#pragma unroll
+  for (int jb = 0; jb < 16; ++jb) v[jb] = jb < T ? part[(size_t)jb * M * (D + 1) + e] : 0.0;
+  double s = 0.0;
+#pragma unroll
+  for (int jb = 0; jb < 16; ++jb) s += v[jb];
+  tot[e] = s;
+}
+
+// dZ (M, D) float, dhyp = {ds2, dl[D]} float from the row totals; the sums over rows in a
+// fixed order (8 row groups per dimension, then the 8 group sums). One workgroup.
+__global__ void __launch_bounds__(256)
+gpk_kzzg_fin_kernel(const double* __restrict__ tot, const float* __restrict__ Z,
                     const float* __restrict__ hyp, int M, int D, float* __restrict__ dZ,
                     float* __restrict__ dhyp) {
-  extern __shared__ double fsm[];   // (M) w1 | (M x D) row terms of dl
-  double* w1s = fsm;
-  double* rt = fsm + M;
-  const int T = (M + 15) >> 4;
-  for (int i = threadIdx.x; i < M; i += 256) {
-    double w1 = 0.0;
-    for (int jb = 0; jb < T; ++jb) w1 += part[((size_t)jb * M + i) * (D + 1)];
-    w1s[i] = w1;
-    for (int d = 0; d < D; ++d) {
-      double wz = 0.0;
-      for (int jb = 0; jb < T; ++jb) wz += part[((size_t)jb * M + i) * (D + 1) + 1 + d];
-      const double l = (double)hyp[1 + d];
+  __shared__ double red[256];
+  __shared__ double w1r[4];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < M * D; e += 256) {
+    const int i = e / D, d = e - i * D;
+    const double l = (double)hyp[1 + d];
+    const double z = (double)Z[e] / l;
+    dZ[e] = (float)(2.0 * (tot[(size_t)i * (D + 1) + 1 + d] - z * tot[(size_t)i * (D + 1)]) / l);
+  }
+  // dl_d = 2/l_d sum_i (w1_i z_id^2 - Wz_id z_id): thread (d, part) with part = tid / D
+  const int nparts = 256 / D;
+  double acc = 0.0;
+  if (tid < nparts * D) {
+    const int d = tid % D, pp = tid / D;
+    const double l = (double)hyp[1 + d];
+    for (int i = pp; i < M; i += nparts) {
       const double z = (double)Z[(size_t)i * D + d] / l;
-      dZ[(size_t)i * D + d] = (float)(2.0 * (wz - z * w1) / l);
-      rt[(size_t)i * D + d] = w1 * z * z - wz * z;
+      acc += tot[(size_t)i * (D + 1)] * z * z - tot[(size_t)i * (D + 1) + 1 + d] * z;
     }
   }
+  red[tid] = acc;
+  // ds2 = sum_i w1_i / s2: one wave per quarter of the rows
+  double w = 0.0;
+  for (int i = tid; i < M; i += 256) w += tot[(size_t)i * (D + 1)];
+  w = wave_sum_d(w);
+  if ((tid & 63) == 0) w1r[tid >> 6] = w;
   __syncthreads();
-  if ((int)threadIdx.x < D) {
-    const int d = threadIdx.x;
+  if (tid < D) {
     double s = 0.0;
-    for (int i = 0; i < M; ++i) s += rt[(size_t)i * D + d];
-    dhyp[1 + d] = (float)(2.0 * s / (double)hyp[1 + d]);
+    for (int pp = 0; pp < nparts; ++pp) s += red[pp * D + tid];
+    dhyp[1 + tid] = (float)(2.0 * s / (double)hyp[1 + tid]);
   }
-  if (threadIdx.x == 64) {
-    double s = 0.0;
-    for (int i = 0; i < M; ++i) s += w1s[i];
-    dhyp[0] = (float)(s / (double)hyp[0]);
-  }
+  if (tid == 0) dhyp[0] = (float)((((w1r[0] + w1r[1]) + w1r[2]) + w1r[3]) / (double)hyp[0]);
 }
 
 template <int MODE>
 hipError_t launch_gemm(const double* A, const double* B, int M, double* C, hipStream_t stream) {
   const int T = (M + 15) >> 4;
   const int ntile = KzzGemm<MODE>::kFull ? T * T : T * (T + 1) / 2;
-  hipLaunchKernelGGL((gpk_kzzg_gemm_kernel<MODE>), dim3((ntile + 3) / 4), dim3(256), 0, stream, A, B,
-                     M, C);
+  hipLaunchKernelGGL((gpk_kzzg_gemm_kernel<MODE>), dim3(ntile), dim3(256), 0, stream, A, B, M, C);
   return hipGetLastError();
 }
 
@@ -223,7 +253,7 @@ hipError_t launch_gemm(const double* A, const double* B, int M, double* C, hipSt
 
 size_t gpk_kzz_grad_ws_bytes(int M, int D) {
   const int T = (M + 15) >> 4;
-  return (2 * (size_t)M * M + (size_t)T * M * (D + 1)) * sizeof(double);
+  return (2 * (size_t)M * M + (size_t)(T + 1) * M * (D + 1)) * sizeof(double);
 }
 
 int gpk_launch_kzz_grad(const GpkKzzGradArgs& a, hipStream_t stream) {
@@ -240,14 +270,12 @@ int gpk_launch_kzz_grad(const GpkKzzGradArgs& a, hipStream_t stream) {
   const int T = (M + 15) >> 4;
   hipLaunchKernelGGL(gpk_kzzg_rbf_kernel, dim3(T * T), dim3(64), 0, stream, b0, a.Z, a.hyp, M, D, part);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  static std::once_flag once;   // fin needs M (D + 1) doubles of LDS (up to 133 KB)
-  std::call_once(once, [] {
-    (void)hipFuncSetAttribute((const void*)gpk_kzzg_fin_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipGetLastError();
-  });
-  hipLaunchKernelGGL(gpk_kzzg_fin_kernel, dim3(1), dim3(256), (size_t)M * (D + 1) * sizeof(double), stream,
-                     part, a.Z, a.hyp, M, D, a.dZ, a.dhyp);
+  double* tot = part + (size_t)T * M * (D + 1);
+  hipLaunchKernelGGL(gpk_kzzg_sum_kernel, dim3((M * (D + 1) + 255) / 256), dim3(256), 0, stream, part, M,
+                     D, tot);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gpk_kzzg_fin_kernel, dim3(1), dim3(256), 0, stream, tot, a.Z, a.hyp, M, D, a.dZ,
+                     a.dhyp);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }

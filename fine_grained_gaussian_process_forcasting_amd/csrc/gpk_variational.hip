@@ -9,10 +9,7 @@
 //     var  = s2 + jitter + sum_m A_mi^2 (s_m^2 - 1), clamped >= 1e-6 (MVN.variance)
 //     ELL  = sum_i -0.5 [((y_i - mean_i)^2 + var_i)/noise + log noise + log 2pi]
 //
-// Kernels:
-//   gpk_kzz_kernel      ONE workgroup: K_ZZ of the shared inducing points, register-resident
-//                       fp64 Cholesky + L^{-1} (4-column steps, GPyTorch's fp64 ladder). The
-//                       reference factors the same matrix b times (Z expanded over the batch).
+// Kernels (the shared K_ZZ factor and its adjoint: gpk_kzz.hip, gpk_kzz_grad.hip):
 //   gpk_var_fwd_kernel  the per-point work as ONE column-tiled GEMM A = L^{-1} [K_ZX(b=0) | ...]:
 //                       a workgroup owns a chunk of TW points of one window and all M rows of A;
 //                       K_ZX chunk from an f32-MFMA Gram (GPyTorch's centred _sq_dist form) in
@@ -73,432 +70,6 @@ template <typename T>
 GPK_DEVICE const T* fresh_ptr(const T* p) {
   asm volatile("" : "+s"(p));
   return p;
-}
-
-// ---------------------------------------------------------------------------
-// K_ZZ factorisation on fp64 MFMA tiles (one workgroup of KT = 512 threads).
-// The lower triangle (M padded to Mp = multiple of 16, identity padding) is held as
-// 16 x 16 tiles in v_mfma_f64_16x16x4f64 accumulators (lane (c, g), reg r <-> row
-// g + 4r, column c), NS tiles per wave for the whole factorisation (Mp = 256: 136
-// tiles, 17 per wave, 136 VGPRs). Step s eliminates columns j0 = 4s .. j0+3:
-//   publish  the owners of tile column j0/16 write those 4 columns (rows >= j0) to LDS;
-//   panel    every thread factors the 4 x 4 pivot block redundantly (hardware rsq / rcp
-//            + Newton steps; GPyTorch's fp64 ladder restarts with more jitter on a
-//            non-positive pivot); one thread per row forms l_i = P_i L4^-T -> LDS and
-//            writes the final L entries;
-//   update   every tile right of the panel takes A -= l_rows l_cols^T: ONE f64 MFMA
-//            (rank 4 = the instruction's k) with both operands read from LDS.
-// L^{-1} is then formed by gpk_kzz_inv_kernel, one workgroup per 16-column block column.
-// ---------------------------------------------------------------------------
-constexpr int KT = 512;   // 8 waves
-// Z row stride (floats): D rounded up to the 16 dims one MFMA k-group reads, + 4, so a
-// row spans an odd number of 16-byte slots and the b128 reads of 16 rows are conflict-free
-__host__ __device__ inline int kzz_zstride(int D) { return ((D + 15) & ~15) + 4; }
-#ifndef GPK_KZZ_SKIP
-#define GPK_KZZ_SKIP 0   // timing-only A/B switches (results invalid when set)
-#endif
-#ifndef GPK_KZZ_STAMPS
-#define GPK_KZZ_STAMPS 0   // debug: phase clocks into Linv[0][1..] (results invalid when set)
-#endif
-#if GPK_KZZ_STAMPS
-#define KZ_STAMP(k) kst[k] = __builtin_amdgcn_s_memtime()
-#define KZ_ACC(k, t0) kst[k] += __builtin_amdgcn_s_memtime() - (t0)
-#else
-#define KZ_STAMP(k)
-#define KZ_ACC(k, t0)
-#endif
-
-GPK_DEVICE double rsq64(double x) {   // 1/sqrt(x), x > 0: hardware estimate + 2 Newton steps
-  double y = __builtin_amdgcn_rsq(x);
-  y = y * (1.5 - 0.5 * x * y * y);
-  y = y * (1.5 - 0.5 * x * y * y);
-  return y;
-}
-GPK_DEVICE double rcp64(double x) {   // 1/x: hardware estimate + 2 Newton steps
-  double y = __builtin_amdgcn_rcp(x);
-  y = y * (2.0 - x * y);
-  y = y * (2.0 - x * y);
-  return y;
-}
-
-// 4 x 4 lower Cholesky l of the symmetric d and li = l^{-1}; false on a non-positive /
-// NaN pivot (bad = its column)
-GPK_DEVICE bool chol4(const double (&d)[4][4], double (&l)[4][4], double (&li)[4][4], int& bad) {
-  double rd[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    double sm = d[j][j];
-#pragma unroll
-    for (int q = 0; q < j; ++q) sm -= l[j][q] * l[j][q];
-    if (!(sm > 0.0)) { bad = j; return false; }
-    const double r = rsq64(sm);
-    l[j][j] = sm * r;
-    rd[j] = r;
-#pragma unroll
-    for (int i = j + 1; i < 4; ++i) {
-      double t = d[i][j];
-#pragma unroll
-      for (int q = 0; q < j; ++q) t -= l[i][q] * l[j][q];
-      l[i][j] = t * r;
-    }
-#pragma unroll
-    for (int i = 0; i < j; ++i) l[i][j] = 0.0;
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (r < c) { li[r][c] = 0.0; continue; }
-      double v = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-      for (int q = c; q < r; ++q) v -= l[r][q] * li[q][c];
-      li[r][c] = v * rd[r];
-    }
-  return true;
-}
-
-GPK_DEVICE void tri_of(int t, int& it, int& jt) {   // lower tiles row-major: row it holds 0..it
-  int r = (int)((__builtin_sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
-  while ((r + 1) * (r + 2) / 2 <= t) ++r;
-  while (r * (r + 1) / 2 > t) --r;
-  it = r;
-  jt = t - r * (r + 1) / 2;
-}
-
-template <int NS>
-__global__ void __launch_bounds__(KT, 1)
-gpk_kzz_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int M, int D,
-               float jitter_var, double jitter_chol, int max_tries, double* __restrict__ L,
-               double* __restrict__ Linv, int* __restrict__ info) {
-  extern __shared__ __attribute__((aligned(16))) float vsm[];
-  const int Mp = (M + 15) & ~15;
-  double* P = (double*)vsm;            // Mp x 4  panel columns (phase 1) / L panel (phase 2)
-  double* lb = P + Mp * 4;             // Mp x 4  l rows (phase 1) / X_k as 4 x Mp (phase 2)
-  double* xr = lb + Mp * 4;            // 4 x Mp  published X rows (phase 2)
-  // phase 2 double-buffers P / lb / xr by step parity (second copies after xr), which
-  // makes the end-of-step barrier unnecessary
-  const int D16 = (D + 15) & ~15;
-  const int ZS = kzz_zstride(D);
-  float* zt = (float*)(xr + Mp * 4 + 3 * Mp * 4);   // M x ZS  Z / l, centred (zero padded)
-  float* zn = zt + M * ZS;             // M
-  float* cm = zn + M;                  // D
-  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const float s2 = hyp[0];
-  const float* ls = hyp + 1;
-#if GPK_KZZ_STAMPS
-  unsigned long long kst[12] = {0};
-#endif
-  KZ_STAMP(0);
-
-  for (int base = 0; base < M * ZS; base += 8 * KT) {   // 8 loads in flight per thread
-    float v[8], l[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = base + u * KT + tid, m = e / ZS, d = e - m * ZS;
-      const bool ok = e < M * ZS && d < D;
-      v[u] = Z[ok ? m * D + d : 0];
-      l[u] = ls[ok ? d : 0];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = base + u * KT + tid, d = e % ZS;
-      if (e < M * ZS) zt[e] = d < D ? v[u] / l[u] : 0.f;
-    }
-  }
-  for (int e = tid; e < 6 * Mp * 4; e += KT) P[e] = 0.0;   // both parities of P / lb / xr
-  lds_barrier();
-  for (int d = wave; d < D; d += KT / 64) {   // column means: one wave per column
-    float sm = 0.f;
-    for (int m = lane; m < M; m += 64) sm += zt[m * ZS + d];
-    sm = wave_sum(sm);
-    if (lane == 0) cm[d] = sm / (float)M;
-  }
-  lds_barrier();
-  for (int e = tid; e < M * ZS; e += KT) {
-    const int d = e % ZS;
-    if (d < D) zt[e] -= cm[d];
-  }
-  lds_barrier();
-  for (int m = tid; m < M; m += KT) {
-    float sm = 0.f;
-    for (int d = 0; d < D; ++d) sm = __builtin_fmaf(zt[m * ZS + d], zt[m * ZS + d], sm);
-    zn[m] = sm;
-  }
-  lds_barrier();
-
-  const int T16 = Mp >> 4;
-  const int ntile = T16 * (T16 + 1) / 2;
-  int its[NS], jts[NS];
-#pragma unroll
-  for (int q = 0; q < NS; ++q) {
-    const int t = wave + 8 * q;
-    int it = T16, jt = T16;   // no tile: coordinates past the end (skipped everywhere)
-    if (t < ntile) tri_of(t, it, jt);
-    its[q] = __builtin_amdgcn_readfirstlane(it);
-    jts[q] = __builtin_amdgcn_readfirstlane(jt);
-  }
-  f64x4 acc[NS];
-  int status = 0;
-  KZ_STAMP(1);
-  for (int attempt = 0; attempt <= max_tries; ++attempt) {
-    double ladder = 0.0;  // GPyTorch adds (jitter_new - jitter_prev) cumulatively
-    {
-      double prev = 0.0, p10 = 1.0;
-      for (int q = 0; q < attempt; ++q) {
-        const double jn = jitter_chol * p10;
-        ladder += jn - prev;
-        prev = jn;
-        p10 *= 10.0;
-      }
-    }
-    // K_ZZ tiles (fp32 arithmetic as the reference's kernel, + jitter, -> fp64 + ladder).
-    // The Gram runs on fp32 MFMA with the A rows fed in the order pi(x) = (x >> 2) + 4 (x & 3),
-    // so the fp32 accumulator (reg r <-> row 4g + r) lands in the fp64 tile layout (row g + 4r).
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-      asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
-      const int j = 16 * jts[q] + c;
-      f32x4 gram = {0.f, 0.f, 0.f, 0.f};
-      if (its[q] < T16) {
-        const int ia = 16 * its[q] + (c >> 2) + 4 * (c & 3);
-        const float* za = zt + (ia < M ? ia : 0) * ZS + 4 * g;
-        const float* zb = zt + (j < M ? j : 0) * ZS + 4 * g;
-        for (int d0 = 0; d0 < D16; d0 += 16) {
-          const float4 av = *(const float4*)(za + d0);
-          const float4 bv = *(const float4*)(zb + d0);
-          gram = mfma32(av.x, bv.x, gram);
-          gram = mfma32(av.y, bv.y, gram);
-          gram = mfma32(av.z, bv.z, gram);
-          gram = mfma32(av.w, bv.w, gram);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * its[q] + g + 4 * r;
-        double v = (i == j) ? 1.0 : 0.0;
-        if (its[q] < T16 && i < M && j < M) {
-          float dist = zn[i] + zn[j] - 2.f * gram[r];
-          dist = dist < 0.f ? 0.f : dist;
-          float kv = s2 * __expf(-0.5f * dist);
-          if (i == j) kv = kv + jitter_var;
-          v = (double)kv;
-          if (i == j) v += ladder;
-        }
-        acc[q][r] = v;
-      }
-    }
-    int failed = 0;
-    KZ_STAMP(2);
-    for (int s = 0; s < (Mp >> 2); ++s) {
-      const int j0 = 4 * s, jt0 = s >> 2, sub = s & 3;
-#if GPK_KZZ_STAMPS
-      unsigned long long ta = __builtin_amdgcn_s_memtime();
-#endif
-      // opaque tile coordinates: the compiler must not hoist every tile's derived LDS
-      // addresses out of the step loop (they would cost more registers than the tiles)
-#pragma unroll
-      for (int q = 0; q < NS; ++q) asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
-      // publish columns j0..j0+3 (tile column jt0, columns 4 sub .. 4 sub + 3), rows >= j0
-#pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        if (jts[q] == jt0 && (c >> 2) == sub) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = 16 * its[q] + g + 4 * r;
-            if (i >= j0) P[i * 4 + (c & 3)] = acc[q][r];
-          }
-        }
-      }
-      lds_barrier();
-      KZ_ACC(6, ta);
-#if GPK_KZZ_STAMPS
-      ta = __builtin_amdgcn_s_memtime();
-#endif
-      double dd[4][4], l4[4][4], l4i[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) dd[r][t] = P[(j0 + r) * 4 + t];
-      int bad = 0;
-#if GPK_KZZ_SKIP & 1
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) l4i[r][t] = (r == t) ? 0.5 : 0.0;
-      if (dd[0][0] == -12345.0) {
-#else
-      if (!chol4(dd, l4, l4i, bad)) {   // uniform: every thread factors the same LDS block
-#endif
-        failed = j0 + bad + 1;
-        break;
-      }
-      for (int i = j0 + tid; i < Mp; i += KT) {   // l_i = P_i L4^{-T}
-        double p[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) p[t] = P[i * 4 + t];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          double v = 0.0;
-#pragma unroll
-          for (int q = 0; q <= t; ++q) v = __builtin_fma(p[q], l4i[t][q], v);
-          lb[i * 4 + t] = v;
-          if (i < M && j0 + t < M && j0 + t <= i) L[(size_t)i * M + j0 + t] = v;
-        }
-      }
-      KZ_ACC(7, ta);
-#if GPK_KZZ_STAMPS
-      ta = __builtin_amdgcn_s_memtime();
-#endif
-      lds_barrier();
-      KZ_ACC(8, ta);
-#if GPK_KZZ_STAMPS
-      ta = __builtin_amdgcn_s_memtime();
-#endif
-      // rank-4 update of every tile with columns beyond the panel: one f64 MFMA each
-#pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        if (its[q] < T16 && 16 * jts[q] + 15 >= j0 + 4 && !(GPK_KZZ_SKIP & 2)) {
-          const double av = lb[(16 * its[q] + c) * 4 + g];
-          const double bv = lb[(16 * jts[q] + c) * 4 + g];
-          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc[q], 0, 0, 0);
-        }
-      }
-      KZ_ACC(9, ta);
-    }
-    if (!failed) {
-      status = attempt > 0 ? -attempt : 0;
-      break;
-    }
-    status = failed;
-    lds_barrier();
-  }
-  KZ_STAMP(3);
-  // L^{-1} is formed by gpk_kzz_inv_kernel (one workgroup per block column), next launch
-  KZ_STAMP(4);
-  for (int i = wave; i < M; i += KT / 64) {   // strict upper triangle of L: one row per wave
-    for (int j = i + 1 + lane; j < M; j += 64) L[(size_t)i * M + j] = 0.0;
-  }
-  if (tid == 0) info[0] = status;
-#if GPK_KZZ_STAMPS
-  KZ_STAMP(5);
-  if (tid == 0) {
-    for (int k = 1; k < 6; ++k) Linv[k] = (double)(kst[k] - kst[k - 1]);
-    for (int k = 6; k < 10; ++k) Linv[k] = (double)kst[k];
-  }
-#endif
-}
-
-// ---------------------------------------------------------------------------
-// L^{-1} of the K_ZZ factor: one workgroup per 16-column block column jb (grid T16), so
-// the block columns run concurrently on different CUs (the serial [L | I] elimination
-// inside the one-workgroup factor kernel took as long as the factorisation). Block
-// forward substitution, right-looking, on fp64 MFMA:
-//   T_u = L_uu^{-1} (the diagonal blocks the column needs, formed in the workgroup),
-//   X_jb = T_jb;  for k = jb ..: S_u += -L_uk X_k (u > k), X_{k+1} = T_{k+1} S_{k+1}.
-// k-order of every MFMA: q = g + 4 kk, so a tile held in acc layout (reg r <-> row g + 4r)
-// is the B operand of k-step kk straight from register kk. S tiles dealt over the 4 waves
-// (u = wave mod 4); the L tiles of the next step are prefetched from L2 during this one.
-// ---------------------------------------------------------------------------
-constexpr int KIT = 256;
-__global__ void __launch_bounds__(KIT)
-gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ info,
-                   double* __restrict__ Linv) {
-  extern __shared__ __attribute__((aligned(16))) double dsm[];
-  const int Mp = (M + 15) & ~15, T16 = Mp >> 4;
-  const int jb = blockIdx.x;
-  const int nb = T16 - jb;            // block rows jb .. T16-1 of this block column
-  double* Tv = dsm;                   // nb x 256: T_{jb+u}, row-major [row][col]
-  double* Xs = Tv + nb * 256;         // nb x 256: X_{jb+u}, row-major
-  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (info[0] > 0) return;           // no factor (the op raises NotPSDError)
-  auto Lat = [&](int i, int j) -> double {   // L with identity padding beyond M
-    if (i < M && j < M) return L[(size_t)i * M + j];
-    return i == j ? 1.0 : 0.0;
-  };
-  for (int e = tid; e < 16 * jb * 16; e += KIT) {   // block rows above the diagonal: zero
-    const int i = e >> 4, j = 16 * jb + (e & 15);
-    if (i < M && j < M) Linv[(size_t)i * M + j] = 0.0;
-  }
-  // diagonal-block inverses: lane group g of wave w takes block u = 4 w + g (+ 16 ...),
-  // lane c its column c by forward substitution
-  for (int u = 4 * wave + g; u < nb; u += 16) {
-    const int b0 = 16 * (jb + u);
-    double lr[16][16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-#pragma unroll
-      for (int q = 0; q <= r; ++q) lr[r][q] = Lat(b0 + r, b0 + q);
-    double x[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      double v = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-      for (int q = 0; q < r; ++q) v = __builtin_fma(-lr[r][q], x[q], v);
-      x[r] = (r >= c) ? v * rcp64(lr[r][r]) : 0.0;
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Tv[u * 256 + r * 16 + c] = x[r];
-  }
-  lds_barrier();
-  for (int e = tid; e < 256; e += KIT) {      // X_jb = T_jb
-    Xs[e] = Tv[e];
-    const int i = 16 * jb + (e >> 4), j = 16 * jb + (e & 15);
-    if (i < M && j < M) Linv[(size_t)i * M + j] = Tv[e];
-  }
-  lds_barrier();
-  f64x4 S[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) S[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-  // A operands of step k: -L_{jb+u, jb+k}[c][g + 4kk] for the wave's tiles u = wave + 4t
-  double an[4][4];
-  auto load_a = [&](int k, double (&dst)[4][4]) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int u = wave + 4 * t;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        dst[t][kk] = (u > k && u < nb) ? -Lat(16 * (jb + u) + c, 16 * (jb + k) + g + 4 * kk) : 0.0;
-    }
-  };
-  load_a(0, an);
-  for (int k = 0; k + 1 < nb; ++k) {
-    double a[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) a[t][kk] = an[t][kk];
-    if (k + 2 < nb) load_a(k + 1, an);
-    double xb[4];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) xb[kk] = Xs[k * 256 + (g + 4 * kk) * 16 + c];
-    const int tn = (k + 1) >> 2;          // slot of S_{k+1} in its owner wave
-    const bool own = wave == ((k + 1) & 3);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int u = wave + 4 * t;
-      if (u > k && u < nb) {
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) S[t] = mfma64(a[t][kk], xb[kk], S[t]);
-      }
-    }
-    if (own) {                            // X_{k+1} = T_{k+1} S_{k+1}
-      f64x4 sv = S[0];
-#pragma unroll
-      for (int t = 1; t < 4; ++t) sv = (t == tn) ? S[t] : sv;
-      f64x4 xv = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) xv = mfma64(Tv[(k + 1) * 256 + c * 16 + g + 4 * kk], sv[kk], xv);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        Xs[(k + 1) * 256 + (g + 4 * r) * 16 + c] = xv[r];
-        const int i = 16 * (jb + k + 1) + g + 4 * r, j = 16 * jb + c;
-        if (i < M && j < M) Linv[(size_t)i * M + j] = xv[r];
-      }
-    }
-    lds_barrier();
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2946,15 +2517,18 @@ gpk_var_kgram_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   for (int e = tid; e < kGPart; e += 256) po[e] = red[e];
 }
 
-// dL^{-1}[p][k] = vm_p u_k + 2 (s_p^2 - 1) sum_{j <= p} L^{-1}[p][j] G[j][k]  (k <= p < M;
-// upper zero) from the reduced totals (fp64). One workgroup.
+// dL^{-1}[p][k] = vm_p u_k + 2 (s_p^2 - 1) (L^{-1} G)[p][k]  (k <= p < M; upper zero) from the
+// reduced totals (fp64). One workgroup: G (symmetric, from its lower tiles) in LDS, wave w
+// forms the 16-row block w of L^{-1} G on fp64 MFMA with its L^{-1} operands requested up
+// front (the triangular k-range: jb <= w).
 __global__ void __launch_bounds__(256)
 gpk_var_gdl_kernel(const double* __restrict__ gtot, const double* __restrict__ Linv,
                    const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
                    double* __restrict__ dLinv) {
   __shared__ double Gs[64][65];
   __shared__ double us[64];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = tid >> 6;
   for (int e = tid; e < kGTiles * 256; e += 256) {   // acc order: tile, reg r, lane (c, g)
     const int t2 = e >> 8, r = (e >> 6) & 3, ln = e & 63;
     int rt = 0;
@@ -2966,17 +2540,33 @@ gpk_var_gdl_kernel(const double* __restrict__ gtot, const double* __restrict__ L
     Gs[col][row] = gtot[e];
   }
   for (int e = tid; e < 64; e += 256) us[e] = gtot[kGTiles * 256 + e];
-  lds_barrier();
-  for (int e = tid; e < M * M; e += 256) {
-    const int p = e / M, k = e - p * M;
-    double v = 0.0;
-    if (k <= p) {
-      double a = 0.0;
-      for (int j = 0; j <= p; ++j) a = __builtin_fma(Linv[(size_t)p * M + j], Gs[j][k], a);
-      const double sd = (double)vstd[p];
-      v = (double)vmean[p] * us[k] + 2.0 * (sd * sd - 1.0) * a;
+  // A operands L^{-1}[16 w + c][16 jb + 4 s + g] for jb <= w, requested before the barrier
+  double la[4][4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int p = 16 * w + c, j = 16 * jb + 4 * s4 + g;
+      const bool ok = jb <= w && p < M && j < M;
+      const double v = Linv[ok ? (size_t)p * M + j : 0];
+      la[jb][s4] = ok ? v : 0.0;
     }
-    dLinv[e] = v;
+  lds_barrier();
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc = mfma64(la[jb][s4], Gs[16 * jb + 4 * s4 + g][16 * kb + c], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = 16 * w + g + 4 * r, k = 16 * kb + c;
+      if (p < M && k < M) {
+        const double sd = (double)vstd[p];
+        dLinv[(size_t)p * M + k] = k <= p ? (double)vmean[p] * us[k] + 2.0 * (sd * sd - 1.0) * acc[r] : 0.0;
+      }
+    }
   }
 }
 
@@ -3277,36 +2867,6 @@ int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t st
   }
 
 }  // namespace
-
-template <int NS>
-int launch_kzz(const GpkKzzArgs& a, size_t lds, hipStream_t stream) {
-  set_lds_once<gpk_kzz_kernel<NS>>();
-  hipLaunchKernelGGL((gpk_kzz_kernel<NS>), dim3(1), dim3(KT), lds, stream, a.Z, a.hyp, a.M, a.D,
-                     a.jitter_var, a.jitter_chol, a.max_tries, a.L, a.Linv, a.info);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  if (GPK_KZZ_STAMPS) return 0;   // (the stamps build reports its clocks through Linv)
-  const int T16 = (a.M + 15) >> 4;
-  set_lds_once<gpk_kzz_inv_kernel>();
-  hipLaunchKernelGGL(gpk_kzz_inv_kernel, dim3(T16), dim3(KIT), (size_t)2 * T16 * 256 * sizeof(double),
-                     stream, a.L, a.M, a.info, a.Linv);
-  e = hipGetLastError();
-  return e == hipSuccess ? 0 : (int)e;
-}
-
-int gpk_launch_kzz(const GpkKzzArgs& a, hipStream_t stream) {
-  const int Mp = (a.M + 15) & ~15;
-  const size_t lds = (size_t)(6 * Mp * 4) * sizeof(double) +
-                     (size_t)(a.M * kzz_zstride(a.D) + a.M + a.D) * sizeof(float);
-  if (lds > 160 * 1024) return -4;
-  const int T16 = Mp >> 4;
-  const int ns = (T16 * (T16 + 1) / 2 + 7) / 8;   // tiles per wave
-  if (ns <= 2) return launch_kzz<2>(a, lds, stream);
-  if (ns <= 5) return launch_kzz<5>(a, lds, stream);
-  if (ns <= 10) return launch_kzz<10>(a, lds, stream);
-  if (ns <= 17) return launch_kzz<17>(a, lds, stream);
-  return -3;
-}
 
 int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream) {
   if (flags != nullptr) {

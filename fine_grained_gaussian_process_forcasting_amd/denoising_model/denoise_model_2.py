@@ -5,6 +5,13 @@ in add_gp_noise (:37) but its definition is commented out (:21), so ``--gp True`
 raises AttributeError there. The evident intent, ``nn.Linear(1, d)``, is restored.
 The reference's global ``torch.autograd.set_detect_anomaly(True)`` (:7) is not
 replicated at import (it is a debugging mode).
+
+forward() runs the two GP blurs of the reference (:46-47, enc then dec through the same
+DeepGPp) as ONE evaluation on the points of both concatenated per window: q(f)'s marginals
+are per point and the layer draws no random numbers (num_likelihood_samples = 1), so the
+enc / dec means and the dec distribution are exactly the two calls' outputs, with one
+variational forward + one adjoint launch chain per step instead of two (and one K_ZZ use).
+``add_gp_noise`` stays the reference's single-input method.
 """
 from __future__ import annotations
 
@@ -46,13 +53,21 @@ class denoise_model_2(nn.Module):
         x_noisy = x + eps_gp
         return x_noisy, dist
 
+    def add_gp_noise_pair(self, enc, dec):
+        """add_gp_noise(enc) and add_gp_noise(dec) (reference :46-47) as one GP evaluation
+        over the concatenated points; returns (enc_noisy, dec_noisy, dist of dec)."""
+        s_enc = enc.shape[1]
+        eps_gp, dist = self.deep_gp.predict(torch.cat([enc, dec], dim=1))
+        e = eps_gp.permute(1, 2, 0)
+        eps = torch.addcmul(self.proj_up.bias, e, self.proj_up.weight.reshape(-1))
+        return enc + eps[:, :s_enc], dec + eps[:, s_enc:], dist.slice_points(s_enc, None)
+
     def forward(self, enc_inputs, dec_inputs):
         eps_enc = torch.randn_like(enc_inputs)
         eps_dec = torch.randn_like(dec_inputs)
         dist = None
         if self.gp:
-            enc_noisy, _ = self.add_gp_noise(enc_inputs)
-            dec_noisy, dist = self.add_gp_noise(dec_inputs)
+            enc_noisy, dec_noisy, dist = self.add_gp_noise_pair(enc_inputs, dec_inputs)
         elif self.n_noise:
             enc_noisy = enc_inputs
             dec_noisy = dec_inputs

@@ -186,12 +186,14 @@ class MultivariateNormal:
     """
 
     def __init__(self, mean: torch.Tensor, variance: Optional[torch.Tensor] = None,
-                 exact=None, added_noise=None, clamp_flag: Optional[torch.Tensor] = None):
+                 exact=None, added_noise=None, clamp_flag: Optional[torch.Tensor] = None,
+                 preclamped: bool = False):
         self._mean = mean
         self._variance = variance
         self._exact = exact                # (X, kernel hyper) for exact-GP priors
         self._added_noise = added_noise    # likelihood noise folded in by GaussianLikelihood
         self._clamp_flag = clamp_flag      # (1,) int32 from gpk_variational_f32: clamp fired
+        self._preclamped = preclamped      # variance already clamped by the kernel, no flag
 
     @property
     def mean(self):
@@ -217,6 +219,12 @@ class MultivariateNormal:
         if self._added_noise is not None:
             var = var + self._added_noise
         min_var = settings.min_variance.value(var.dtype)
+        if self._preclamped and self._added_noise is None:
+            # a point slice of a kernel output: a clamped entry is exactly min_var
+            from .ops import record_or_run
+            flag = (var <= min_var).any().to(torch.int32).reshape(1)
+            record_or_run("clamp", (flag, min_var), lambda: warn_if_clamped(flag, min_var))
+            return var
         if self._clamp_flag is not None and self._added_noise is None:
             # the kernel already clamped (fp32 min_variance); it tells us whether it did:
             # one host read of the flag, as GPyTorch's own .lt(min_var).any() sync
@@ -240,11 +248,22 @@ class MultivariateNormal:
         batch_size = torch.Size(batch_size)
         mean = self._mean.expand(*batch_size, *self.event_shape)
         var = self._variance.expand(*batch_size, *self.event_shape) if self._variance is not None else None
-        return MultivariateNormal(mean, var, self._exact, self._added_noise, self._clamp_flag)
+        return MultivariateNormal(mean, var, self._exact, self._added_noise, self._clamp_flag,
+                                  self._preclamped)
 
     def add_noise(self, noise):
         total = noise if self._added_noise is None else self._added_noise + noise
-        return MultivariateNormal(self._mean, self._variance, self._exact, total, self._clamp_flag)
+        return MultivariateNormal(self._mean, self._variance, self._exact, total, self._clamp_flag,
+                                  self._preclamped)
+
+    def slice_points(self, start, stop):
+        """The marginals of points [start, stop) (diagonal-query outputs of the variational
+        path only): the clamp warning then reflects exactly the sliced points."""
+        if self._exact is not None or self._variance is None:
+            raise NotImplementedError("point slices are defined for variational outputs")
+        sl = (Ellipsis, slice(start, stop))
+        return MultivariateNormal(self._mean[sl], self._variance[sl], None, self._added_noise, None,
+                                  preclamped=self._clamp_flag is not None or self._preclamped)
 
     def log_prob(self, value: torch.Tensor) -> torch.Tensor:
         """Exact-GP marginal log density (fused RBF + Cholesky + solve + logdet kernel)."""

@@ -35,7 +35,10 @@ read, so every replay that a check covers is bracketed: the parameters and the
 optimizer state are snapshotted (device copies) when a check block starts, a sticky
 device flag collects every hard failure (info > 0) of every replay in the block, and
 on a failure the snapshot is restored before the error is raised -- the parameters
-and Adam moments come back exactly as they were before the failing block.
+and Adam moments come back exactly as they were before the failing block. Every
+replay condenses its verdicts into a device ring slot, so a block of ``check_every``
+replays is checked with ONE host sync and still warns once per replay, in order
+(``check_every`` > 1 keeps the replays back to back on the GPU).
 
 The ``warmup`` eager steps that precede the capture are real
 training steps on the sample inputs (PyTorch's documented whole-network capture
@@ -83,7 +86,7 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
 
         self.graph = torch.cuda.CUDAGraph()
-        self.checks = ops.DeferredChecks(device=self.static_inputs[0].device)
+        self.checks = ops.DeferredChecks(device=self.static_inputs[0].device, slots=check_every)
         optimizer.zero_grad(set_to_none=True)
         ops._RECORDERS.append(self.checks)
         try:
@@ -93,6 +96,7 @@ class GraphedStep:
                 self.static_outputs = self.loss_fn(*self.static_inputs)
                 self._loss(self.static_outputs).backward()
                 self.optimizer.step()
+                self.checks.finalize()     # this replay's verdicts -> the device ring
         finally:
             ops._RECORDERS.remove(self.checks)
         invalidate_caches()
@@ -143,7 +147,7 @@ class GraphedStep:
         if self._n % self.check_every == 0:
             self._block_open = False
             try:
-                self.checks.check()
+                self.checks.check(self.check_every)
             except Exception:
                 self.rollback()
                 raise

@@ -172,17 +172,29 @@ class DeferredChecks:
     """Host-side verdicts recorded while a HIP graph is being captured.
 
     A captured step cannot read device memory on the host (the capture would break),
-    so psd_safe_cholesky's info check and the variance-clamp flag are RECORDED instead:
-    the recorded tensors live in the graph's memory pool and are rewritten by every
-    replay, so ``check()`` after a replay raises / warns exactly as the eager call
-    would have for that replay's data (graphs.GraphedStep calls it).
+    so psd_safe_cholesky's info check and the variance-clamp flag are RECORDED instead.
+    Each recorded check is condensed IN THE GRAPH into a 3-int verdict (max info,
+    ladder steps, NaN in the inputs / clamp bit), and ``finalize()`` (captured at the
+    end of the step) writes the step's verdicts into slot ``replay % slots`` of a device
+    ring. ``check(n)`` after n replays reads the ring with ONE device->host copy and
+    warns / raises for each of the n replays in order, exactly as the eager calls would
+    have -- so a block of ``slots`` replays costs one host sync, not one per check.
     """
 
-    def __init__(self, device=None):
+    MAX_ITEMS = 16   # recorded checks per step (the cfg-3 step records 2-3)
+
+    def __init__(self, device=None, slots: int = 1):
         self.items = []
-        # (1,) int32 device flag: any hard failure since reset_sticky(). Allocated before
-        # the capture (a tensor created inside it would be re-zeroed by every replay)
+        self.slots = max(1, int(slots))
+        self._verdicts = []
+        self.ring = None
+        # (1,) int32 device flag: any hard failure since reset_sticky(); (1,) int64 replay
+        # counter. Allocated before the capture (a tensor created inside it would be
+        # re-zeroed by every replay)
         self.sticky = torch.zeros(1, dtype=torch.int32, device=device) if device is not None else None
+        self.counter = torch.zeros(1, dtype=torch.int64, device=device) if device is not None else None
+        self._ring = (torch.zeros(self.slots, self.MAX_ITEMS, 3, dtype=torch.int32, device=device)
+                      if device is not None else None)
 
     def add(self, kind: str, args: tuple) -> None:
         self.items.append((kind, args))
@@ -195,22 +207,82 @@ class DeferredChecks:
                 raise RuntimeError("DeferredChecks used in a capture without a device flag "
                                    "(construct it with device=...)")
             self.sticky.copy_(torch.maximum(self.sticky, (info > 0).any().to(torch.int32).reshape(1)))
+            inputs = [t for t in args[4] if t is not None]
+            nan = torch.zeros((), dtype=torch.int32, device=info.device)
+            for t in inputs:
+                nan = nan | torch.isnan(t).any().to(torch.int32)
+            self._verdicts.append(torch.stack([info.max().to(torch.int32),
+                                               (-info).max().clamp_min(0).to(torch.int32), nan]))
+        else:
+            flag = args[0]
+            z = torch.zeros((), dtype=torch.int32, device=flag.device)
+            self._verdicts.append(torch.stack([flag.reshape(-1)[0].to(torch.int32), z, z]))
+
+    def finalize(self) -> None:
+        """Captured at the end of the step: this replay's verdicts -> ring slot."""
+        if not self._verdicts or self.counter is None:
+            return
+        if len(self._verdicts) > self.MAX_ITEMS:
+            raise RuntimeError(f"more than {self.MAX_ITEMS} numerical checks recorded in one step")
+        v = torch.stack(self._verdicts)                                # (n_items, 3)
+        n = v.shape[0]
+        # masked write of slot (replay mod slots): no index kernels, the ring was allocated
+        # before the capture (outside the graph's private pool)
+        hit = (torch.arange(self.slots, device=v.device) == self.counter % self.slots).view(-1, 1, 1)
+        self._ring[:, :n].copy_(torch.where(hit, v.unsqueeze(0), self._ring[:, :n]))
+        self.counter.add_(1)
+        self.ring = self._ring[:, :n]
 
     def reset_sticky(self) -> None:
         if self.sticky is not None:
             self.sticky.zero_()
 
-    def check(self) -> None:
-        for kind, args in self.items:
-            if kind == "cholesky":
-                info, jitter, what, max_tries, inputs = args
-                check_cholesky_info(info, jitter, inputs, what, max_tries)
-            else:
-                from .gp import warn_if_clamped
-                warn_if_clamped(*args)
+    def _replay_verdicts(self, n: int):
+        """Host copy of the last n replays' verdicts, oldest first (one sync)."""
+        both = torch.cat([self.ring.reshape(-1).to(torch.int64), self.counter.reshape(-1)]).cpu()
+        cnt = int(both[-1])
+        ring = both[:-1].reshape(self.ring.shape)
+        n = min(n, self.slots, cnt)
+        return [ring[(cnt - n + r) % self.slots] for r in range(n)]
+
+    def check(self, n: int = 1) -> None:
+        if self.ring is None:        # nothing condensed (e.g. recorded outside GraphedStep)
+            for kind, args in self.items:
+                if kind == "cholesky":
+                    info, jitter, what, max_tries, inputs = args
+                    check_cholesky_info(info, jitter, inputs, what, max_tries)
+                else:
+                    from .gp import warn_if_clamped
+                    warn_if_clamped(*args)
+        else:
+            for verdicts in self._replay_verdicts(n):
+                for (kind, args), v in zip(self.items, verdicts.tolist()):
+                    if kind == "cholesky":
+                        _raise_or_warn_verdict(v, args[1], args[2], args[3])
+                    elif v[0] & 1:
+                        from .gp import warn_if_clamped
+                        warn_if_clamped(torch.ones(1, dtype=torch.int32), args[1])
         if self.sticky is not None and int(self.sticky.item()) != 0:
             raise NotPSDError("a replay of this check block failed psd_safe_cholesky (not PD after "
                               "the jitter ladder, or NaN inputs); state rolled back to the block start")
+
+
+def _raise_or_warn_verdict(v, jitter: float, what: str, max_tries: int) -> None:
+    """check_cholesky_info from a condensed verdict [max info, ladder steps, NaN inputs]."""
+    max_info, steps, nan = v
+    if max_info >= INFO_TIMEOUT:
+        raise GpkInternalError(f"{what}: kernel spin-wait timed out (info = 1<<20)")
+    failed = max_info > 0
+    if failed and nan:
+        raise NanError(f"{what}: NaN elements in the inputs.")
+    if failed:
+        steps = max_tries
+    for i in range(steps):
+        warnings.warn(f"A not p.d., added jitter of {jitter * (10 ** i):.1e} to the diagonal",
+                      NumericalWarning)
+    if failed:
+        raise NotPSDError(f"Matrix not positive definite after repeatedly adding jitter up to "
+                          f"{jitter * 10 ** (max_tries - 1):.1e}.")
 
 
 _RECORDERS: list = []

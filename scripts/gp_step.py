@@ -15,7 +15,8 @@ synthetic traffic-like frame): no per-step host->device copy.
 
 GP share = t(step with gp=True) - t(step with the GP blur off, same backbone work).
 Both eager (the reference's loop) and HIP-graph-captured (graphs.GraphedStep: one graph
-launch per step) timings are reported.
+launch per step, the numerical verdicts of 10 replays read with one host sync) timings
+are reported.
 
     python scripts/gp_step.py [cfg3|cfg1] [steps] [graph-gp]
 """
@@ -133,7 +134,10 @@ def run(cfg, steps, modes=("eager", "graph", "eager_anomaly"), gps=(True, False)
                     for k in range(3):
                         step(k)
                 else:
-                    gstep = GraphedStep(lambda enc, dec, y: model(enc, dec, y), opt, batches[0])
+                    # the verdicts of 10 replays are read with one host sync (per-replay
+                    # warnings preserved, graphs.GraphedStep): replays stay back to back
+                    gstep = GraphedStep(lambda enc, dec, y: model(enc, dec, y), opt, batches[0],
+                                        check_every=10)
 
                     def step(k):
                         return gstep(*batches[k % len(batches)])

@@ -3,7 +3,7 @@
 # first, K_ZZ timings, then the whole GPU suite, smoke, bench and the graphed cfg-3 step
 # kernel stats with / without the GP branch
 set -o pipefail
-R="$GRAFT_REPO_ROOT"; cd "$R"; O=gpurun_out/r03p; mkdir -p $O
+R="$GRAFT_REPO_ROOT"; cd "$R"; O=gpurun_out/${OUT:-r03p}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_elbo_gpu.py "tests/test_variational_gpu.py" "tests/test_variational_grad_gpu.py" > $O/quick.log 2>&1 || { tail -40 $O/quick.log; exit 1; }
 tail -n 2 $O/quick.log

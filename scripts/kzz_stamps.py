@@ -1,7 +1,7 @@
-"""Phase clocks of a GPK_KZZ_STAMPS=1 build (GPK_LIB): Linv[0][1..9] =
-prologue, tile build, phase 1, phase 2, zero fill, then phase-1 step parts
-(publish+barrier, chol+l rows, barrier, update) summed over steps.
-   python scripts/kzz_stamps.py [M] [D]"""
+"""Per-step phase clocks of a GPK_KZZ_STAMPS=1 build of gpk_kzz16_kernel (load it with
+GPK_LIB=<path>): info[1 + 3k .. 3 + 3k] = s_memtime at step k's start, after its diagonal
+barrier and after its TRSM barrier (workgroup thread 0, first attempt).
+   GPK_LIB=... python scripts/kzz_stamps.py [M] [D]"""
 import math
 import os
 import sys
@@ -9,17 +9,35 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from fine_grained_gaussian_process_forcasting_amd import ops  # noqa: E402
+from fine_grained_gaussian_process_forcasting_amd import _native  # noqa: E402
 
 M, D = (int(v) for v in (sys.argv[1:] + ["256", "32"])[:2])
 LN2 = math.log(2.0)
 dev = torch.device("cuda", 0)
 g = torch.Generator().manual_seed(0)
 Z = (torch.randn(M, D, generator=g) / math.sqrt(D)).to(dev)
-kz_h = torch.cat([torch.tensor([LN2]), torch.full((D,), LN2)]).to(dev)
+h = torch.cat([torch.tensor([LN2]), torch.full((D,), LN2)]).to(dev)
+T = (M + 15) // 16
+L = torch.empty(M, M, dtype=torch.float64, device=dev)
+Li = torch.empty(M, M, dtype=torch.float64, device=dev)
+info = torch.zeros(4 + 3 * T, dtype=torch.int32, device=dev)
+lib = _native.lib()
 for _ in range(3):
-    kz = ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h)
+    rc = lib.gpk_kzz_chol_f64(Z.data_ptr(), h.data_ptr(), M, D, 1e-4, 1e-8, 3, L.data_ptr(), Li.data_ptr(),
+                              info.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
 torch.cuda.synchronize()
-v = kz.Linv[0, 1:10].cpu().tolist()
-names = ["prologue", "build", "phase1", "phase2", "zero", "p1.publish", "p1.chol_rows", "p1.barrier2", "p1.update"]
-print(f"M={M} D={D} info={int(kz.info[0])} " + " ".join(f"{n}={x:.0f}" for n, x in zip(names, v)), flush=True)
+v = info.cpu().tolist()
+st = [v[1 + 3 * k: 4 + 3 * k] for k in range(T)]
+rows = []
+for k in range(T):
+    nxt = st[k + 1][0] if k + 1 < T else None
+    diag = (st[k][1] - st[k][0]) & 0xffffffff
+    trsm = (st[k][2] - st[k][1]) & 0xffffffff
+    upd = ((nxt - st[k][2]) & 0xffffffff) if nxt is not None else 0
+    rows.append((diag, trsm, upd))
+print(f"M={M} D={D} info={v[0]}  per step (s_memtime ticks): diag+barrier / trsm+barrier / update")
+for k, (a, b, c) in enumerate(rows):
+    print(f"k={k:2d} {a:7d} {b:7d} {c:7d}")
+tot = [sum(r[i] for r in rows) for i in range(3)]
+print("sum", tot, "total", sum(tot))

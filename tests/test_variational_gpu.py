@@ -60,7 +60,9 @@ def test_kzz_cholesky_parity(cuda_device, M, D):
                                              # (row blocks, dims) instantiation, ragged M / N
                                              (3, 70, 100, 7, True), (2, 50, 96, 20, True),
                                              (2, 33, 180, 40, True), (2, 64, 256, 16, True),
-                                             (1, 40, 250, 64, True), (5, 192, 256, 32, True)])
+                                             (1, 40, 250, 64, True), (5, 192, 256, 32, True),
+                                             # M <= 64 with D in (32, 64]: the LDS-tiled path
+                                             (3, 40, 48, 48, True), (2, 30, 64, 64, True)])
 def test_variational_parity(cuda_device, B, N, M, D, trained):
     from fine_grained_gaussian_process_forcasting_amd import ops
     X, Z, m, s, w, b0, y = _case(B, N, M, D, seed=B * 7 + N, trained=trained)

@@ -22,7 +22,9 @@ def _rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-@pytest.mark.parametrize("B,N,M,D", [(4, 24, 16, 8), (3, 40, 32, 16), (2, 64, 64, 32), (2, 20, 8, 4)])
+@pytest.mark.parametrize("B,N,M,D", [(4, 24, 16, 8), (3, 40, 32, 16), (2, 64, 64, 32), (2, 20, 8, 4),
+                                     # D in (32, 64] at M <= 64 (DQ = 64 variants)
+                                     (3, 40, 48, 48), (2, 30, 64, 64)])
 def test_variational_grads_vs_oracle(cuda_device, B, N, M, D):
     from fine_grained_gaussian_process_forcasting_amd import ops_autograd
     g = torch.Generator().manual_seed(B * 1000 + N + M)
