@@ -224,7 +224,9 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed, label="BASELINE
                               "achieved": sum(var_adj_flops_per_window(N, M, D)) * B / (ms["bwd"] * 1e-3) / 1e12,
                               "peak": sum(var_adj_flops_per_window(N, M, D)) / adj_roof_s / 1e12,
                               "unit": "TFLOP/s", "frac": adj_roof_s * B / (ms["bwd"] * 1e-3),
-                              "flops_per_window": dict(zip(("fp32", "fp64"), var_adj_flops_per_window(N, M, D)))},
+                              "flops_per_window": dict(zip(("fp32", "fp64"), var_adj_flops_per_window(N, M, D))),
+                              "traffic": load_traffic(f"var_adjoint_B{B}_N{N}_M{M}_D{D}"),
+                              "algorithmic_bytes": 4 * (2 * B * N * D + 2 * B * N)},
         "mean_ell": float(out.ell.double().mean()),
         "elbo_rel_err_vs_fp64_oracle": elbo_rel_err(X, y, Z, ls, w, vm, vs, out.ell, D),
         "info": int(kz.info.item()),

@@ -81,13 +81,23 @@ def main():
         json.dump({"bench": rows, "var3_leg": rows3}, fo, indent=1)
     summary = {}
     for k, v in rows.items():
-        if k.startswith("gpk_exact_kernel<16, 8, false, true>"):   # N=256 (not the cfg-2 leg)
+        if k.startswith("gpk_exact_kernel<16, 8, false, true") and k.endswith("grid=262144"):   # B=512 N=256
             summary["exact_B512_N256_D32"] = {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
                                               "source": "profiles/r03_pmc.json bench " + k}
         if k.startswith("gpk_var_fwd_r_kernel<32>"):
             summary["var_B1024_N256_M64_D32"] = {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
                                                  "fetch_raw_bytes": v["fetch_bytes_raw"],
                                                  "source": "profiles/r03_pmc.json bench " + k}
+    adj = [v for k, v in rows.items() if k.split(" grid")[0] in (
+        "gpk_var_adj_r_kernel<32>", "gpk_var_kgram_r_kernel<32>", "gpk_var_gdl_kernel", "gpk_var_fin_kernel")
+        or (k.startswith("gpk_var_red_kernel") and not k.endswith("grid=596736"))]
+    if adj:
+        summary["var_adjoint_B1024_N256_M64_D32"] = {
+            "hbm_bytes_per_launch": sum(v["hbm_bytes_per_launch"] for v in adj),
+            "hbm_bytes_per_launch_raw": sum(v["fetch_bytes_raw"] + v["write_bytes"] for v in adj),
+            "hbm_bytes_per_launch_x2": sum(v["hbm_bytes_per_launch"] for v in adj),
+            "algorithmic_bytes": 4 * (2 * 1024 * 256 * 32 + 2 * 1024 * 256),
+            "source": "profiles/r03_pmc.json bench gpk_var_adj_r / kgram_r / red / gdl / fin"}
     with open(os.path.join(OUT, "pmc_summary.json"), "w") as fo:
         json.dump(summary, fo, indent=1)
     print(json.dumps(summary, indent=1))
