@@ -162,6 +162,21 @@ int gpk_meanfield_kl_f32(const float* m, const float* s, int M, float* kl, const
   return gpk_launch_kl(m, s, M, kl, gkl, dm, ds, (hipStream_t)stream);
 }
 
+int gpk_record_check(const int* info, int n, const float* in0, long long n0, const float* in1,
+                     long long n1, int kind, int* ring, long long* counter, int slots, int item,
+                     int items, int* sticky, void* stream) {
+  if (kind < 0 || kind > 2) return -7;
+  if (kind != 2 && info == nullptr) return -1;
+  if (kind == 0 && (n < 1 || (n0 > 0 && in0 == nullptr) || (n1 > 0 && in1 == nullptr))) return -2;
+  if (ring == nullptr && kind != 2) return -8;
+  if (counter == nullptr) return -9;
+  if (slots < 1) return -10;
+  if (kind != 2 && (item < 0 || item >= items)) return -11;
+  if (kind == 0 && sticky == nullptr) return -13;
+  return gpk_launch_verdict(info, n, in0, n0, in1, n1, kind, ring, counter, slots, item, items, sticky,
+                            kind == 2, (hipStream_t)stream);
+}
+
 int gpk_variational_f32(const float* X, const float* Z, const double* Linv, const float* vmean,
                         const float* vstd, const float* hyp, const float* y, int B, int N, int M,
                         int D, float* mean, float* var, float* ell, int* flags, void* stream) {

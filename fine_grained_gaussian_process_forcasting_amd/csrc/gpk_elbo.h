@@ -9,3 +9,6 @@ int gpk_launch_ell_grad(const float* y, const float* mean, const float* var, con
                         float* dnoise_part, hipStream_t stream);
 int gpk_launch_kl(const float* m, const float* s, int M, float* kl, const float* gkl, float* dm,
                   float* ds, hipStream_t stream);
+int gpk_launch_verdict(const int* info, int n, const float* in0, long long n0, const float* in1,
+                       long long n1, int kind, int* ring, long long* counter, int slots, int item,
+                       int items, int* sticky, int advance, hipStream_t stream);

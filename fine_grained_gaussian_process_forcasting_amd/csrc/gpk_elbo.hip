@@ -111,3 +111,82 @@ int gpk_launch_kl(const float* m, const float* s, int M, float* kl, const float*
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
+
+// ---------------------------------------------------------------------------
+// Verdict of one recorded numerical check of a HIP-graph replay (graphs.GraphedStep):
+// ring[slot][item] = {max info, max(-info, 0), NaN in the inputs} (kind 0: a
+// psd_safe_cholesky info vector) or {flag, 0, 0} (kind 1: the variance-clamp flag word),
+// slot = counter % slots; sticky |= (max info > 0) for kind 0; kind 2 only bumps the replay
+// counter (the step's end). The NaN scan runs only for a failed factorisation. One
+// workgroup: replaces ~10 small torch reductions per recorded check.
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256)
+gpk_verdict_kernel(const int* __restrict__ info, int n, const float* __restrict__ in0, long long n0,
+                   const float* __restrict__ in1, long long n1, int kind, int* __restrict__ ring,
+                   long long* __restrict__ counter, int slots, int item, int items, int* __restrict__ sticky,
+                   int advance) {
+  __shared__ int red[3][4];
+  __shared__ int fail;
+  const int tid = threadIdx.x;
+  if (kind == 2) {   // the step's end: advance the replay counter only
+    if (tid == 0) counter[0] = counter[0] + 1;
+    return;
+  }
+  int mx = -2147483647, mn = 0, nan = 0;
+  if (kind == 0) {
+    for (int i = tid; i < n; i += 256) {
+      const int v = info[i];
+      mx = v > mx ? v : mx;
+      mn = -v > mn ? -v : mn;
+    }
+  } else if (tid == 0) {
+    mx = info[0];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mx = max(mx, __shfl_xor(mx, off, 64));
+    mn = max(mn, __shfl_xor(mn, off, 64));
+  }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = mx;
+    red[1][tid >> 6] = mn;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w) {
+      mx = max(mx, red[0][w]);
+      mn = max(mn, red[1][w]);
+    }
+    fail = kind == 0 && mx > 0;
+  }
+  __syncthreads();
+  if (fail) {   // NaN scan of the inputs only for a failed factorisation (as the eager check)
+    for (long long i = tid; i < n0; i += 256) nan |= (in0[i] != in0[i]);
+    for (long long i = tid; i < n1; i += 256) nan |= (in1[i] != in1[i]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nan |= __shfl_xor(nan, off, 64);
+    if ((tid & 63) == 0) red[2][tid >> 6] = nan;
+    __syncthreads();
+    if (tid == 0) nan = (red[2][0] | red[2][1]) | (red[2][2] | red[2][3]);
+  }
+  if (tid == 0) {
+    const long long cnt = counter[0];
+    int* dst = ring + ((size_t)(cnt % slots) * items + item) * 3;
+    dst[0] = mx;
+    dst[1] = kind == 0 ? mn : 0;
+    dst[2] = kind == 0 ? nan : 0;
+    if (kind == 0 && mx > 0) sticky[0] = 1;
+    if (advance) counter[0] = cnt + 1;
+  }
+}
+}  // namespace
+
+int gpk_launch_verdict(const int* info, int n, const float* in0, long long n0, const float* in1,
+                       long long n1, int kind, int* ring, long long* counter, int slots, int item,
+                       int items, int* sticky, int advance, hipStream_t stream) {
+  hipLaunchKernelGGL(gpk_verdict_kernel, dim3(1), dim3(256), 0, stream, info, n, in0, n0, in1, n1, kind,
+                     ring, counter, slots, item, items, sticky, advance);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}

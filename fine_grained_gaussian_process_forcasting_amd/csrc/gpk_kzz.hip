@@ -58,7 +58,7 @@ GPK_DEVICE double readlane_d(double v, int lane) {
 }
 
 #ifndef GPK_KZZ_WAVES
-#define GPK_KZZ_WAVES 8
+#define GPK_KZZ_WAVES 16   // 15 workers + the diagonal wave (4 waves / SIMD, 128 VGPRs each)
 #endif
 #ifndef GPK_KZZ_STAMPS
 #define GPK_KZZ_STAMPS 0   // debug: per-step phase clocks into info[1..] (results still valid)
@@ -171,9 +171,8 @@ GPK_DEVICE double ladder_of(int attempt, double jitter_chol) {   // GPyTorch: cu
   return ladder;
 }
 
-// Waves 0 .. KW-2 are WORKERS holding the upper triangle's tiles (whole block columns, greedy
-// balanced: columns T-1 .. 0 each to the least-loaded worker); wave KW-1 is the DIAGONAL wave
-// and holds no tile. Per step k:
+// Waves 0 .. KW-2 are WORKERS holding the upper triangle's tiles (dealt round-robin in
+// column-major order); wave KW-1 is the DIAGONAL wave and holds no tile. Per step k:
 //   [A] barrier: L_kk, L_kk^{-1} (LDS) and the step's status are out;
 //   [B] workers: TRSM of block row k -> LDS panel + L; diagonal wave: the diagonal blocks of
 //       L and L^{-1} to HBM; barrier;
@@ -285,35 +284,17 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
     }
   } else {
     // ================= workers =================
-    // greedy balanced block-column assignment (identical on every wave)
+    // upper tiles in column-major order t = j (j + 1) / 2 + i, dealt round-robin to the workers
     int its[NS], jts[NS];
     {
-      int load[NWK];
-#pragma unroll
-      for (int w = 0; w < NWK; ++w) load[w] = 0;
-      int n = 0;
-#pragma unroll
-      for (int q = 0; q < NS; ++q) { its[q] = T; jts[q] = T; }
-      for (int col = T - 1; col >= 0; --col) {
-        int best = 0;
-#pragma unroll
-        for (int w = 1; w < NWK; ++w) best = load[w] < load[best] ? w : best;
-#pragma unroll
-        for (int w = 0; w < NWK; ++w) load[w] += (w == best) ? col + 1 : 0;
-        if (best == wave) {
-          for (int r0 = 0; r0 <= col; ++r0) {
-#pragma unroll
-            for (int q = 0; q < NS; ++q) {
-              if (q == n) { its[q] = r0; jts[q] = col; }
-            }
-            ++n;
-          }
-        }
-      }
+      const int ntile = T * (T + 1) / 2;
 #pragma unroll
       for (int q = 0; q < NS; ++q) {
-        its[q] = __builtin_amdgcn_readfirstlane(its[q]);
-        jts[q] = __builtin_amdgcn_readfirstlane(jts[q]);
+        const int t = wave + NWK * q;
+        int it = T, jt = T;   // no tile: coordinates past the end (skipped everywhere)
+        if (t < ntile) tile_of(t, T, it, jt);
+        its[q] = __builtin_amdgcn_readfirstlane(it);
+        jts[q] = __builtin_amdgcn_readfirstlane(jt);
       }
     }
     f64x4 acc[NS];
@@ -536,18 +517,12 @@ int launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
 
 int gpk_launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
   const int T = (a.M + 15) >> 4;
-  // tiles per worker: whole block columns, greedily balanced over KW - 1 workers
-  int load[32] = {0}, ns = 0;
-  for (int col = T - 1; col >= 0; --col) {
-    int best = 0;
-    for (int w = 1; w < KW - 1; ++w) best = load[w] < load[best] ? w : best;
-    load[best] += col + 1;
-    ns = load[best] > ns ? load[best] : ns;
-  }
+  const int ns = (T * (T + 1) / 2 + KW - 2) / (KW - 1);   // tiles per worker (round-robin)
+  if (ns <= 2) return launch_kzz16<2>(a, stream);
   if (ns <= 4) return launch_kzz16<4>(a, stream);
-  if (ns <= 8) return launch_kzz16<8>(a, stream);
-  if (ns <= 12) return launch_kzz16<12>(a, stream);
-  if (ns <= 16) return launch_kzz16<16>(a, stream);
+  if (ns <= 7) return launch_kzz16<7>(a, stream);
+  if (ns <= 10) return launch_kzz16<10>(a, stream);
+  if (ns <= 17) return launch_kzz16<17>(a, stream);
   if (ns <= 21) return launch_kzz16<21>(a, stream);
   return -3;
 }

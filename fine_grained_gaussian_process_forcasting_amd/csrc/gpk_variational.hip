@@ -2433,25 +2433,61 @@ gpk_var_kgram_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   float u[4] = {0.f, 0.f, 0.f, 0.f};
   const int nch = (N + 31) / 32;
   const long long total = (long long)B * nch;
-  for (long long t = (long long)blockIdx.x * 4 + wave; t < total; t += (long long)gridDim.x * 4) {
+  const long long stride = (long long)gridDim.x * 4;
+  // the next chunk's raw point values and weights are requested before this chunk's math
+  // (software pipeline over the wave's chunks: one memory latency per wave, not per chunk)
+  float rx[2][DQ / 4], gvr[2][4], gmr[2][4];
+  auto fetch = [&](long long t, float (&x)[2][DQ / 4], float (&gv)[2][4], float (&gm)[2][4]) {
     const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
     const size_t col0 = (size_t)b * N;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = i0 + 16 * q + c;
+      const float* xr = X + (col0 + (i < N ? i : 0)) * D;
+#pragma unroll
+      for (int s4 = 0; s4 < DQ / 4; ++s4) {
+        const int d = 4 * s4 + g;
+        x[q][s4] = xr[d < D ? d : 0];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = i0 + 16 * q + 4 * g + r;
+        const size_t e = col0 + (ii < N ? ii : 0);
+        gv[q][r] = wsgv[e];
+        gm[q][r] = gmean[e];
+      }
+    }
+  };
+  long long t = (long long)blockIdx.x * 4 + wave;
+  if (t < total) fetch(t, rx, gvr, gmr);
+  for (; t < total; t += stride) {
+    const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
     const float* sm = fresh_lds(vsm);
     const float* zs = sm + L::zs;
     const float* zn = sm + L::zn;
     RegPoints<DQ> P;
-    load_points<DQ, false>(X, N, D, b, i0, il, cmv, wv, P);
-    // per-register point weights (point 16 q + 4 g + r), requested up front
-    float gvr[2][4], gmr[2][4];
+    float gvc[2][4], gmc[2][4];
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2; ++q) {
+      const int i = i0 + 16 * q + c;
+      float nn = 0.f;
+#pragma unroll
+      for (int s4 = 0; s4 < DQ / 4; ++s4) {
+        const int d = 4 * s4 + g;
+        const float v = (i < N && d < D) ? rx[q][s4] * il[s4] - cmv[s4] : 0.f;
+        P.xb[q][s4] = v;
+        nn = __builtin_fmaf(v, v, nn);
+      }
+      nn += __shfl_xor(nn, 16, 64);
+      nn += __shfl_xor(nn, 32, 64);
+      P.xn[q] = nn;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = i0 + 16 * q + 4 * g + r;
-        const size_t e = col0 + (i < N ? i : 0);
-        gvr[q][r] = wsgv[e];
-        gmr[q][r] = gmean[e];
+        gvc[q][r] = gvr[q][r];
+        gmc[q][r] = gmr[q][r];
       }
+    }
+    if (t + stride < total) fetch(t + stride, rx, gvr, gmr);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       float xn[4];
@@ -2472,8 +2508,8 @@ gpk_var_kgram_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
           const float d2 = __builtin_fmaxf(znp + xn[r] - 2.f * acc[r], 0.f);
           const float kv = ok ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * d2) : 0.f;
           KT[rt][r] = kv;
-          W[rt][r] = kv * gvr[q][r];
-          u[rt] = __builtin_fmaf(gmr[q][r], kv, u[rt]);
+          W[rt][r] = kv * gvc[q][r];
+          u[rt] = __builtin_fmaf(gmc[q][r], kv, u[rt]);
         }
       }
       // G(rt, rt') += K_rt diag(gv) K_rt'^T = sum_s mfma(KT_rt.reg[s], W_rt'.reg[s])

@@ -174,9 +174,9 @@ class DeferredChecks:
     A captured step cannot read device memory on the host (the capture would break),
     so psd_safe_cholesky's info check and the variance-clamp flag are RECORDED instead.
     Each recorded check is condensed IN THE GRAPH into a 3-int verdict (max info,
-    ladder steps, NaN in the inputs / clamp bit), and ``finalize()`` (captured at the
-    end of the step) writes the step's verdicts into slot ``replay % slots`` of a device
-    ring. ``check(n)`` after n replays reads the ring with ONE device->host copy and
+    ladder steps, NaN in the inputs / clamp bit) by one gpk_record_check launch, written
+    into slot ``replay % slots`` of a device ring; ``finalize()`` (captured at the end of
+    the step) advances the replay counter. ``check(n)`` after n replays reads the ring with ONE device->host copy and
     warns / raises for each of the n replays in order, exactly as the eager calls would
     have -- so a block of ``slots`` replays costs one host sync, not one per check.
     """
@@ -186,7 +186,6 @@ class DeferredChecks:
     def __init__(self, device=None, slots: int = 1):
         self.items = []
         self.slots = max(1, int(slots))
-        self._verdicts = []
         self.ring = None
         # (1,) int32 device flag: any hard failure since reset_sticky(); (1,) int64 replay
         # counter. Allocated before the capture (a tensor created inside it would be
@@ -195,43 +194,52 @@ class DeferredChecks:
         self.counter = torch.zeros(1, dtype=torch.int64, device=device) if device is not None else None
         self._ring = (torch.zeros(self.slots, self.MAX_ITEMS, 3, dtype=torch.int32, device=device)
                       if device is not None else None)
+        self._keep = []   # tensors the recorded verdict launches read (kept alive with the graph)
 
     def add(self, kind: str, args: tuple) -> None:
+        """Record a check; in a capture also its in-graph verdict (include/gpk.h::
+        gpk_record_check: one small kernel per check, the ring slot of this replay)."""
         self.items.append((kind, args))
-        if kind == "cholesky":
-            # fold this replay's hard failures (info > 0: NotPSD / NaN / timeout) into the
-            # sticky flag IN the graph, so failures of replays that are not checked
-            # individually (check_every > 1) are not lost
-            info = args[0]
-            if self.sticky is None:
+        if self.sticky is None:
+            if kind == "cholesky":
                 raise RuntimeError("DeferredChecks used in a capture without a device flag "
                                    "(construct it with device=...)")
-            self.sticky.copy_(torch.maximum(self.sticky, (info > 0).any().to(torch.int32).reshape(1)))
-            inputs = [t for t in args[4] if t is not None]
-            nan = torch.zeros((), dtype=torch.int32, device=info.device)
-            for t in inputs:
-                nan = nan | torch.isnan(t).any().to(torch.int32)
-            self._verdicts.append(torch.stack([info.max().to(torch.int32),
-                                               (-info).max().clamp_min(0).to(torch.int32), nan]))
+            return
+        if not self.sticky.is_cuda:   # host tensors (tests of the bookkeeping): torch ops
+            if kind == "cholesky":
+                self.sticky.copy_(torch.maximum(self.sticky, (args[0] > 0).any().to(torch.int32).reshape(1)))
+            return
+        item = len(self.items) - 1
+        if item >= self.MAX_ITEMS:
+            raise RuntimeError(f"more than {self.MAX_ITEMS} numerical checks recorded in one step")
+        t = args[0]
+        if kind == "cholesky":
+            info = t.reshape(-1)
+            ins = [x.detach().reshape(-1).float() for x in args[4] if x is not None][:2]
+            ins = [x if x.is_contiguous() else x.contiguous() for x in ins]
+            p = [(x.data_ptr(), x.numel()) for x in ins] + [(None, 0)] * (2 - len(ins))
+            rc = _native.lib().gpk_record_check(info.data_ptr(), info.numel(), p[0][0], p[0][1], p[1][0],
+                                                p[1][1], 0, self._ring.data_ptr(), self.counter.data_ptr(),
+                                                self.slots, item, self.MAX_ITEMS, self.sticky.data_ptr(),
+                                                _stream_ptr(info.device))
+            self._keep.append(ins)
         else:
-            flag = args[0]
-            z = torch.zeros((), dtype=torch.int32, device=flag.device)
-            self._verdicts.append(torch.stack([flag.reshape(-1)[0].to(torch.int32), z, z]))
+            flag = t.reshape(-1).to(torch.int32)
+            rc = _native.lib().gpk_record_check(flag.data_ptr(), 1, None, 0, None, 0, 1, self._ring.data_ptr(),
+                                                self.counter.data_ptr(), self.slots, item, self.MAX_ITEMS,
+                                                None, _stream_ptr(flag.device))
+            self._keep.append([flag])
+        _native.check(rc, "gpk_record_check")
 
     def finalize(self) -> None:
-        """Captured at the end of the step: this replay's verdicts -> ring slot."""
-        if not self._verdicts or self.counter is None:
+        """Captured at the end of the step: advance the replay counter (the ring slot)."""
+        if not self.items or self.counter is None or not self.counter.is_cuda:
             return
-        if len(self._verdicts) > self.MAX_ITEMS:
-            raise RuntimeError(f"more than {self.MAX_ITEMS} numerical checks recorded in one step")
-        v = torch.stack(self._verdicts)                                # (n_items, 3)
-        n = v.shape[0]
-        # masked write of slot (replay mod slots): no index kernels, the ring was allocated
-        # before the capture (outside the graph's private pool)
-        hit = (torch.arange(self.slots, device=v.device) == self.counter % self.slots).view(-1, 1, 1)
-        self._ring[:, :n].copy_(torch.where(hit, v.unsqueeze(0), self._ring[:, :n]))
-        self.counter.add_(1)
-        self.ring = self._ring[:, :n]
+        rc = _native.lib().gpk_record_check(None, 0, None, 0, None, 0, 2, None, self.counter.data_ptr(),
+                                            self.slots, 0, self.MAX_ITEMS, None,
+                                            _stream_ptr(self.counter.device))
+        _native.check(rc, "gpk_record_check")
+        self.ring = self._ring[:, :len(self.items)]
 
     def reset_sticky(self) -> None:
         if self.sticky is not None:
@@ -384,6 +392,24 @@ class VariationalOut:
     flags: Optional[torch.Tensor]  # (1,) int32: bit 0 = the variance clamp fired
 
 
+_CONST_PAIRS: dict = {}
+
+
+def _const_pair(a: float, b: float, device) -> torch.Tensor:
+    """Device tensor [a, b] for python-float hyper entries, cached per (device, a, b) so a
+    step packs its hyper vector with ONE cat kernel. Never cached while a HIP graph is being
+    captured (the tensor would live in the graph's private pool): GraphedStep's eager
+    warm-up steps populate the cache first."""
+    key = (str(torch.device(device)), float(a), float(b))
+    t = _CONST_PAIRS.get(key)
+    if t is not None:
+        return t
+    t = torch.stack([torch.full((), float(a), device=device), torch.full((), float(b), device=device)])
+    if not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+        _CONST_PAIRS[key] = t
+    return t
+
+
 def pack_variational_hyper(outputscale, noise, jitter, bias, weights, lengthscale, D, device):
     ls = _scalar_tensor(lengthscale, device)
     if ls.numel() == 1:
@@ -391,8 +417,11 @@ def pack_variational_hyper(outputscale, noise, jitter, bias, weights, lengthscal
     w = _scalar_tensor(weights, device).reshape(-1)
     if w.numel() != D:
         raise ValueError(f"LinearMean weights must have D={D} entries, got {w.numel()}")
-    return torch.cat([_scalar_tensor(outputscale, device)[:1], _scalar_tensor(noise, device)[:1],
-                      _scalar_tensor(jitter, device)[:1], _scalar_tensor(bias, device)[:1],
+    if not isinstance(noise, torch.Tensor) and not isinstance(jitter, torch.Tensor):
+        mid = _const_pair(noise, jitter, device)
+    else:
+        mid = torch.cat([_scalar_tensor(noise, device)[:1], _scalar_tensor(jitter, device)[:1]])
+    return torch.cat([_scalar_tensor(outputscale, device)[:1], mid, _scalar_tensor(bias, device)[:1],
                       w, ls]).contiguous()
 
 

@@ -111,9 +111,10 @@ int gpk_exact_posterior_f32(const float* X, const float* L, const float* z, cons
  *   Linv = L^{-1}
  * K_ZZ = s2 * exp(-0.5 ||(z_i - z_j)/l||^2) with ARD lengthscales (GPyTorch's centred
  * GEMM-form squared distance, diagonal not zeroed: Z requires grad in the reference).
- * Factor: ONE workgroup (fp64 MFMA rank-4 right-looking steps on register tiles, the
- * fp64 ladder restarted in-kernel); inverse: one workgroup per 16-column block column
- * (block forward substitution on fp64 MFMA), the block columns on different CUs.
+ * Factor: ONE workgroup (16 waves: 15 hold the upper triangle as fp64-MFMA register tiles,
+ * a diagonal wave factors each 16 x 16 diagonal block one step ahead; 16-column right-looking
+ * steps; the fp64 ladder restarted in-kernel); inverse: one workgroup per 16-column block
+ * column (block forward substitution on fp64 MFMA), the block columns on different CUs.
  *
  * Replaces (reference): the per-window (b-fold redundant) fp64 Cholesky that
  * VariationalStrategy._cholesky_factor runs for ToyDeepGPHiddenLayer
@@ -175,6 +176,22 @@ int gpk_gauss_ell_grad_f32(const float* y, const float* mean, const float* var, 
                            float* dnoise_part, void* stream);
 int gpk_meanfield_kl_f32(const float* m, const float* s, int M, float* kl, const float* gkl,
                          float* dm, float* ds, void* stream);
+
+/*
+ * Condensed verdict of one host-side numerical check inside a captured HIP graph
+ * (graphs.GraphedStep): kind 0 = a psd_safe_cholesky info vector (n entries; in0 / in1 =
+ * the factorised inputs, scanned for NaN only when a factorisation failed), kind 1 = the
+ * variance-clamp flag word, kind 2 = end of the step (advance the replay counter).
+ *   ring[(counter % slots) * items + item] = {max info, max(-info, 0), NaN in the inputs}
+ *   sticky |= (max info > 0)
+ * so the host reads the verdicts of a block of replays with one copy and warns / raises
+ * per replay exactly as GPyTorch's eager psd_safe_cholesky / MultivariateNormal.variance
+ * checks (linear_operator utils/cholesky.py).
+ * ring : (slots, items, 3) int device;  counter : (1,) int64 device;  sticky : (1,) int device
+ */
+int gpk_record_check(const int* info, int n, const float* in0, long long n0, const float* in1,
+                     long long n1, int kind, int* ring, long long* counter, int slots, int item,
+                     int items, int* sticky, void* stream);
 
 /*
  * Batched variational predictive distribution and expected log likelihood:
