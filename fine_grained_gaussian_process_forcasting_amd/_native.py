@@ -47,6 +47,13 @@ SIGNATURES = {
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gpk_meanfield_kl_f32": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
+    "gpk_variational_elbo_f32": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p, c_void_p,
+                                         c_void_p, c_int, c_int, c_int, ctypes.c_float, ctypes.c_float,
+                                         c_void_p, c_void_p, c_void_p]),
+    "gpk_variational_elbo_grad_f32": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p,
+                                              c_void_p, c_void_p, c_int, c_int, c_int, ctypes.c_float,
+                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p]),
     "gpk_record_check": (c_int, [c_void_p, c_int, c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong,
                                  c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "gpk_variational_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

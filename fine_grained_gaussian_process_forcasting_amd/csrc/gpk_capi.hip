@@ -162,6 +162,52 @@ int gpk_meanfield_kl_f32(const float* m, const float* s, int M, float* kl, const
   return gpk_launch_kl(m, s, M, kl, gkl, dm, ds, (hipStream_t)stream);
 }
 
+int gpk_variational_elbo_f32(const float* y, long long ldy, const float* mean, long long ldm,
+                             const float* var, long long ldv, const float* noise, const float* m,
+                             const float* s, int M, int R, int N, float kl_scale, float min_var,
+                             float* elbo, int* clamp_flag, void* stream) {
+  if (y == nullptr) return -1;
+  if (ldy < N) return -2;
+  if (mean == nullptr) return -3;
+  if (ldm < N) return -4;
+  if (var == nullptr) return -5;
+  if (ldv < N) return -6;
+  if (noise == nullptr) return -7;
+  if (m == nullptr) return -8;
+  if (s == nullptr) return -9;
+  if (M < 1) return -10;
+  if (R < 0) return -11;
+  if (N < 1) return -12;
+  if (elbo == nullptr) return -15;
+  if (R == 0) return 0;
+  return gpk_launch_elbo(y, ldy, mean, ldm, var, ldv, noise, m, s, M, R, N, kl_scale, min_var, elbo,
+                         clamp_flag, (hipStream_t)stream);
+}
+
+int gpk_variational_elbo_grad_f32(const float* y, long long ldy, const float* mean, long long ldm,
+                                  const float* var, long long ldv, const float* noise, const float* m,
+                                  const float* s, int M, int R, int N, float kl_scale, const float* gelbo,
+                                  float* dmean, float* dvar, float* dnoise_part, float* dm, float* ds,
+                                  void* stream) {
+  if (y == nullptr) return -1;
+  if (ldy < N) return -2;
+  if (mean == nullptr) return -3;
+  if (ldm < N) return -4;
+  if (var == nullptr) return -5;
+  if (ldv < N) return -6;
+  if (noise == nullptr) return -7;
+  if (m == nullptr) return -8;
+  if (s == nullptr) return -9;
+  if (M < 1) return -10;
+  if (R < 1) return -11;
+  if (N < 1) return -12;
+  if (gelbo == nullptr) return -14;
+  if (dmean == nullptr || dvar == nullptr || dnoise_part == nullptr || dm == nullptr || ds == nullptr)
+    return -15;
+  return gpk_launch_elbo_grad(y, ldy, mean, ldm, var, ldv, noise, m, s, M, R, N, kl_scale, gelbo, dmean,
+                              dvar, dnoise_part, dm, ds, (hipStream_t)stream);
+}
+
 int gpk_record_check(const int* info, int n, const float* in0, long long n0, const float* in1,
                      long long n1, int kind, int* ring, long long* counter, int slots, int item,
                      int items, int* sticky, void* stream) {

@@ -190,3 +190,111 @@ int gpk_launch_verdict(const int* info, int n, const float* in0, long long n0, c
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
+
+// ---------------------------------------------------------------------------
+// The whole per-row ELBO of VariationalELBO (combine_terms, one mean-field layer) in ONE
+// launch each way (forecast_denoising.py:86-89 through DeepApproximateMLL):
+//   elbo_r = ell_r / N - kl_scale * KL(q(u) || N(0, I)),  kl_scale = beta / num_data
+// y / mean / var rows may be strided (a point slice of a joint GP output: no copies); the
+// variance-clamp flag of the rows (any var <= min_var: the kernel-clamped entries) is
+// produced on the way (MultivariateNormal.variance's warning).
+// ---------------------------------------------------------------------------
+namespace {
+GPK_DEVICE float block_sum_all(float v, float* red) {   // result valid in every thread
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float s = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return s;
+}
+
+GPK_DEVICE float kl_meanfield(const float* m, const float* s, int M, float* red) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < M; i += 256) {
+    const float s2 = s[i] * s[i];
+    acc += s2 + m[i] * m[i] - 1.f - __logf(s2);
+  }
+  return 0.5f * block_sum_all(acc, red);
+}
+
+__global__ void __launch_bounds__(256)
+gpk_elbo_kernel(const float* __restrict__ y, long long ldy, const float* __restrict__ mean, long long ldm,
+                const float* __restrict__ var, long long ldv, const float* __restrict__ noise,
+                const float* __restrict__ m, const float* __restrict__ s, int M, int N, float kl_scale,
+                float min_var, float* __restrict__ elbo, int* __restrict__ clamp_flag) {
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  const float nz = noise[0], inv = 1.f / nz, cst = __logf(nz) + kLog2Pi;
+  float acc = 0.f;
+  int clamped = 0;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const float d = y[r * ldy + i] - mean[r * ldm + i];
+    const float v = var[r * ldv + i];
+    acc += (d * d + v) * inv + cst;
+    clamped |= v <= min_var;
+  }
+  const float ell = -0.5f * block_sum_all(acc, red);
+  const float kl = kl_meanfield(m, s, M, red);
+  if (threadIdx.x == 0) elbo[r] = ell / (float)N - kl_scale * kl;
+  if (clamp_flag != nullptr && __any(clamped) && (threadIdx.x & 63) == 0)
+    (void)__hip_atomic_fetch_or(clamp_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// backward for the objective sum_r g_r elbo_r: dmean, dvar (R, N, contiguous), per-row
+// d/dnoise partials, and (workgroup 0) dm, ds of the KL term
+__global__ void __launch_bounds__(256)
+gpk_elbo_grad_kernel(const float* __restrict__ y, long long ldy, const float* __restrict__ mean, long long ldm,
+                     const float* __restrict__ var, long long ldv, const float* __restrict__ noise,
+                     const float* __restrict__ m, const float* __restrict__ s, int M, int R, int N,
+                     float kl_scale, const float* __restrict__ g, float* __restrict__ dmean,
+                     float* __restrict__ dvar, float* __restrict__ dnoise_part, float* __restrict__ dm,
+                     float* __restrict__ ds) {
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  const float nz = noise[0], inv = 1.f / nz;
+  const float gr = g[r] / (float)N;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const float d = y[r * ldy + i] - mean[r * ldm + i];
+    const float q = d * d + var[r * ldv + i];
+    dmean[(size_t)r * N + i] = gr * d * inv;
+    dvar[(size_t)r * N + i] = -0.5f * gr * inv;
+    acc += q * inv * inv - inv;
+  }
+  const float sq = block_sum_all(acc, red);
+  if (threadIdx.x == 0) dnoise_part[r] = 0.5f * gr * sq;
+  if (r == 0) {   // d/d{m, s} of -kl_scale * KL * sum_r g_r
+    float gs = 0.f;
+    for (int i = threadIdx.x; i < R; i += 256) gs += g[i];
+    const float gk = -kl_scale * block_sum_all(gs, red);
+    for (int i = threadIdx.x; i < M; i += 256) {
+      dm[i] = gk * m[i];
+      ds[i] = gk * (s[i] - 1.f / s[i]);
+    }
+  }
+}
+}  // namespace
+
+int gpk_launch_elbo(const float* y, long long ldy, const float* mean, long long ldm, const float* var,
+                    long long ldv, const float* noise, const float* m, const float* s, int M, int R, int N,
+                    float kl_scale, float min_var, float* elbo, int* clamp_flag, hipStream_t stream) {
+  if (clamp_flag != nullptr) {
+    const hipError_t e = hipMemsetAsync(clamp_flag, 0, sizeof(int), stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(gpk_elbo_kernel, dim3(R), dim3(256), 0, stream, y, ldy, mean, ldm, var, ldv, noise, m,
+                     s, M, N, kl_scale, min_var, elbo, clamp_flag);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int gpk_launch_elbo_grad(const float* y, long long ldy, const float* mean, long long ldm, const float* var,
+                         long long ldv, const float* noise, const float* m, const float* s, int M, int R,
+                         int N, float kl_scale, const float* g, float* dmean, float* dvar, float* dnoise_part,
+                         float* dm, float* ds, hipStream_t stream) {
+  hipLaunchKernelGGL(gpk_elbo_grad_kernel, dim3(R), dim3(256), 0, stream, y, ldy, mean, ldm, var, ldv, noise,
+                     m, s, M, R, N, kl_scale, g, dmean, dvar, dnoise_part, dm, ds);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}

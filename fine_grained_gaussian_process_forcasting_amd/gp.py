@@ -444,6 +444,43 @@ class _ApproximateMarginalLogLikelihood(nn.Module):
 
 
 class VariationalELBO(_ApproximateMarginalLogLikelihood):
+    def forward(self, approximate_dist_f: MultivariateNormal, target: torch.Tensor, **kwargs):
+        fused = self._fused(approximate_dist_f, target)
+        return fused if fused is not None else super().forward(approximate_dist_f, target, **kwargs)
+
+    def _fused(self, dist, target):
+        """ELL / N - KL / (num_data / beta) for every row in ONE launch each way
+        (gpk::variational_elbo) when the terms are the hot path's: a Gaussian likelihood, a
+        variational output of the kernels, one unbatched mean-field strategy. Same warnings as
+        the unfused expression (the variance clamp flag)."""
+        if not self.combine_terms or not isinstance(self.likelihood, GaussianLikelihood):
+            return None
+        mean, var = dist._mean, dist._variance
+        if (var is None or dist._exact is not None or dist._added_noise is not None or not mean.is_cuda
+                or mean.dtype != torch.float32 or var.shape != mean.shape
+                or (dist._clamp_flag is None and not dist._preclamped)):
+            return None
+        strategies = [m for m in self.model.modules() if isinstance(m, VariationalStrategy)]
+        if len(strategies) != 1:
+            return None
+        q = strategies[0].variational_distribution
+        if not isinstance(q, MeanFieldVariationalDistribution) or q.variational_mean.dim() != 1:
+            return None
+        shape = mean.shape
+        N = shape[-1]
+        y = torch.broadcast_to(target, shape).to(torch.float32)
+        min_var = settings.min_variance.value(var.dtype)
+        elbo, flag = torch.ops.gpk.variational_elbo(
+            y.reshape(-1, N), mean.reshape(-1, N), var.reshape(-1, N), self.likelihood.noise.reshape(1),
+            q.variational_mean, q._variational_stddev, float(self.beta) / float(self.num_data), float(min_var))
+        # MultivariateNormal.variance's clamp warning: the variational kernel's own flag when the
+        # distribution carries it, else the rows' flag computed with the ELBO
+        from .ops import record_or_run
+        f = dist._clamp_flag if dist._clamp_flag is not None else (flag if dist._preclamped else None)
+        if f is not None:
+            record_or_run("clamp", (f, min_var), lambda: warn_if_clamped(f, min_var))
+        return elbo.reshape(shape[:-1])
+
     def _log_likelihood_term(self, variational_dist_f, target, **kwargs):
         if hasattr(self.likelihood, "expected_log_prob_sum"):
             return self.likelihood.expected_log_prob_sum(target, variational_dist_f)

@@ -15,6 +15,8 @@ instead of being opaque Python. Each op is one C-ABI call of include/gpk.h on
   gpk::variational_adj(x, Linv, Z, vmean, vstd, hyper, gmean, gvar) -> (dX, dLinv, dZ, dpar)
   gpk::gauss_ell(y, mean, var, noise) -> ell (R,)                             [autograd]
   gpk::meanfield_kl(m, s) -> kl (1,)                                          [autograd]
+  gpk::variational_elbo(y, mean, var, noise, m, s, kl_scale, min_var) -> (elbo (R,), flag)
+                                                                               [autograd]
 
 Reference call sites they serve: GPModel.py:10-13 + ExactMarginalLogLikelihood
 (exact_mll), ExactGPModel in eval mode (exact_posterior), DeepGP.py:33-73 VariationalStrategy (kzz_factor, variational_fwd),
@@ -282,3 +284,48 @@ def _kl_backward(ctx, gkl):
 
 
 meanfield_kl.register_autograd(_kl_backward, setup_context=_kl_setup)
+
+
+@torch.library.custom_op("gpk::variational_elbo", mutates_args=(), device_types="cuda")
+def variational_elbo(y: Tensor, mean: Tensor, var: Tensor, noise: Tensor, vmean: Tensor, vstd: Tensor,
+                     kl_scale: float, min_var: float) -> Tuple[Tensor, Tensor]:
+    """(R,) per-row ELBO ell_r / N - kl_scale KL(q(u)) and the variance-clamp flag (1,)."""
+    return ops.variational_elbo(y, mean, var, noise.reshape(1).contiguous().float(), vmean, vstd, kl_scale,
+                                min_var)
+
+
+@variational_elbo.register_fake
+def _(y, mean, var, noise, vmean, vstd, kl_scale, min_var):
+    return mean.new_empty(mean.shape[0]), mean.new_empty(1, dtype=torch.int32)
+
+
+@torch.library.custom_op("gpk::variational_elbo_grad", mutates_args=(), device_types="cuda")
+def variational_elbo_grad(y: Tensor, mean: Tensor, var: Tensor, noise: Tensor, vmean: Tensor, vstd: Tensor,
+                          kl_scale: float, gelbo: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    return ops.variational_elbo_grad(y, mean, var, noise.reshape(1).contiguous().float(), vmean, vstd,
+                                     kl_scale, gelbo)
+
+
+@variational_elbo_grad.register_fake
+def _(y, mean, var, noise, vmean, vstd, kl_scale, gelbo):
+    R, N = mean.shape
+    return (mean.new_empty(R, N), mean.new_empty(R, N), mean.new_empty(1), torch.empty_like(vmean),
+            torch.empty_like(vstd))
+
+
+def _elbo_setup(ctx, inputs, output):
+    y, mean, var, noise, vmean, vstd, kl_scale, min_var = inputs
+    ctx.kl_scale = kl_scale
+    ctx.save_for_backward(y, mean, var, noise, vmean, vstd)
+    ctx.mark_non_differentiable(output[1])
+
+
+def _elbo_backward(ctx, gelbo, _gflag):
+    y, mean, var, noise, vmean, vstd = ctx.saved_tensors
+    dmean, dvar, dnoise, dm, ds = torch.ops.gpk.variational_elbo_grad(y, mean, var, noise, vmean, vstd,
+                                                                      ctx.kl_scale, gelbo.contiguous())
+    return (None, dmean, dvar, dnoise.reshape(noise.shape), dm.reshape(vmean.shape), ds.reshape(vstd.shape),
+            None, None)
+
+
+variational_elbo.register_autograd(_elbo_backward, setup_context=_elbo_setup)

@@ -589,3 +589,54 @@ def meanfield_kl_grad(m, s, gkl):
                                             dm.data_ptr(), ds.data_ptr(), _stream_ptr(m.device))
     _native.check(rc, "gpk_meanfield_kl_f32")
     return dm, ds
+
+
+def _rows(t: torch.Tensor):
+    """(tensor, leading dimension) of a (R, N) float32 view with unit column stride."""
+    if t.dim() != 2 or t.stride(1) != 1 or t.dtype != torch.float32:
+        t = t.contiguous().float()
+    return t, (t.stride(0) if t.shape[0] > 1 else t.shape[1])
+
+
+def variational_elbo(y, mean, var, noise, vmean, vstd, kl_scale: float, min_var: float):
+    """(elbo (R,), clamp flag (1,) int32) of include/gpk.h::gpk_variational_elbo_f32."""
+    _require_device(y, mean, var, noise, vmean, vstd)
+    R, N = mean.shape
+    y, ldy = _rows(y)
+    mean, ldm = _rows(mean)
+    var, ldv = _rows(var)
+    dev = mean.device
+    elbo = torch.empty(R, device=dev, dtype=torch.float32)
+    flag = torch.empty(1, device=dev, dtype=torch.int32)
+    m = vmean.detach().reshape(-1).contiguous().float()
+    s = vstd.detach().reshape(-1).contiguous().float()
+    rc = _native.lib().gpk_variational_elbo_f32(y.data_ptr(), ldy, mean.data_ptr(), ldm, var.data_ptr(), ldv,
+                                                noise.data_ptr(), m.data_ptr(), s.data_ptr(), m.numel(), R, N,
+                                                float(kl_scale), float(min_var), elbo.data_ptr(), flag.data_ptr(),
+                                                _stream_ptr(dev))
+    _native.check(rc, "gpk_variational_elbo_f32")
+    return elbo, flag
+
+
+def variational_elbo_grad(y, mean, var, noise, vmean, vstd, kl_scale: float, gelbo):
+    """(dmean, dvar, dnoise (1,), dvmean, dvstd) for the objective sum_r gelbo_r elbo_r."""
+    R, N = mean.shape
+    y, ldy = _rows(y)
+    mean, ldm = _rows(mean)
+    var, ldv = _rows(var)
+    dev = mean.device
+    m = vmean.detach().reshape(-1).contiguous().float()
+    s = vstd.detach().reshape(-1).contiguous().float()
+    dmean = torch.empty(R, N, device=dev, dtype=torch.float32)
+    dvar = torch.empty(R, N, device=dev, dtype=torch.float32)
+    part = torch.empty(R, device=dev, dtype=torch.float32)
+    dm = torch.empty_like(m)
+    ds = torch.empty_like(s)
+    g = gelbo.reshape(-1).contiguous().float()
+    rc = _native.lib().gpk_variational_elbo_grad_f32(y.data_ptr(), ldy, mean.data_ptr(), ldm, var.data_ptr(),
+                                                     ldv, noise.data_ptr(), m.data_ptr(), s.data_ptr(), m.numel(),
+                                                     R, N, float(kl_scale), g.data_ptr(), dmean.data_ptr(),
+                                                     dvar.data_ptr(), part.data_ptr(), dm.data_ptr(),
+                                                     ds.data_ptr(), _stream_ptr(dev))
+    _native.check(rc, "gpk_variational_elbo_grad_f32")
+    return dmean, dvar, part.sum().reshape(1), dm, ds

@@ -178,6 +178,31 @@ int gpk_meanfield_kl_f32(const float* m, const float* s, int M, float* kl, const
                          float* dm, float* ds, void* stream);
 
 /*
+ * The per-row ELBO of VariationalELBO (combine_terms, one whitened mean-field layer) in one
+ * launch each way:
+ *   elbo_r = ell_r / N - kl_scale * KL(N(m, diag s^2) || N(0, I)),  kl_scale = beta / num_data
+ *   ell_r  = sum_i -0.5 [((y_ri - mean_ri)^2 + var_ri) / noise + log noise + log 2 pi]
+ * Rows r of y / mean / var start at r * ld (ld >= N: a point slice of a joint output needs no
+ * copy). clamp_flag (or NULL): set to 1 if any var_ri <= min_var (the kernel-clamped entries:
+ * MultivariateNormal.variance's NumericalWarning). The backward (objective sum_r g_r elbo_r)
+ * writes dmean, dvar (R, N contiguous), per-row d/dnoise partials and dm, ds (M).
+ *
+ * Replaces (reference): DeepApproximateMLL(VariationalELBO(likelihood, model, num_data=d))
+ * at forecast_denoising.py:86-89 (upstream mlls/variational_elbo.py +
+ * _approximate_mll.py: expected_log_prob(...).sum(-1).div(N) - kl.div(num_data / beta))
+ * and its autograd backward (train.py:166); SURVEY.md §8a row a14.
+ */
+int gpk_variational_elbo_f32(const float* y, long long ldy, const float* mean, long long ldm,
+                             const float* var, long long ldv, const float* noise, const float* m,
+                             const float* s, int M, int R, int N, float kl_scale, float min_var,
+                             float* elbo, int* clamp_flag, void* stream);
+int gpk_variational_elbo_grad_f32(const float* y, long long ldy, const float* mean, long long ldm,
+                                  const float* var, long long ldv, const float* noise, const float* m,
+                                  const float* s, int M, int R, int N, float kl_scale, const float* gelbo,
+                                  float* dmean, float* dvar, float* dnoise_part, float* dm, float* ds,
+                                  void* stream);
+
+/*
  * Condensed verdict of one host-side numerical check inside a captured HIP graph
  * (graphs.GraphedStep): kind 0 = a psd_safe_cholesky info vector (n entries; in0 / in1 =
  * the factorised inputs, scanned for NaN only when a factorisation failed), kind 1 = the

@@ -68,6 +68,7 @@ def test_elbo_ops_opcheck(cuda_device):
     m = torch.randn(12, device=dev, requires_grad=True)
     s = (0.5 + torch.rand(12, device=dev)).requires_grad_(True)
     torch.library.opcheck(torch.ops.gpk.meanfield_kl, (m, s))
+    torch.library.opcheck(torch.ops.gpk.variational_elbo, (y, mean, var, noise, m, s, 0.1, 1e-6))
 
 
 def test_variational_elbo_uses_fused_terms_and_matches_torch(cuda_device):
@@ -92,3 +93,46 @@ def test_variational_elbo_uses_fused_terms_and_matches_torch(cuda_device):
         kl = 0.5 * (s2.sum() + q.variational_mean.pow(2).sum() - s2.numel() - s2.log().sum())
         ref = (ll - kl / 16).mean(0)
     assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6), (got, ref)
+
+
+@pytest.mark.parametrize("sliced", [False, True])
+def test_fused_elbo_value_and_grads_vs_unfused(cuda_device, sliced):
+    """gpk::variational_elbo (VariationalELBO's fused path) against the unfused GPyTorch-form
+    expression (expected_log_prob(...).sum(-1) / N - KL / num_data), value and every
+    gradient (mean / var of the GP, noise, q(u)); ``sliced``: the dec point slice of a joint
+    enc + dec output (strided rows, no copy), as denoise_model_2 produces it."""
+    from fine_grained_gaussian_process_forcasting_amd import settings
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.DeepGP import DeepGPp
+    from fine_grained_gaussian_process_forcasting_amd.gp import VariationalELBO
+    from fine_grained_gaussian_process_forcasting_amd.mlls import DeepApproximateMLL
+    dev = cuda_device
+    torch.manual_seed(3)
+    model = DeepGPp(16, 77).to(dev)
+    x = torch.randn(6, 50, 16, device=dev) / 4
+    y = torch.randn(1, 6, 30 if sliced else 50, device=dev)
+    params = [p for p in model.parameters() if p.requires_grad]
+
+    def run(fused):
+        with settings.num_likelihood_samples(1):
+            _, dist = model.predict(x)
+            if sliced:
+                dist = dist.slice_points(20, None)
+            mll = DeepApproximateMLL(VariationalELBO(model.likelihood, model, 16))
+            if fused:
+                out = mll(dist, y)
+            else:
+                base = mll.base_mll
+                ll = base.likelihood.expected_log_prob(y, dist).sum(-1).div(dist.event_shape[0])
+                out = (ll - base.model.variational_strategy.kl_divergence().div(base.num_data)).mean(0)
+        gr = torch.autograd.grad(out.sum(), params, allow_unused=True)
+        return out.detach(), gr
+
+    a, ga = run(True)
+    b, gb = run(False)
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a, b)
+    for p, u, v in zip(params, ga, gb):
+        if v is None:
+            assert u is None or float(u.abs().max()) == 0.0
+            continue
+        assert u is not None
+        assert torch.allclose(u, v, rtol=1e-4, atol=1e-6), (p.shape, float((u - v).abs().max()))
