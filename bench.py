@@ -98,6 +98,47 @@ def time_launches(fn, n):
     return e0.elapsed_time(e1) / n, out
 
 
+def time_graph(fn, n, warm=3):
+    """GPU time of ONE call of ``fn``: n calls captured into one HIP graph, replayed once
+    untimed (the first replay of a fresh graph exec uploads it), then one timed replay
+    between HIP events, / n. No host work sits between the launches, so this is what the
+    kernels take back to back -- the way a captured training step (graphs.GraphedStep) runs
+    them. Side legs only; the headline loop is eager."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(warm):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            out = fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n, out
+
+
+def time_side(fn, n):
+    """(graph ms, eager ms, result) of a side-leg op: graph replay (time_graph) and n eager
+    back-to-back calls after 3 warm-up calls (time_launches; includes host launch work)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    eager, out = time_launches(fn, n)
+    try:
+        graph, out = time_graph(fn, n)
+    except Exception:   # capture not possible here: report the eager time only
+        graph = None
+    return graph, eager, out
+
+
 def cpu_exact_baseline(N, D, seconds, threads):
     """GPyTorch's own CPU arithmetic for this path (oracle.exact_mll_torch_cpu: the
     _sq_dist GEMM, torch.linalg.cholesky_ex + jitter ladder, cholesky_solve, logdet;
@@ -192,11 +233,16 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed, label="BASELINE
     for _ in range(warmup):
         kz, out, adj = step()
     torch.cuda.synchronize()
-    # each phase in its own back-to-back loop (same inputs as the step's)
-    ms = {"kzz": time_launches(lambda: ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h), steps)[0],
-          "fwd": time_launches(lambda: ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper,
-                                                               want_flags=False), steps)[0],
-          "bwd": time_launches(lambda: ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv), steps)[0]}
+    # each phase in its own back-to-back loop (same inputs as the step's): GPU time from a
+    # graph replay (time_graph), the eager loop beside it
+    phases = {"kzz": lambda: ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h),
+              "fwd": lambda: ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False),
+              "bwd": lambda: ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv)}
+    ms, eager = {}, {}
+    for k, fn in phases.items():
+        gms, ems, _ = time_side(fn, steps)
+        ms[k] = gms if gms is not None else ems
+        eager[k] = ems
     if world > 1:
         t = torch.tensor([ms["kzz"], ms["fwd"], ms["bwd"]], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -213,6 +259,9 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed, label="BASELINE
         "windows_per_s_train_step": B * world / ((ms["kzz"] + ms["fwd"] + ms["bwd"]) * 1e-3),
         "kernel_ms": {"gpk_kzz_chol_f64": ms["kzz"], "gpk_variational_f32": ms["fwd"],
                       "gpk_variational_adjoint_f32": ms["bwd"]},
+        "eager_ms": {"gpk_kzz_chol_f64": eager["kzz"], "gpk_variational_f32": eager["fwd"],
+                     "gpk_variational_adjoint_f32": eager["bwd"],
+                     "note": "eager back-to-back calls incl. host launch work; kernel_ms = graph replay"},
         "roofline": {"kernel": "gpk_var_fwd_r_kernel" if (M <= 64 and D <= 32) else "gpk_var_fwd_l_kernel",
                      "bound": "mfma",
                      "achieved": achieved / 1e12, "peak": (f32 + f64) / roof_s / 1e12,
@@ -355,12 +404,11 @@ def main():
     cfg2 = None
     if rank == 0 and not args.no_cfg2:
         X2, y2 = make_inputs(128, 128, D, dev, seed=11)
-        for _ in range(3):
-            ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper)
-        ms2, o2 = time_launches(lambda: ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper), 20)
+        g2, e2, o2 = time_side(lambda: ops.exact_mll(X2, y2, None, None, None, None, hyper=hyper), 20)
+        ms2 = g2 if g2 is not None else e2
         b2, f2 = bytes_per_window(128, D), flops_per_window(128, D)
         cfg2 = {"workload": "exact-GP windows B=128 N=128 D=32 (BASELINE configs[1]), L written",
-                "kernel_ms": ms2, "windows_per_s": 128 / (ms2 * 1e-3),
+                "kernel_ms": ms2, "eager_ms": e2, "windows_per_s": 128 / (ms2 * 1e-3),
                 "hbm_frac": b2 * 128 / (ms2 * 1e-3) / HBM_PEAK,
                 "fp32_frac": f2 * 128 / (ms2 * 1e-3) / FP32_PEAK,
                 "note": "128 windows occupy half of the 256 CUs: latency-bound by one window's chain"}
@@ -378,34 +426,31 @@ def main():
             Xs_, ys_ = X[:Bs].contiguous(), y[:Bs].contiguous()
             Ls_ = torch.empty(Bs, N, N, device=dev)
             f = lambda: ops.exact_mll(Xs_, ys_, None, None, None, None, hyper=hyper, L_out=Ls_)  # noqa: E731
-            for _ in range(3):
-                f()
-            msG, _ = time_launches(f, 20)
-            strong_share[f"G{G}"] = {"windows_per_rank": Bs, "kernel_ms": msG,
+            gG, eG, _ = time_side(f, 20)
+            msG = eG   # eager, like the headline loop it is compared with
+            strong_share[f"G{G}"] = {"windows_per_rank": Bs, "kernel_ms": msG, "graph_ms": gG,
                                      "implied_speedup": kern_ms / msG if B == 512 else None}
 
-    grad_ms = post_ms = None
+    grad_ms = post_ms = grad_eager = post_eager = None
     if not args.no_grad:
         fw = ops.exact_mll(X, y, None, None, None, None, hyper=hyper, want_L=True, want_z=True)
         gout = torch.ones(B, device=dev)
-        ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout)
-        torch.cuda.synchronize()
-        grad_ms = time_launches(lambda: ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout), 5)[0]
+        gg, grad_eager, _ = time_side(lambda: ops.exact_mll_grad(X, fw.L, fw.z, hyper, gout), 10)
+        grad_ms = gg if gg is not None else grad_eager
         # eval-mode posterior at Ns = N new points per window from the same factor
         Xs = make_inputs(B, N, D, dev, seed=77 + rank)[0]
-        ops.exact_posterior(X, fw.L, fw.z, hyper, Xs)
-        torch.cuda.synchronize()
-        post_ms = time_launches(lambda: ops.exact_posterior(X, fw.L, fw.z, hyper, Xs), 5)[0]
+        gp_, post_eager, _ = time_side(lambda: ops.exact_posterior(X, fw.L, fw.z, hyper, Xs), 10)
+        post_ms = gp_ if gp_ is not None else post_eager
 
     var = None
     if not args.no_var:
-        var = variational_leg(dev, args.var_B, args.var_N, args.var_M, D, max(5, args.steps // 5),
+        var = variational_leg(dev, args.var_B, args.var_N, args.var_M, D, max(20, args.steps // 2),
                               3, world, seed=7 + rank)
 
     # the cfg-3 GP shape the reference trains (DeepGP default M=256; enc N=192, dec N=96, b=256)
     var3 = None
     if rank == 0 and not args.no_var3:
-        var3 = {f"N{n}": variational_leg(dev, 256, n, 256, D, 10, 3, 1, seed=13 + n,
+        var3 = {f"N{n}": variational_leg(dev, 256, n, 256, D, 20, 3, 1, seed=13 + n,
                                          label=f"cfg-3 GP shape, {'enc' if n == 192 else 'dec'}")
                 for n in (192, 96)}
 
@@ -441,13 +486,13 @@ def main():
             "mean_mll": mean_mll,
         }
         if grad_ms is not None:
-            line["backward"] = {"kernel": "gpk_exact_mll_grad_f32", "kernel_ms": grad_ms,
+            line["backward"] = {"kernel": "gpk_exact_mll_grad_f32", "kernel_ms": grad_ms, "eager_ms": grad_eager,
                                 "windows_per_s_per_gpu": B / (grad_ms * 1e-3),
                                 "note": "analytic dX/dy/dhyper of the same windows; not the headline"}
         if post_ms is not None:
             pb = 4 * (2 * N * D + N * (N + 1) // 2 + N + 2 * N)     # X, Xs, lower L, z; mean + var
             pf = 2 * N * N * D + N * N * N + 2 * N * N + 10 * N * N  # Gram, TRSM, mean/var, RBF
-            line["posterior"] = {"kernel": "gpk_exact_posterior_f32", "kernel_ms": post_ms,
+            line["posterior"] = {"kernel": "gpk_exact_posterior_f32", "kernel_ms": post_ms, "eager_ms": post_eager,
                                  "test_points_per_window": N,
                                  "windows_per_s_per_gpu": B / (post_ms * 1e-3),
                                  "hbm_frac": pb * B / (post_ms * 1e-3) / HBM_PEAK,
