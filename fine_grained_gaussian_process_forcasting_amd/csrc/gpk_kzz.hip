@@ -6,24 +6,26 @@
 // variational_strategy.py); the reference runs it b times per GP call (Z expanded over the
 // batch). oracle/gp_oracle.py::kzz_factor restates it.
 //
-// gpk_kzz16_kernel<NS>: ONE workgroup of 8 waves; the UPPER triangle of K_ZZ (padded to
+// gpk_kzz16_kernel<NS>: ONE workgroup of 16 waves; the UPPER triangle of K_ZZ (padded to
 // T 16-blocks, identity padding) is held as 16 x 16 fp64 tiles in v_mfma_f64_16x16x4f64
 // accumulators (acc layout: lane (c, g), reg r <-> row g + 4r, column c) for the whole
-// factorisation, wave w owning block columns w and T - 1 - w (T + 1 tiles). Blocked
-// right-looking Cholesky of R = L^T in 16-column steps (T steps instead of the 4-column
-// kernel's 4T):
-//   diag   the owner wave of column k factors T'_kk in ONE readlane-broadcast sweep of the
-//          augmented [T_kk | I] (lanes 0-15: columns of T_kk -> rows of L_kk, lanes 16-31:
-//          identity columns -> columns of L_kk^{-1}) -- LOOK-AHEAD: during step k - 1's
-//          update, right after its own T'_kk is updated, while the other waves update;
+// factorisation by 15 WORKER waves (tiles dealt round-robin in column-major order, NS per
+// wave); wave 15 is the DIAGONAL wave and holds no tile. Blocked right-looking Cholesky of
+// R = L^T in 16-column steps:
+//   diag   the diagonal wave factors T'_kk in ONE sweep of the augmented [T_kk | I] (lanes
+//          0-15: columns of T_kk -> rows of L_kk, lanes 16-31: identity columns -> columns of
+//          L_kk^{-1}), broadcasts by 64-bit DPP (diag_col64) -- LOOK-AHEAD: the owner of
+//          (k+1, k+1) updates and hands it over (LDS + flag) first in step k's update, so the
+//          sweep overlaps the workers' trailing update;
 //   TRSM   owners of block row k: R_kj = L_kk^{-1} T'_kj (4 f64 MFMAs, the register tile is
 //          the B operand) -> LDS panel + L's block (j, k);
 //   update every tile (i, j), k < i <= j: T'_ij -= R_ki^T R_kj (4 f64 MFMAs, both operands
 //          read from the LDS panel in acc layout: conflict-free; R_kj once per column).
 // Two workgroup barriers per step. GPyTorch's fp64 ladder restarts in-kernel (info = -t).
-// gpk_kzz_inv_kernel: L^{-1}, one workgroup per 16-column block column (block forward
-// substitution on fp64 MFMA; the diagonal-block inverses come from the factor kernel, which
-// forms each L_kk^{-1} anyway), the block columns on different CUs.
+// gpk_kzz_inv_kernel: L^{-1}, one workgroup of 16 waves per 16-column block column (block
+// forward substitution on fp64 MFMA, one S tile per wave; the diagonal-block inverses come
+// from the factor kernel, which forms each L_kk^{-1} anyway), the block columns on
+// different CUs.
 #include "gpk_common.h"
 #include "gpk_internal.h"
 #include "gpk_kzz.h"
@@ -68,6 +70,55 @@ constexpr int KT = 64 * KW;
 __host__ __device__ inline int kzz_zstride(int D) { return ((D + 15) & ~15) + 4; }
 constexpr int kLinvStride = 17;   // L_kk^{-1} rows in LDS (odd: conflict-free column reads)
 
+#ifndef GPK_KZZ_DPP
+#define GPK_KZZ_DPP 1   // 1: the diagonal sweep broadcasts by 64-bit DPP (row_newbcast); 0: readlanes
+#endif
+
+// x of lane 16 r' + i for every lane of row r' (64-bit row_newbcast:i)
+template <int I>
+GPK_DEVICE double nbc(double x) {
+  return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + I, 0xf, 0xf, false);
+}
+// row 0's value in rows 0 and 1 (and row 2's in rows 2 and 3): permlane16_swap per half
+GPK_DEVICE double row_even_both(double x) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const unsigned nl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false)[0];
+  const unsigned nh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false)[0];
+  return __builtin_bit_cast(double, ((unsigned long long)nh << 32) | nl);
+}
+
+// Column Q of the fused sweep (layout of factor_diag): every lane gets -R[Q][c] of its row's
+// R lane (row 0), the pivot by DPP, then v[i] += (-R[Q][i]) v[Q] for i > Q with -R[Q][i]
+// broadcast from lane i of the row. No readlanes: the sweep keeps issuing beside the
+// workers' MFMA and LDS waves (the readlane form starves there, scripts/microbench).
+template <int Q>
+GPK_DEVICE void diag_col64(double (&v)[16]) {
+  const double ta = row_even_both(v[Q]);
+  const double p = nbc<Q>(ta);
+  const double s = rsq64(p);
+  const double nr = -(ta * s);
+  v[Q] = v[Q] * s;
+  if constexpr (Q < 15) {
+#pragma unroll
+    for (int i = Q + 1; i < 16; ++i) {
+      double b;
+      switch (i) {   // (compile-time after unrolling)
+        case 1: b = nbc<1>(nr); break;   case 2: b = nbc<2>(nr); break;
+        case 3: b = nbc<3>(nr); break;   case 4: b = nbc<4>(nr); break;
+        case 5: b = nbc<5>(nr); break;   case 6: b = nbc<6>(nr); break;
+        case 7: b = nbc<7>(nr); break;   case 8: b = nbc<8>(nr); break;
+        case 9: b = nbc<9>(nr); break;   case 10: b = nbc<10>(nr); break;
+        case 11: b = nbc<11>(nr); break; case 12: b = nbc<12>(nr); break;
+        case 13: b = nbc<13>(nr); break; case 14: b = nbc<14>(nr); break;
+        default: b = nbc<15>(nr); break;
+      }
+      v[i] = __builtin_fma(b, v[Q], v[i]);
+    }
+    diag_col64<Q + 1>(v);
+  }
+}
+
 // The owner wave factors the (updated) diagonal tile t = T'_kk held in its registers:
 // one readlane-broadcast sweep of the augmented [T_kk | I] (lanes 0-15: columns of T_kk
 // -> rows of L_kk, lanes 16-31: identity columns -> columns of L_kk^{-1}). Results: lkk
@@ -86,6 +137,19 @@ GPK_DEVICE void factor_diag(const f64x4 t, int k, double* dbuf, double* lkk, dou
     v[i] = left ? x : ((lane - 16 == i) ? 1.0 : 0.0);
   }
   int bad = 0;
+#if GPK_KZZ_DPP
+  diag_col64<0>(v);
+  {
+    // first column whose R[c][c] is not positive-finite (a non-positive pivot makes it NaN
+    // through the rsqrt; the columns before it are untouched by that)
+    double dg = v[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) dg = (c == i) ? v[i] : dg;
+    const bool okd = (dg > 0.0) && (dg < __builtin_huge_val());
+    const unsigned long long badm = __ballot(lane < 16 && !okd);
+    bad = badm ? __builtin_ctzll(badm) + 1 : 0;
+  }
+#else
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const double p = readlane_d(v[q], q);
@@ -97,6 +161,7 @@ GPK_DEVICE void factor_diag(const f64x4 t, int k, double* dbuf, double* lkk, dou
 #pragma unroll
     for (int i = q + 1; i < 16; ++i) v[i] = __builtin_fma(-readlane_d(v[i], q), t, v[i]);
   }
+#endif
   // lanes 0-15: v[i] = L_kk[c][i] (i <= c); lanes 16-31: v[i] = L_kk^{-1}[i][c - 16]
   if (left) {
 #pragma unroll
@@ -396,9 +461,10 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
 //   T_u = L_uu^{-1} (the diagonal blocks of Linv, written by gpk_kzz16_kernel),
 //   X_jb = T_jb;  for k = jb ..: S_u += -L_uk X_k (u > k), X_{k+1} = T_{k+1} S_{k+1}.
 // k-order of every MFMA: q = g + 4 kk, so a tile held in acc layout (reg r <-> row g + 4r)
-// is the B operand of k-step kk straight from register kk. S tiles dealt over the 4 waves
-// (u = wave mod 4); the L tiles of the next step are prefetched from L2 during this one.
-constexpr int KIT = 256;
+// is the B operand of k-step kk straight from register kk. S tiles dealt over 16 waves
+// (u = wave mod 16: one tile per wave up to M = 256, so a step costs one 4-MFMA chain per
+// wave, not four); the L tiles of the next step are prefetched from L2 during this one.
+constexpr int KIT = 1024, KIW = KIT / 64, KIS = 2;   // KIS slots: up to 32 block rows
 __global__ void __launch_bounds__(KIT)
 gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ info,
                    double* __restrict__ Linv) {
@@ -433,15 +499,15 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
     if (i < M && j < M) Linv[(size_t)i * M + j] = Tv[e];
   }
   lds_barrier();
-  f64x4 S[4];
+  f64x4 S[KIS];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) S[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-  // A operands of step k: -L_{jb+u, jb+k}[c][g + 4kk] for the wave's tiles u = wave + 4t
-  double an[4][4];
-  auto load_a = [&](int k, double (&dst)[4][4]) {
+  for (int t = 0; t < KIS; ++t) S[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // A operands of step k: -L_{jb+u, jb+k}[c][g + 4kk] for the wave's tiles u = wave + KIW t
+  double an[KIS][4];
+  auto load_a = [&](int k, double (&dst)[KIS][4]) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int u = wave + 4 * t;
+    for (int t = 0; t < KIS; ++t) {
+      const int u = wave + KIW * t;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
         dst[t][kk] = (u > k && u < nb) ? -Lat(16 * (jb + u) + c, 16 * (jb + k) + g + 4 * kk) : 0.0;
@@ -449,20 +515,20 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
   };
   load_a(0, an);
   for (int k = 0; k + 1 < nb; ++k) {
-    double a[4][4];
+    double a[KIS][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < KIS; ++t)
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) a[t][kk] = an[t][kk];
     if (k + 2 < nb) load_a(k + 1, an);
     double xb[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) xb[kk] = Xs[k * 256 + (g + 4 * kk) * 16 + c];
-    const int tn = (k + 1) >> 2;          // slot of S_{k+1} in its owner wave
-    const bool own = wave == ((k + 1) & 3);
+    const int tn = (k + 1) / KIW;         // slot of S_{k+1} in its owner wave
+    const bool own = wave == ((k + 1) % KIW);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int u = wave + 4 * t;
+    for (int t = 0; t < KIS; ++t) {
+      const int u = wave + KIW * t;
       if (u > k && u < nb) {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) S[t] = mfma64(a[t][kk], xb[kk], S[t]);
@@ -471,7 +537,7 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
     if (own) {                            // X_{k+1} = T_{k+1} S_{k+1}
       f64x4 sv = S[0];
 #pragma unroll
-      for (int t = 1; t < 4; ++t) sv = (t == tn) ? S[t] : sv;
+      for (int t = 1; t < KIS; ++t) sv = (t == tn) ? S[t] : sv;
       f64x4 xv = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) xv = mfma64(Tv[(k + 1) * 256 + c * 16 + g + 4 * kk], sv[kk], xv);
