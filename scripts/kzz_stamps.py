@@ -25,7 +25,7 @@ lib = _native.lib()
 for _ in range(3):
     rc = lib.gpk_kzz_chol_f64(Z.data_ptr(), h.data_ptr(), M, D, 1e-4, 1e-8, 3, L.data_ptr(), Li.data_ptr(),
                               info.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    assert rc == 0
+    assert rc == 0, f"rc={rc}"
 torch.cuda.synchronize()
 v = info.cpu().tolist()
 st = [v[1 + 3 * k: 4 + 3 * k] for k in range(T)]
