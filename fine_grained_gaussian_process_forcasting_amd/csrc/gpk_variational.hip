@@ -1805,7 +1805,22 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
   const float s2 = hyp[0];
   const float* ls = hyp + 4 + D;
   __shared__ float cms[kCmParts * 64];
-  for (int e = tid; e < M * D; e += 256) fzs[e] = Z[e] / ls[e % D];
+  // (every global read of this one-workgroup kernel is issued in batches of 8 per thread:
+  // one memory latency per batch instead of one per element)
+  for (int base = 0; base < M * D; base += 8 * 256) {
+    float zv[8], lv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + 256 * u + tid, ec = e < M * D ? e : 0;
+      zv[u] = Z[ec];
+      lv[u] = ls[ec % D];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + 256 * u + tid;
+      if (e < M * D) fzs[e] = zv[u] / lv[u];
+    }
+  }
   lds_barrier();
   col_means(fzs, M, D, D, D, cms, cmf);   // the same fp32 sums as stage_inducing: the identical centre
   for (int e = tid; e < M * D; e += 256) fzs[e] -= cmf[e % D];
@@ -1818,17 +1833,43 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
   const double sumQ = rx2[D], sumgv = rx2[D + 1];
   const double* gx = rx2 + D + 2;
   const double sumgm = gx[D];
-  for (int e = tid; e < M * D; e += 256) {
-    const int p = e / D, d = e - p * D;
-    dZ[e] = (float)((QX[e] - (double)fzs[e] * q[p]) / (double)ls[d]);
+  for (int base = 0; base < M * D; base += 8 * 256) {
+    double xv[8], qv[8];
+    float lv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + 256 * u + tid, ec = e < M * D ? e : 0;
+      const int p = ec / D, d = ec - p * D;
+      xv[u] = QX[ec];
+      qv[u] = q[p];
+      lv[u] = ls[d];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + 256 * u + tid;
+      if (e < M * D) dZ[e] = (float)((xv[u] - (double)fzs[e] * qv[u]) / (double)lv[u]);
+    }
   }
   const int nk = 256 / D;
   double acc = 0.0;
   if (tid < nk * D) {
     const int d = tid % D, k = tid / D;
-    for (int p = k; p < M; p += nk) {
-      const double zsv = (double)fzs[p * D + d];
-      acc += q[p] * zsv * zsv - 2.0 * zsv * QX[(size_t)p * D + d];
+    for (int p0 = k; p0 < M; p0 += 8 * nk) {   // p ascending, as one sequential sum
+      double qv[8], xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = p0 + nk * u, pc = p < M ? p : 0;
+        qv[u] = q[pc];
+        xv[u] = QX[(size_t)pc * D + d];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = p0 + nk * u;
+        if (p < M) {
+          const double zsv = (double)fzs[p * D + d];
+          acc += qv[u] * zsv * zsv - 2.0 * zsv * xv[u];
+        }
+      }
     }
   }
   red[tid] = acc;
@@ -1860,6 +1901,11 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
 // live in LDS, shared by the 4 waves; only the adjoint's Q^T needs a per-wave LDS
 // transpose (one tile at a time).
 // ---------------------------------------------------------------------------
+#ifndef GPK_FWD_OCC
+#define GPK_FWD_OCC 3   // waves per SIMD gpk_var_fwd_r_kernel's register budget is sized for (3: 161
+                         // VGPRs, cfg 5 forward 55.7 vs 56.6 us unbounded; a next-chunk point
+                         // prefetch measured slower at 3 (spills) and at 2 waves/SIMD)
+#endif
 constexpr int RLS = 66;        // L^{-1} row stride (doubles)
 
 template <int DQ>
@@ -2025,7 +2071,7 @@ GPK_DEVICE void dim_consts(const float* sm, const float* ls, const float* w, int
 }
 
 template <int DQ>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, GPK_FWD_OCC)
 gpk_var_fwd_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
                      const double* __restrict__ Linv, const float* __restrict__ vmean,
                      const float* __restrict__ vstd, const float* __restrict__ hyp, int B, int N,

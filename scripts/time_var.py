@@ -27,7 +27,7 @@ gv = torch.randn(B, N, generator=g).to(dev)
 kz = ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h)
 
 
-def timeit(fn, n=10):
+def timeit(fn, n=30):
     # back-to-back calls between one event pair: the GPU stays busy, so host launch
     # latency is hidden whenever the kernels are longer than it
     for _ in range(3):
