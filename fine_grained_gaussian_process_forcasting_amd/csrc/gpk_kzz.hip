@@ -119,16 +119,13 @@ GPK_DEVICE void diag_col64(double (&v)[16]) {
   }
 }
 
-// The owner wave factors the (updated) diagonal tile t = T'_kk held in its registers:
-// one readlane-broadcast sweep of the augmented [T_kk | I] (lanes 0-15: columns of T_kk
+// The diagonal wave factors the (updated, handed-over) diagonal tile t = T'_kk:
+// one broadcast sweep (diag_col64) of the augmented [T_kk | I] (lanes 0-15: columns of T_kk
 // -> rows of L_kk, lanes 16-31: identity columns -> columns of L_kk^{-1}). Results: lkk
 // (16 x 17, row-major L_kk), linv (16 x 17, L_kk^{-1}) in LDS; status = failed column + 1.
-GPK_DEVICE void factor_diag(const f64x4 t, int k, double* dbuf, double* lkk, double* linv,
-                            int* status) {
-  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) dbuf[(g + 4 * r) * 16 + c] = t[r];
-  wave_lds_sync();
+GPK_DEVICE void factor_diag(int k, const double* dbuf, double* lkk, double* linv, int* status,
+                            int* stamp) {
+  const int lane = threadIdx.x & 63, c = lane & 15;
   double v[16];
   const bool left = lane < 16;
 #pragma unroll
@@ -137,6 +134,12 @@ GPK_DEVICE void factor_diag(const f64x4 t, int k, double* dbuf, double* lkk, dou
     v[i] = left ? x : ((lane - 16 == i) ? 1.0 : 0.0);
   }
   int bad = 0;
+#if GPK_KZZ_STAMPS
+  if (stamp != nullptr) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the tile is in registers
+    if (lane == 0) stamp[1] = (int)__builtin_amdgcn_s_memtime();
+  }
+#endif
 #if GPK_KZZ_DPP
   diag_col64<0>(v);
   {
@@ -171,6 +174,9 @@ GPK_DEVICE void factor_diag(const f64x4 t, int k, double* dbuf, double* lkk, dou
     for (int i = 0; i < 16; ++i) linv[i * kLinvStride + c] = v[i];
   }
   if (lane == 0) status[0] = bad == 0 ? 0 : 16 * k + bad;
+#if GPK_KZZ_STAMPS
+  if (stamp != nullptr && lane == 0) stamp[2] = (int)__builtin_amdgcn_s_memtime();
+#endif
 }
 
 // LDS flag words of the factor kernel (volatile, LDS address space: ds_read / ds_write only)
@@ -309,6 +315,10 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
   int result = 0;
   if (wave == NWK) {
     // ================= diagonal wave =================
+    // critical path: win issue arbitration against the workers' MFMA / LDS streams (the
+    // stamps show the step-k+1 sweep taking 13 K cycles beside step k's update at M = 256
+    // vs 6 K alone)
+    __builtin_amdgcn_s_setprio(3);
     for (int attempt = 0; attempt <= max_tries; ++attempt) {
       int failed = 0;
       for (int k = -1; k < T; ++k) {
@@ -331,10 +341,14 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
         }
         if (k + 1 < T) {   // [C] look-ahead: factor T'_{k+1,k+1} once it is handed over
           kzz_spin_until(fl, attempt * (T + 1) + k + 1);
-          f64x4 t;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) t[r] = dbuf[r * 64 + lane];
-          factor_diag(t, k + 1, dbuf, lkk, linv, flagw + kKfStatus);
+          int* stamp = nullptr;
+#if GPK_KZZ_STAMPS
+          if (attempt == 0) {
+            stamp = info + 1 + 3 * T + 3 * (k + 1);
+            if (lane == 0) stamp[0] = (int)__builtin_amdgcn_s_memtime();
+          }
+#endif
+          factor_diag(k + 1, dbuf, lkk, linv, flagw + kKfStatus, stamp);
         }
       }
       if (!failed) {
@@ -347,6 +361,7 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
       if (lane == 0) fl[kKfStatus] = 0;
       lds_barrier();
     }
+    __builtin_amdgcn_s_setprio(0);
   } else {
     // ================= workers =================
     // upper tiles in column-major order t = j (j + 1) / 2 + i, dealt round-robin to the workers
@@ -369,9 +384,9 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
       for (int q = 0; q < NS; ++q) {
         asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
         if (its[q] < T) acc[q] = kzz_tile(zt, zn, ZS, D16, M, T, its[q], jts[q], s2, jitter_var, ladder);
-        if (its[q] == 0 && jts[q] == 0) {   // hand tile (0, 0) to the diagonal wave
+        if (its[q] == 0 && jts[q] == 0) {   // hand tile (0, 0) to the diagonal wave (row-major)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dbuf[r * 64 + lane] = acc[q][r];
+          for (int r = 0; r < 4; ++r) dbuf[(g + 4 * r) * 16 + c] = acc[q][r];
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
           if (lane == 0) fl[kKfTile] = attempt * (T + 1);
         }
@@ -422,7 +437,7 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) acc[q] = mfma64(-panel[kk * 64 + lane], panel[kk * 64 + lane], acc[q]);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dbuf[r * 64 + lane] = acc[q][r];
+            for (int r = 0; r < 4; ++r) dbuf[(g + 4 * r) * 16 + c] = acc[q][r];   // row-major
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
             if (lane == 0) fl[kKfTile] = attempt * (T + 1) + k + 1;
           }

@@ -24,5 +24,5 @@ for c in ('cfg3', 'cfg1'):
     d = json.load(open('$O/gp_step_' + c + '.json'))
     print(c, {m: {k: (v if not isinstance(v, dict) else round(v['ms_per_step'], 3)) for k, v in d[m].items()} for m in ('eager', 'graph', 'eager_anomaly')})"
 bash scripts/gpu_r03q.sh || exit 6
-GPK_LIB=$R/fine_grained_gaussian_process_forcasting_amd/_lib_ab/kzz_stamps/libgpk.so timeout -k 10 100 python scripts/kzz_stamps.py 256 > $O/kzz_stamps_256.txt 2>&1; tail -n 25 $O/kzz_stamps_256.txt
+GPK_LIB=$R/fine_grained_gaussian_process_forcasting_amd/_lib_ab/kzz_stamps/libgpk.so timeout -k 10 100 python scripts/kzz_stamps.py 256 32 > $O/kzz_stamps_256.txt 2>&1; tail -n 25 $O/kzz_stamps_256.txt
 echo DONE

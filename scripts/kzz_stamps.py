@@ -1,6 +1,7 @@
 """Per-step phase clocks of a GPK_KZZ_STAMPS=1 build of gpk_kzz16_kernel (load it with
 GPK_LIB=<path>): info[1 + 3k .. 3 + 3k] = s_memtime at step k's start, after its diagonal
-barrier and after its TRSM barrier (workgroup thread 0, first attempt).
+barrier and after its TRSM barrier (workgroup thread 0, first attempt); info[1 + 3T + 3k ..]
+= the diagonal wave's factor of tile (k, k): hand-over seen, tile in registers, factor done.
    GPK_LIB=... python scripts/kzz_stamps.py [M] [D]"""
 import math
 import os
@@ -20,7 +21,7 @@ h = torch.cat([torch.tensor([LN2]), torch.full((D,), LN2)]).to(dev)
 T = (M + 15) // 16
 L = torch.empty(M, M, dtype=torch.float64, device=dev)
 Li = torch.empty(M, M, dtype=torch.float64, device=dev)
-info = torch.zeros(4 + 3 * T, dtype=torch.int32, device=dev)
+info = torch.zeros(8 + 6 * T, dtype=torch.int32, device=dev)
 lib = _native.lib()
 for _ in range(3):
     rc = lib.gpk_kzz_chol_f64(Z.data_ptr(), h.data_ptr(), M, D, 1e-4, 1e-8, 3, L.data_ptr(), Li.data_ptr(),
@@ -41,3 +42,11 @@ for k, (a, b, c) in enumerate(rows):
     print(f"k={k:2d} {a:7d} {b:7d} {c:7d}")
 tot = [sum(r[i] for r in rows) for i in range(3)]
 print("sum", tot, "total", sum(tot))
+ds = [v[1 + 3 * T + 3 * k: 4 + 3 * T + 3 * k] for k in range(T)]
+print("diagonal wave, factor of (k,k) (ticks): hand-over seen -> tile loaded / sweep + LDS writes; "
+      "hand-over seen relative to the previous step's TRSM barrier")
+for k in range(1, T):
+    ld = (ds[k][1] - ds[k][0]) & 0xffffffff
+    sw = (ds[k][2] - ds[k][1]) & 0xffffffff
+    ho = (ds[k][0] - st[k - 1][2]) & 0xffffffff
+    print(f"k={k:2d} load {ld:6d} sweep {sw:6d}  handover-after-trsm {ho:6d}")
