@@ -180,12 +180,13 @@ GPK_DEVICE void factor_diag(int k, const double* dbuf, double* lkk, double* linv
 }
 
 // LDS flag words of the factor kernel (volatile, LDS address space: ds_read / ds_write only)
-enum KzzFlag { kKfTile = 0, kKfTmo = 1, kKfStatus = 2 };
+// kKfTile + (t & 1): epoch of the last diagonal tile t handed over into dbuf[t & 1]
+enum KzzFlag { kKfTile = 0, kKfTmo = 1, kKfStatus = 2, kKfTile1 = 3 };
 constexpr int kKzzTimeout = 1 << 20;   // info code of an expired spin-wait (never NotPSD)
 
-GPK_DEVICE void kzz_spin_until(lds_vint* f, int target) {
+GPK_DEVICE void kzz_spin_until(lds_vint* f, int word, int target) {
   int n = 0;
-  while (f[kKfTile] != target) {
+  while (f[word] != target) {
     if (++n > (1 << 20)) {   // bounded: a logic error ends as info = 1 << 20, never a hang
       f[kKfTmo] = 1;
       break;
@@ -260,8 +261,8 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
   extern __shared__ __attribute__((aligned(16))) double dsm[];
   const int T = (M + 15) >> 4;
   double* panel = dsm;                 // (T - 1) tiles x 256, [slot][reg][lane]
-  double* dbuf = panel + (size_t)(T > 1 ? T - 1 : 1) * 256;   // 256: the hand-over tile
-  double* linv = dbuf + 256;           // 16 x 17: L_kk^{-1}
+  double* dbuf = panel + (size_t)(T > 1 ? T - 1 : 1) * 256;   // 2 x 256: hand-over tiles (parity)
+  double* linv = dbuf + 512;           // 16 x 17: L_kk^{-1}
   double* lkk = linv + 16 * kLinvStride;                      // 16 x 17: L_kk
   int* flagw = (int*)(lkk + 16 * kLinvStride);                // KzzFlag words
   lds_vint* fl = as_lds_flags(flagw);
@@ -290,7 +291,7 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
       if (e < M * ZS) zt[e] = d < D ? v[u] / l[u] : 0.f;
     }
   }
-  if (tid < 4) flagw[tid] = tid == kKfTile ? -1 : 0;
+  if (tid < 4) flagw[tid] = (tid == kKfTile || tid == kKfTile1) ? -1 : 0;
   lds_barrier();
   for (int d = wave; d < D; d += KT / 64) {   // column means: one wave per column
     float sm = 0.f;
@@ -339,16 +340,30 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
           }
           lds_barrier();
         }
-        if (k + 1 < T) {   // [C] look-ahead: factor T'_{k+1,k+1} once it is handed over
-          kzz_spin_until(fl, attempt * (T + 1) + k + 1);
+        if (k + 1 < T) {
+          // [C] look-ahead: tile k+1 was handed over through panel k-1 one step earlier; the
+          // diagonal wave applies panel k's R_{k,k+1} (slot 0) itself and factors it
+          const int tk = k + 1;
+          double* db = dbuf + (tk & 1) * 256;
+          kzz_spin_until(fl, kKfTile + 3 * (tk & 1), attempt * (T + 1) + tk);
           int* stamp = nullptr;
 #if GPK_KZZ_STAMPS
           if (attempt == 0) {
-            stamp = info + 1 + 3 * T + 3 * (k + 1);
+            stamp = info + 1 + 3 * T + 3 * tk;
             if (lane == 0) stamp[0] = (int)__builtin_amdgcn_s_memtime();
           }
 #endif
-          factor_diag(k + 1, dbuf, lkk, linv, flagw + kKfStatus, stamp);
+          f64x4 t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[r] = db[r * 64 + lane];
+          if (k >= 0) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) t = mfma64(-panel[kk * 64 + lane], panel[kk * 64 + lane], t);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) db[(g + 4 * r) * 16 + c] = t[r];   // row-major for the sweep
+          wave_lds_sync();
+          factor_diag(tk, db, lkk, linv, flagw + kKfStatus, stamp);
         }
       }
       if (!failed) {
@@ -384,11 +399,12 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
       for (int q = 0; q < NS; ++q) {
         asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
         if (its[q] < T) acc[q] = kzz_tile(zt, zn, ZS, D16, M, T, its[q], jts[q], s2, jitter_var, ladder);
-        if (its[q] == 0 && jts[q] == 0) {   // hand tile (0, 0) to the diagonal wave (row-major)
+        if (its[q] == jts[q] && its[q] < 2 && its[q] < T) {   // hand tiles (0,0), (1,1) over raw
+          const int tk = its[q];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dbuf[(g + 4 * r) * 16 + c] = acc[q][r];
+          for (int r = 0; r < 4; ++r) dbuf[tk * 256 + r * 64 + lane] = acc[q][r];
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-          if (lane == 0) fl[kKfTile] = attempt * (T + 1);
+          if (lane == 0) fl[kKfTile + 3 * tk] = attempt * (T + 1) + tk;
         }
       }
       int failed = 0;
@@ -430,23 +446,26 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
 #if GPK_KZZ_STAMPS
         if (tid == 0 && attempt == 0) info[3 + 3 * k] = (int)__builtin_amdgcn_s_memtime();
 #endif
-        // [C] the hand-over tile first, then the rest of the trailing update
+        // [C] hand over (k+2, k+2) through panel k first (the diagonal wave applies panel
+        // k+1 to it itself); (k+1, k+1) is the diagonal wave's from here on
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
-          if (its[q] == k + 1 && jts[q] == k + 1) {
+          if (its[q] == k + 2 && jts[q] == k + 2 && k + 2 < T) {
+            const int tk = k + 2;
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) acc[q] = mfma64(-panel[kk * 64 + lane], panel[kk * 64 + lane], acc[q]);
+            for (int kk = 0; kk < 4; ++kk)
+              acc[q] = mfma64(-panel[256 + kk * 64 + lane], panel[256 + kk * 64 + lane], acc[q]);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dbuf[(g + 4 * r) * 16 + c] = acc[q][r];   // row-major
+            for (int r = 0; r < 4; ++r) dbuf[(tk & 1) * 256 + r * 64 + lane] = acc[q][r];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            if (lane == 0) fl[kKfTile] = attempt * (T + 1) + k + 1;
+            if (lane == 0) fl[kKfTile + 3 * (tk & 1)] = attempt * (T + 1) + tk;
           }
         }
         // (a program-order software pipeline of the operand reads -- tile q+1's requested
         // before tile q's MFMAs -- measured slower: 155 vs 148 us at M = 256)
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
-          if (its[q] > k && its[q] < T && !(its[q] == k + 1 && jts[q] == k + 1)) {
+          if (its[q] > k && its[q] < T && !(its[q] == jts[q] && its[q] <= k + 2)) {
             const double* pa = panel + (size_t)(its[q] - k - 1) * 256;
             const double* pb = panel + (size_t)(jts[q] - k - 1) * 256;
 #pragma unroll
@@ -579,7 +598,7 @@ void set_lds_once() {
 template <int NS>
 int launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
   const int T = (a.M + 15) >> 4;
-  const size_t lds = (size_t)((T > 1 ? T - 1 : 1) * 256 + 256 + 2 * 16 * kLinvStride) * sizeof(double) +
+  const size_t lds = (size_t)((T > 1 ? T - 1 : 1) * 256 + 512 + 2 * 16 * kLinvStride) * sizeof(double) +
                      4 * sizeof(int) + (size_t)(a.M * kzz_zstride(a.D) + a.M + a.D) * sizeof(float);
   if (lds > 160 * 1024) return -4;
   set_lds_once<gpk_kzz16_kernel<NS>>();
