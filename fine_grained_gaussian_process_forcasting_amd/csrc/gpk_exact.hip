@@ -116,6 +116,10 @@ GPK_DEVICE int plan_tile(int t) {
   return i | (j << 8);
 }
 
+// R_kk^{-T} in LDS: 16 rows of stride kWS floats (20: the diagonal wave's 16-B row writes and
+// the workers' column reads are both conflict-free; 16 was 4-way on both)
+constexpr int kWS = 20, kWBuf = 16 * kWS;
+
 struct ExactLds {
   // offsets in floats
   int xf, xh, xl, nrm, rv, rw, panel, wbuf, dsc, hbuf, cpart, rbfc, red, total;
@@ -132,10 +136,13 @@ __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
   o.rw = o.rv + NB * 16;                 // working copy of -(y - c) (the RHS column)
   o.panel = o.rw + NB * 16;
   o.wbuf = o.panel + 2 * (NB + 1) * 256;  // (panel: double-buffered R rows)
-  o.dsc = o.wbuf + 2 * 256;              // (wbuf: R_kk^{-T}, double-buffered by step parity)
+  o.dsc = o.wbuf + 2 * kWBuf;            // (wbuf: R_kk^{-T}, double-buffered by step parity)
   o.hbuf = o.dsc + 256;                  // (dsc: the diagonal wave's working tile)
-  o.cpart = o.hbuf + 2 * 512;            // (hbuf: look-ahead hand-off {(k,k+1), (k+1,k+1)} x parity)
-  o.rbfc = o.cpart + 64 * W + 256;      // RbfK (16-byte aligned)
+  // (hbuf: look-ahead hand-off {(k,k+1), (k+1,k+1)} x parity). The prologue's column
+  // partials and means (64 W + 256 <= 1280 floats for W <= 16) alias dsc + hbuf: both are
+  // first written after the prologue's closing barrier.
+  o.cpart = o.dsc;
+  o.rbfc = o.hbuf + 2 * 512;             // RbfK (16-byte aligned)
   o.red = o.rbfc + 4;
   o.total = o.red + 4 * W + 40;
   return o;
@@ -365,7 +372,7 @@ GPK_DEVICE f32x4 trsm_tile(const WOp& w, const f32x4 t) { return trsm_tile_f32(w
 GPK_DEVICE f32x4 load_w(const float* wb, int c, int grp) {
   f32x4 q;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) q[r] = wb[(4 * grp + r) * 16 + c];
+  for (int r = 0; r < 4; ++r) q[r] = wb[(4 * grp + r) * kWS + c];
   return q;
 }
 // The same through volatile LDS reads (ordered after a flag read, see worker_step).
@@ -374,7 +381,7 @@ GPK_DEVICE f32x4 load_w_v(const float* wb, int c, int grp) {
   const lds_vfloat* w = (const lds_vfloat*)wb;
   f32x4 q;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) q[r] = w[(4 * grp + r) * 16 + c];
+  for (int r = 0; r < 4; ++r) q[r] = w[(4 * grp + r) * kWS + c];
   return q;
 }
 
@@ -429,7 +436,7 @@ GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) { return mma_tn(v, v, d); }
 // from one instruction stream: at step m every lane does
 //   v[m] *= rsqrt(pivot);   v[i] -= R[m][i] * v[m]   (i > m)
 // with R[m][i] broadcast from R-lane i by readlane. `tile` holds -T in acc
-// layout. -W (transposed: wbuf[c*16+m] = -W[m][c]) is published FIRST together
+// layout. -W (transposed: wbuf[c*kWS+m] = -W[m][c]) is published FIRST together
 // with the pass/fail verdict (every pivot checked positive-finite on the scalar
 // broadcast: v_cmp_class), then the factor-done flag is raised; only then the L
 // diagonal block, the exact failing column and log|T| are produced.
@@ -475,7 +482,7 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
   if (grp == 1) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
-      *(f32x4*)&wbuf[c * 16 + 4 * g] = f32x4{-v[4 * g], -v[4 * g + 1], -v[4 * g + 2], -v[4 * g + 3]};
+      *(f32x4*)&wbuf[c * kWS + 4 * g] = f32x4{-v[4 * g], -v[4 * g + 1], -v[4 * g + 2], -v[4 * g + 3]};
   }
   // diagonal of R (lane c < 16 holds R[c][c] in v[c])
   float dg = v[0];
@@ -711,7 +718,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // served in order, and the diagonal wave completes its R_KK^{-T} and failure-word writes
   // before it releases the flag, so reads issued after a flag read that sees epoch K see
   // them too (all volatile: the compiler keeps the order). Otherwise: wait, re-read.
-  const float* wbk = x.wbuf + (K & 1) * 256;
+  const float* wbk = x.wbuf + (K & 1) * kWBuf;
   const int flag_now = x.vflag[kFlagFact];
   int fail = x.vflag[kFlagFail + e0 / 32];
   f32x4 q = load_w_v(wbk, c, grp);
@@ -966,7 +973,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // served in order, and the diagonal wave completes its R_KK^{-T} and failure-word writes
   // before it releases the flag, so reads issued after a flag read that sees epoch K see
   // them too (all volatile: the compiler keeps the order). Otherwise: wait, re-read.
-  const float* wbk = x.wbuf + (K & 1) * 256;
+  const float* wbk = x.wbuf + (K & 1) * kWBuf;
   const int flag_now = x.vflag[kFlagFact];
   int fail = x.vflag[kFlagFail + e0 / 32];
   f32x4 q = load_w_v(wbk, c, grp);
@@ -1473,7 +1480,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       spin_until(vflag, kFlagT00, 32 * attempt);
       for (int k = 0; k < NB; ++k) {
         const int epoch = 32 * attempt + k;
-        float* wb = wbuf + (k & 1) * 256;
+        float* wb = wbuf + (k & 1) * kWBuf;
         unsigned long long dt0 = 0;
         if constexpr (STAMPS) {
           dt0 = __builtin_amdgcn_s_memtime();
