@@ -53,6 +53,10 @@
 #ifndef GPK_TRSM_F16
 #define GPK_TRSM_F16 0   // 1: trailing-tile TRSM on split-f16 MFMA (measured 3 % slower: more spills); 0 = fp32 MFMA
 #endif
+#ifndef GPK_EXACT_PRIO
+#define GPK_EXACT_PRIO 1   // workers raise their issue priority to this for the hand-over and the TRSM
+                           // (0: off; 1 measured 2.5 % faster per launch, scripts/gpu_ab_prio.sh)
+#endif
 #ifndef GPK_DIAG_DPP
 #define GPK_DIAG_DPP 1   // diagonal sweep as DPP-broadcast FMAs (gpk_diag_dpp.inc); 0 = readlane form
 #endif
@@ -902,6 +906,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   };
   if constexpr (K > 0) {
     if constexpr (!LAST) {
+      if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // hand-over: the diagonal wave waits
       if (wv == TA % WK) {
         upd_ij(acc[TA / WK], IC<K>{}, IC<K + 1>{});
         publish_tile(hA, lane, acc[TA / WK], x.vflag, kFlagHA, e0 + K);
@@ -910,6 +915,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
         upd_ij(acc[TB / WK], IC<K + 1>{}, IC<K + 1>{});
         publish_tile(hA + 256, lane, acc[TB / WK], x.vflag, kFlagHB, e0 + K);
       }
+      if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     // trailing update from panel K-1 over the other tiles with i >= K
     // (t < P(K-1)), highest slot first. Re-laundered: the hand-over branches
@@ -986,6 +992,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
   if (fail != 0) return 1;
+  if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // TRSM: panel K gates step K+1
   const WOp wq = w_split(q);
   constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
   constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
@@ -1023,6 +1030,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // panel K and z_K are out: count in at the step barrier, then do the work that
   // does not depend on the other waves (zero-L, deferred RBF) before waiting on it
   worker_arrive(x);
+  if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
   // deferred RBF of block row K+2 (its diagonal tile is handed over at step K+1)
   if constexpr (K + 2 < NB) {
     constexpr int RLO = plan_P<NB>(K + 2), RHI = plan_P<NB>(K + 1) - 1;
