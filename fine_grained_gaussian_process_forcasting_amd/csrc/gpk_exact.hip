@@ -53,6 +53,9 @@
 #ifndef GPK_TRSM_F16
 #define GPK_TRSM_F16 0   // 1: trailing-tile TRSM on split-f16 MFMA (measured 3 % slower: more spills); 0 = fp32 MFMA
 #endif
+#ifndef GPK_EXACT_PRIO_RHS
+#define GPK_EXACT_PRIO_RHS 1   // raise the worker priority already at the right-hand side (0: at the TRSM)
+#endif
 #ifndef GPK_EXACT_PRIO
 #define GPK_EXACT_PRIO 1   // workers raise their issue priority to this for the hand-over and the TRSM
                            // (0: off; 1 measured 2.5 % faster per launch, scripts/gpu_ab_prio.sh)
@@ -943,6 +946,9 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     static_for_desc<NALL>(bulk);
   }
   GPK_WSTAMP(2, 1)  // trailing update (+ hand-over)
+#if GPK_EXACT_PRIO_RHS
+  __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // zero-L + right-hand side lead into the TRSM
+#endif
   // zero L's strictly-upper part of block-row K (streams out behind the MFMAs)
   if (x.Lb != nullptr) {
     const int N = FULL ? 16 * NB : x.N;
