@@ -78,6 +78,19 @@ def var_adj_flops_per_window(N, M, D):
     return 3 * D * M * N + 5 * M * N + 4 * M * N * D + 10 * M * N + 6 * D * N, 3 * M * M * N
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), for the cpu_baseline record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def make_inputs(B, N, D, device, seed):
     g = torch.Generator().manual_seed(seed)
     X = (torch.randn(B, N, D, generator=g) / math.sqrt(D)).to(device)
@@ -334,18 +347,26 @@ def main():
     ap.add_argument("--no-grad", action="store_true", help="skip the backward side measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end train-step side leg")
     ap.add_argument("--no-cfg2", action="store_true", help="skip the B=128 N=128 side leg")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend (nccl = RCCL; gloo only for the one-GPU world-2 test)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="every rank uses cuda:0 (tests/test_world2_gpu.py: two ranks on one GPU)")
     args = ap.parse_args()
 
     rank, local, world = env_rank_world()
     if world != args.gpus and world == 1 and args.gpus > 1:
         raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
+    local = 0 if args.share_device else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # under torchrun the process group is created even at world size 1, so the RCCL
     # init / barrier / MAX all-reduce path of the timed region runs on a one-GPU box too
     pg = world > 1 or "RANK" in os.environ
     if pg:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     N, D = args.N, args.D
     if args.strong:
@@ -394,8 +415,12 @@ def main():
     elapsed = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     ops.check_cholesky_info(info, 1e-6, inputs=(X,))
+    rank_times = None
     if pg:
         t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        every = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(every, t)
+        rank_times = [[float(v) for v in r.tolist()] for r in every]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = (float(v) for v in t.tolist())
     mean_mll = float(totals[-1].item()) / B_total
@@ -470,13 +495,16 @@ def main():
             "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "precision": "f32 inputs / outputs, fp32 RBF exponent, diagonal factor and TRSM; the Gram "
+                         "and the trailing Cholesky updates on split-f16 MFMA (hi + lo planes, 22 "
+                         "significant bits, every product exact, fp32 accumulation: DESIGN.md §4.1)",
             "data": "synthetic",
             "config": {"workload": "exact-GP windows (BASELINE configs[3]): RBF Gram + jittered "
                                    "Cholesky + forward solve + MLL, L written; MLL partials "
                                    "all-reduced once per timed region",
                        "windows_per_gpu": B, "N": N, "D": D, "global_batch": B_total,
                        "parallelism": f"window-sharded x{world}", "kernel": "gpk_exact_mll_f32",
-                       "process_group": "nccl" if pg else None},
+                       "process_group": args.backend if pg else None},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": load_traffic(f"exact_B{B}_N{N}_D{D}"),
@@ -485,6 +513,10 @@ def main():
                          "fp32_frac": fpw * B / (kern_ms * 1e-3) / FP32_PEAK},
             "mean_mll": mean_mll,
         }
+        if rank_times is not None:
+            line["rank_times"] = {"ms_per_step": [r[0] / args.steps * 1e3 for r in rank_times],
+                                  "kernel_ms": [r[1] for r in rank_times],
+                                  "note": "per-rank values before the MAX all-reduce"}
         if grad_ms is not None:
             line["backward"] = {"kernel": "gpk_exact_mll_grad_f32", "kernel_ms": grad_ms, "eager_ms": grad_eager,
                                 "windows_per_s_per_gpu": B / (grad_ms * 1e-3),
@@ -517,6 +549,7 @@ def main():
             v_one, s_one = cpu_exact_baseline(N, D, args.cpu_seconds / 2, 1)
             line["cpu_baseline"] = {
                 "value": v_all, "unit": "windows/s", "cores": nthr, "kind": "port",
+                "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
                 "sample": f"{s_all} through oracle.exact_mll_torch_cpu (GPyTorch's torch-CPU "
                           f"arithmetic, fp32, MKL) on {nthr} host threads (the job's CPU share; "
                           f"os.cpu_count()={os.cpu_count()})",

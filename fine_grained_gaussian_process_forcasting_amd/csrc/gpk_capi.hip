@@ -199,11 +199,17 @@ int gpk_variational_elbo_grad_f32(const float* y, long long ldy, const float* me
   if (m == nullptr) return -8;
   if (s == nullptr) return -9;
   if (M < 1) return -10;
-  if (R < 1) return -11;
+  if (R < 0) return -11;
   if (N < 1) return -12;
-  if (gelbo == nullptr) return -14;
-  if (dmean == nullptr || dvar == nullptr || dnoise_part == nullptr || dm == nullptr || ds == nullptr)
+  if (R > 0 && gelbo == nullptr) return -14;
+  if (dm == nullptr || ds == nullptr || (R > 0 && (dmean == nullptr || dvar == nullptr || dnoise_part == nullptr)))
     return -15;
+  if (R == 0) {
+    // an empty batch (the forward's no-op): no rows, and the KL enters scaled by sum g = 0
+    hipError_t e = hipMemsetAsync(dm, 0, sizeof(float) * (size_t)M, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipMemsetAsync(ds, 0, sizeof(float) * (size_t)M, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : (int)e;
+  }
   return gpk_launch_elbo_grad(y, ldy, mean, ldm, var, ldv, noise, m, s, M, R, N, kl_scale, gelbo, dmean,
                               dvar, dnoise_part, dm, ds, (hipStream_t)stream);
 }

@@ -60,6 +60,10 @@
 #define GPK_EXACT_PRIO 1   // workers raise their issue priority to this for the hand-over and the TRSM
                            // (0: off; 1 measured 2.5 % faster per launch, scripts/gpu_ab_prio.sh)
 #endif
+#ifndef GPK_KO
+#define GPK_KO 0   // development knockouts (timing only, results wrong): 1 TRSM MFMA, 2 RHS, 4 zero-L,
+                   // 8 deferred RBF, 16 bulk trailing update, 32 TRSM L stores, 64 diagonal sweep
+#endif
 #ifndef GPK_DIAG_DPP
 #define GPK_DIAG_DPP 1   // diagonal sweep as DPP-broadcast FMAs (gpk_diag_dpp.inc); 0 = readlane form
 #endif
@@ -475,7 +479,7 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
     __builtin_amdgcn_sched_barrier(0);
   }
 #if GPK_DIAG_DPP
-  diag_sweep_dpp(v);
+  if (!(GPK_KO & 64)) diag_sweep_dpp(v);
 #else
   diag_sweep<0>(v);
 #endif
@@ -496,7 +500,7 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
 #pragma unroll
   for (int i = 1; i < 16; ++i) dg = (c == i) ? v[i] : dg;
   const bool okd = (dg > 0.f) && (dg < __builtin_huge_valf());
-  const unsigned long long badm = __ballot(lane < 16 && !okd);
+  const unsigned long long badm = (GPK_KO != 0) ? 0ull : __ballot(lane < 16 && !okd);
   if (badm != 0 && lane == 0) *fail_flag = 1;  // provisional: exact column below
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   if (lane == 0) flags[kFlagFact] = epoch;
@@ -938,7 +942,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if constexpr (s == TD / WK) sk = sk || (wv == TD % WK);
       if constexpr (!LAST && s == TA / WK) sk = sk || (wv == TA % WK);
       if constexpr (!LAST && s == TB / WK) sk = sk || (wv == TB % WK);
-      if (!sk) upd(acc[s], I);
+      if (!sk && !(GPK_KO & 16)) upd(acc[s], I);
     };
     if constexpr (NALL < SLOTS && (Pkm1 % WK) != 0) {
       if (wv < Pkm1 % WK) bulk(IC<NALL>{});
@@ -950,7 +954,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // zero-L + right-hand side lead into the TRSM
 #endif
   // zero L's strictly-upper part of block-row K (streams out behind the MFMAs)
-  if (x.Lb != nullptr) {
+  if (!(GPK_KO & 4) && x.Lb != nullptr) {
     const int N = FULL ? 16 * NB : x.N;
     const int c0 = 16 * (K + 1);
     for (int q = wv; q < 16; q += WK) {
@@ -969,7 +973,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // (rw holds -(y - c); only column 0 of the tile is live, so it round-trips
   // through LDS on the c == 0 lanes)
   const int rfirst = K + (((wv - K) % WK) + WK) % WK;
-  if constexpr (K > 0) {
+  if constexpr (K > 0 && !(GPK_KO & 2)) {
     for (int i = rfirst; i < NB; i += WK) {
       f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -997,7 +1001,10 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     q = load_w_v(wbk, c, grp);
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
-  if (fail != 0) return 1;
+  if (GPK_KO == 0 && fail != 0) {
+    __builtin_amdgcn_s_setprio(0);   // the jitter-ladder retry starts at the base priority
+    return 1;
+  }
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // TRSM: panel K gates step K+1
   const WOp wq = w_split(q);
   constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
@@ -1010,9 +1017,9 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
         const int t = wv + WK * s;
         if (t >= TLO && t <= THI) {
           const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
-          const f32x4 rkj = pan_store(pcur + j * 256, lane, trsm_tile(wq, acc[s]));
+          const f32x4 rkj = pan_store(pcur + j * 256, lane, (GPK_KO & 1) ? acc[s] : trsm_tile(wq, acc[s]));
           // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
-          if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
+          if (!(GPK_KO & 32) && x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
         }
       });
     }
@@ -1038,7 +1045,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   worker_arrive(x);
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
   // deferred RBF of block row K+2 (its diagonal tile is handed over at step K+1)
-  if constexpr (K + 2 < NB) {
+  if constexpr (K + 2 < NB && !(GPK_KO & 8)) {
     constexpr int RLO = plan_P<NB>(K + 2), RHI = plan_P<NB>(K + 1) - 1;
     constexpr int SLO = RLO / WK;
     constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;

@@ -50,7 +50,14 @@ class ToyDeepGPHiddenLayer(nn.Module):
                                         batch_shape=batch_shape, ard_num_dims=None)
 
     def forward(self, x):
-        return self.variational_strategy(x)
+        """The layer's PRIOR at x, as reference DeepGP.py:51-54 returns it:
+        MultivariateNormal(mean_module(x), covar_module(x)). GPyTorch's VariationalStrategy
+        calls it on the inducing points for the prior; callers that call it directly get the
+        prior marginals here -- the mean and the kernel diagonal (outputscale); the full prior
+        covariance is not materialised on this path (q(f) comes from __call__)."""
+        mean_x = self.mean_module(x)
+        var_x = self.covar_module.outputscale.reshape(()).expand(mean_x.shape)
+        return MultivariateNormal(mean_x, var_x)
 
     def __call__(self, x, *other_inputs, **kwargs):
         """DeepGP.py:56-73 + DeepGPLayer.__call__ (upstream models/deep_gps/deep_gp.py).

@@ -214,8 +214,13 @@ class MultivariateNormal:
     @property
     def variance(self):
         if self._variance is None:
-            raise NotImplementedError("variance of an exact-GP prior is not materialised on this path")
-        var = self._variance
+            if self._exact is None:
+                raise NotImplementedError("this distribution carries no variance")
+            # exact-GP prior: diag K(x, x) = outputscale (the RBF is 1 on the diagonal), as
+            # GPyTorch's lazy kernel diagonal returns it
+            var = self._exact[2].reshape(()).expand(self._mean.shape)
+        else:
+            var = self._variance
         if self._added_noise is not None:
             var = var + self._added_noise
         min_var = settings.min_variance.value(var.dtype)
@@ -315,7 +320,9 @@ class GaussianLikelihood(nn.Module):
         gfx950 launch forward and one backward (gpk::gauss_ell) instead of ~10 elementwise
         kernels each way; the per-point form above stays GPyTorch's API."""
         mean, variance = input.mean, input.variance
-        if not (mean.is_cuda and mean.dtype == torch.float32 and variance.shape == mean.shape):
+        if not (mean.is_cuda and mean.dtype == torch.float32 and variance.shape == mean.shape
+                and self.noise.numel() == 1):
+            # (a batched noise model has one noise per batch entry: the unfused expression)
             return self.expected_log_prob(target, input).sum(-1)
         shape = mean.shape
         N = shape[-1]
@@ -454,6 +461,10 @@ class VariationalELBO(_ApproximateMarginalLogLikelihood):
         variational output of the kernels, one unbatched mean-field strategy. Same warnings as
         the unfused expression (the variance clamp flag)."""
         if not self.combine_terms or not isinstance(self.likelihood, GaussianLikelihood):
+            return None
+        # the fused op takes one scalar noise and returns no target gradient: a batched noise
+        # model or a target that requires grad takes the unfused path
+        if self.likelihood.noise.numel() != 1 or (torch.is_tensor(target) and target.requires_grad):
             return None
         mean, var = dist._mean, dist._variance
         if (var is None or dist._exact is not None or dist._added_noise is not None or not mean.is_cuda

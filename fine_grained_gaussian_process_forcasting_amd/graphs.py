@@ -40,6 +40,16 @@ replay condenses its verdicts into a device ring slot, so a block of ``check_eve
 replays is checked with ONE host sync and still warns once per replay, in order
 (``check_every`` > 1 keeps the replays back to back on the GPU).
 
+Cost and granularity of the rollback: the snapshot is one ``_foreach_copy_`` of every
+parameter and every optimizer-state tensor (≈ 3x the parameter bytes under Adam), issued
+once per check block, outside the graph. With ``check_every = k`` a failure restores the
+state from before the block's FIRST replay, so the successful replays that preceded the
+failing one inside the block are undone too (the eager loop would have kept them); pick
+``check_every = 1`` for eager-exact failure granularity, or a larger block for fewer host
+syncs and snapshots (``scripts/gp_step.py`` times the graphed step with ``check_every = 10``:
+its numbers include one snapshot per 10 replays). ``rollback=False`` skips the snapshot
+entirely: a failing block still raises, but leaves the parameters as the replays left them.
+
 The ``warmup`` eager steps that precede the capture are real
 training steps on the sample inputs (PyTorch's documented whole-network capture
 recipe). The package's factor caches are keyed on tensor version counters, which a
@@ -58,7 +68,7 @@ from .ops_autograd import invalidate_caches
 class GraphedStep:
     def __init__(self, loss_fn: Callable[..., object], optimizer: torch.optim.Optimizer,
                  sample_inputs: Sequence[torch.Tensor], warmup: int = 3, check_every: int = 1,
-                 loss_index: int = 0):
+                 loss_index: int = 0, rollback: bool = True):
         if not torch.cuda.is_available():
             raise RuntimeError("GraphedStep needs a ROCm device (HIP graphs); there is no CPU path")
         for t in sample_inputs:
@@ -75,6 +85,7 @@ class GraphedStep:
         self.optimizer = optimizer
         self.check_every = check_every
         self.loss_index = loss_index
+        self.rollback_enabled = rollback
         self.static_inputs = [t.detach().clone() for t in sample_inputs]
         self._n = 0
 
@@ -106,7 +117,7 @@ class GraphedStep:
             for v in optimizer.state.get(p, {}).values():
                 if isinstance(v, torch.Tensor) and v.is_cuda:
                     self._state.append(v)
-        self._backup = [t.detach().clone() for t in self._state]
+        self._backup = [t.detach().clone() for t in self._state] if rollback else None
         self._block_open = False
 
     def _loss(self, outputs) -> torch.Tensor:
@@ -138,7 +149,8 @@ class GraphedStep:
         if not self._block_open:
             # start of a check block: snapshot parameters + optimizer state (device copies,
             # stream-ordered before the replay) and clear the sticky failure flag
-            torch._foreach_copy_(self._backup, [t.detach() for t in self._state])
+            if self._backup is not None:
+                torch._foreach_copy_(self._backup, [t.detach() for t in self._state])
             self.checks.reset_sticky()
             self._block_open = True
         self.graph.replay()
@@ -156,6 +168,7 @@ class GraphedStep:
     def rollback(self) -> None:
         """Restore the parameters and optimizer state saved at the start of the current
         check block (called automatically when a replay's verdict raises)."""
-        with torch.no_grad():
-            torch._foreach_copy_([t.detach() for t in self._state], self._backup)
+        if self._backup is not None:
+            with torch.no_grad():
+                torch._foreach_copy_([t.detach() for t in self._state], self._backup)
         self._block_open = False

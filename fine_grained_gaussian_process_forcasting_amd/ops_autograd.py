@@ -89,6 +89,22 @@ class KzzCache:
         self._entry = entry
         return Linv
 
+    def note_consumers(self, *outputs):
+        """Mark the current grad-mode entry spent as soon as ANY backward pass reaches an
+        output computed from it -- also an ``autograd.grad`` over a subset of inputs that
+        stops short of the factor (the factor's own hook never fires then), so the next
+        forward refactors instead of reusing a factor whose consumers' graph was freed."""
+        e = self._entry
+        if e is None or not e["grad"]:
+            return
+
+        def _spent(g, entry=e):
+            entry["spent"] = True
+            return g
+        for t in outputs:
+            if isinstance(t, torch.Tensor) and t.requires_grad:
+                t.register_hook(_spent)
+
     def check_pending(self):
         """psd_safe_cholesky's verdict on a freshly computed factor (one host sync). Called
         after the first kernel that consumes the factor has been queued, so the GPU is
@@ -128,5 +144,6 @@ def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module
         key_tensors = (Z, s2, ls)
     Linv = cache.factor(Z, s2, ls, jitter, key_tensors)
     mean, var, flags, _ = torch.ops.gpk.variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, float(jitter))
+    cache.note_consumers(mean, var)
     cache.check_pending()
     return mean, var, flags

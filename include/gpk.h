@@ -185,7 +185,8 @@ int gpk_meanfield_kl_f32(const float* m, const float* s, int M, float* kl, const
  * Rows r of y / mean / var start at r * ld (ld >= N: a point slice of a joint output needs no
  * copy). clamp_flag (or NULL): set to 1 if any var_ri <= min_var (the kernel-clamped entries:
  * MultivariateNormal.variance's NumericalWarning). The backward (objective sum_r g_r elbo_r)
- * writes dmean, dvar (R, N contiguous), per-row d/dnoise partials and dm, ds (M).
+ * writes dmean, dvar (R, N contiguous), per-row d/dnoise partials and dm, ds (M). R = 0 is
+ * accepted by both (the forward writes nothing; the backward zero-fills dm and ds).
  *
  * Replaces (reference): DeepApproximateMLL(VariationalELBO(likelihood, model, num_data=d))
  * at forecast_denoising.py:86-89 (upstream mlls/variational_elbo.py +

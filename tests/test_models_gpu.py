@@ -199,6 +199,20 @@ def test_kzz_factor_shared_by_enc_and_dec_calls(cuda_device, monkeypatch):
         model.predict(dec)
         model.predict(enc[:2])
     assert calls["chol"] == 3
+    # a backward that stops short of the factor (autograd.grad w.r.t. the inputs only)
+    # still retires the entry: the next grad-mode forward refactors, and its full backward
+    # reaches a live K_ZZ node
+    model.train()
+    xg = enc.clone().requires_grad_(True)
+    with settings.num_likelihood_samples(1):
+        mx, _ = model.predict(xg)
+        (gx,) = torch.autograd.grad(mx.sum(), [xg])
+        assert calls["chol"] == 4 and gx.abs().sum() > 0
+        mx2, _ = model.predict(xg)
+    assert calls["chol"] == 5
+    model.zero_grad(set_to_none=True)
+    mx2.sum().backward()
+    assert vs.inducing_points.grad is not None and calls["adj"] == 2
 
 
 def test_concurrent_callers_match_serial(cuda_device):
