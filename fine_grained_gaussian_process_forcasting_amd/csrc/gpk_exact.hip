@@ -147,7 +147,7 @@ __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
   o.rw = o.rv + NB * 16;                 // working copy of -(y - c) (the RHS column)
   o.panel = o.rw + NB * 16;
   o.wbuf = o.panel + 2 * (NB + 1) * 256;  // (panel: double-buffered R rows)
-  o.dsc = o.wbuf + 2 * kWBuf;            // (wbuf: R_kk^{-T}, double-buffered by step parity)
+  o.dsc = o.wbuf + 3 * kWBuf;            // (wbuf: R_kk^{-T}, triple-buffered by step mod 3)
   o.hbuf = o.dsc + 256;                  // (dsc: the diagonal wave's working tile)
   // (hbuf: look-ahead hand-off {(k,k+1), (k+1,k+1)} x parity). The prologue's column
   // partials and means (64 W + 256 <= 1280 floats for W <= 16) alias dsc + hbuf: both are
@@ -155,7 +155,7 @@ __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
   o.cpart = o.dsc;
   o.rbfc = o.hbuf + 2 * 512;             // RbfK (16-byte aligned)
   o.red = o.rbfc + 4;
-  o.total = o.red + 4 * W + 40;
+  o.total = o.red + 4 * W + 96;          // flag words (see the kFlag enum)
   return o;
 }
 
@@ -187,11 +187,42 @@ GPK_DEVICE void barrier_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+#ifndef GPK_EXACT_COL
+#define GPK_EXACT_COL 0   // 1: column-ownership worker plan for N = 256 at 8 waves (worker_step_col)
+#endif
+#ifndef GPK_ZL_ORDER
+#define GPK_ZL_ORDER 0   // which block row's upper zeros a step writes (see worker_step_split)
+#endif
+#ifndef GPK_RBF_UPFRONT
+#define GPK_RBF_UPFRONT 0   // 1: every RBF tile in the prologue (0: block row k+2 deferred into step k)
+#endif
+#ifndef GPK_RHS_BATCH
+#define GPK_RHS_BATCH 0   // 1: the right-hand-side rows of a step as one batch of loads, then the MFMAs
+#endif
+#ifndef GPK_LDEFER
+#define GPK_LDEFER 0   // 1: the workers store their L tiles after the step arrive (read back from the panel)
+#endif
+static_assert(!GPK_LDEFER || GPK_SPLIT_UPDATE, "GPK_LDEFER reads the split panel planes");
+#ifndef GPK_LST_AUX
+#define GPK_LST_AUX 17   // L stores: -1 plain global stores; >= 0 buffer stores with this cache-policy aux
+                         // (17 = sc0 sc1: write-through, the lines leave L2 -- 64.5 -> 59.2 us per B=512 launch)
+#endif
+// One 16-byte store into a window's L (base = the window's L, wave-uniform).
+GPK_DEVICE void lstore(float* base, int off, const f32x4 v) {
+  if constexpr (GPK_LST_AUX < 0) {
+    *(f32x4*)&base[off] = v;
+  } else {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off * 4, 0, GPK_LST_AUX < 0 ? 0 : GPK_LST_AUX);
+  }
+}
+
 // FULL: N == 16 * NB (no padding) -- every row and column of every tile is real.
 template <bool FULL>
 GPK_DEVICE void store4(float* p, int N, int row, int colg, const f32x4 v) {
   if constexpr (FULL) {
-    *(f32x4*)&p[(size_t)row * N + colg] = v;
+    lstore(p, row * N + colg, v);
     return;
   }
   if (row >= N) return;
@@ -201,6 +232,23 @@ GPK_DEVICE void store4(float* p, int N, int row, int colg, const f32x4 v) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (colg + r < N) p[(size_t)row * N + colg + r] = v[r];
+  }
+}
+
+// Zero L's strictly-upper part of block row KZ (rows 16 KZ .. +15, columns >= 16 (KZ + 1)):
+// rows q = first, first + step, ... of the block by this wave, 16 B per lane.
+template <bool FULL>
+GPK_DEVICE void zero_l_block(float* Lb, int N, int KZ, int first, int step, int lane) {
+  const int c0 = 16 * (KZ + 1);
+  for (int q = first; q < 16; q += step) {
+    const int row = 16 * KZ + q;
+    if (row < N) {
+      if ((N & 3) == 0) {
+        for (int cc = c0 + 4 * lane; cc < N; cc += 256) lstore(Lb, row * N + cc, f32x4{0.f, 0.f, 0.f, 0.f});
+      } else {
+        for (int cc = c0 + lane; cc < N; cc += 64) Lb[(size_t)row * N + cc] = 0.f;
+      }
+    }
   }
 }
 
@@ -296,6 +344,11 @@ enum : int {
   kFlagTmo = 21,    // a spin wait ran out (safety net: the launch still drains)
   kFlagInvSigma = 30,
   kFlagGm2 = 31,
+  // column-ownership worker path (GPK_EXACT_COL): words 64.. (STAMPS builds use 24..39)
+  kFlagPan = 64,    // [64 + j]: panel tile R_{k,j} of the latest step k is out      (epoch)
+  kFlagZ = 80,      // z_k of the latest step k is out                               (epoch)
+  kFlagTrsm = 81,   // worker TRSM phases completed in this attempt (one add per wave per step)
+  kFlagBulk = 82,   // worker steps whose panel reads are all done (one add per wave per step)
 };
 
 // Poll an LDS flag until it reaches `target`. Every wait is bounded: after
@@ -417,6 +470,12 @@ GPK_DEVICE pan_op_t pan_load(const float* tile, int lane) { return load_split_hl
 GPK_DEVICE f32x4 pan_mma(const pan_op_t q, const float* ptile, int lane, f32x4 d) {
   return mma_tn_split(q, ptile, lane, d);
 }
+GPK_DEVICE f32x4 pan_mma_op(const pan_op_t q, const pan_op_t p_hl, f32x4 d) {   // d += Q^T P, both loaded
+  const half8_t p_lh = {p_hl[4], p_hl[5], p_hl[6], p_hl[7], p_hl[0], p_hl[1], p_hl[2], p_hl[3]};
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q, p_hl, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q, p_lh, d, 0, 0, 0);
+  return d;
+}
 GPK_DEVICE f32x4 pan_store(float* tile, int lane, const f32x4 v) {
   half4_t h, l;
   const f32x4 o = round_split_f16(v, h, l);
@@ -439,6 +498,7 @@ GPK_DEVICE f32x4 pan_store(float* tile, int lane, const f32x4 v) {
   return v;
 }
 GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) { return mma_tn(v, v, d); }
+GPK_DEVICE f32x4 pan_mma_op(const pan_op_t q, const pan_op_t p, f32x4 d) { return mma_tn(q, p, d); }
 #endif
 
 // Factor one 16x16 diagonal tile T in ONE wave (the diagonal wave).
@@ -587,19 +647,25 @@ GPK_DEVICE f32x4 rbf_tile(const float* smem, const RbfK& k, int i, int j, int la
     g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah2, bh2, g, 0, 0, 0);
     g = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah2, bl2, g, 0, 0, 0);
   }
-  const float gm2 = k.gm2, s2 = k.s2, diagval = k.diagval;
+  const float gm2 = k.gm2, ns2 = -k.s2, diagval = k.diagval;
   f32x4 o;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int row = 16 * i + 4 * grp + q;
     float dist = __builtin_fmaf(gm2, g[q], nr[q] + nc);
     dist = dist < 0.f ? 0.f : dist;  // clamp_min(0), NaN-propagating like torch
-    float v = s2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);
-    if (row == col) v = diagval;
-    if constexpr (!FULL) {
-      if (row >= N || col >= N) v = (row == col) ? 1.f : 0.f;
+    o[q] = ns2 * __builtin_amdgcn_exp2f(nhalf_log2e * dist);   // -K (accumulator sign)
+  }
+  if (i == j) {   // wave-uniform: only diagonal tiles pay for the diagonal / padding selects
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (16 * i + 4 * grp + q == col) o[q] = -diagval;
+  }
+  if constexpr (!FULL) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 16 * i + 4 * grp + q;
+      if (row >= N || col >= N) o[q] = (row == col) ? -1.f : 0.f;
     }
-    o[q] = -v;
   }
   return o;
 }
@@ -729,7 +795,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // served in order, and the diagonal wave completes its R_KK^{-T} and failure-word writes
   // before it releases the flag, so reads issued after a flag read that sees epoch K see
   // them too (all volatile: the compiler keeps the order). Otherwise: wait, re-read.
-  const float* wbk = x.wbuf + (K & 1) * kWBuf;
+  const float* wbk = x.wbuf + (K % 3) * kWBuf;
   const int flag_now = x.vflag[kFlagFact];
   int fail = x.vflag[kFlagFail + e0 / 32];
   f32x4 q = load_w_v(wbk, c, grp);
@@ -842,7 +908,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if (row < N) {
         if ((N & 3) == 0) {
           for (int cc = c0 + 4 * lane; cc < N; cc += 256)
-            *(f32x4*)&x.Lb[(size_t)row * N + cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+            lstore(x.Lb, row * N + cc, f32x4{0.f, 0.f, 0.f, 0.f});
         } else {
           for (int cc = c0 + lane; cc < N; cc += 64) x.Lb[(size_t)row * N + cc] = 0.f;
         }
@@ -850,7 +916,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     }
   }
   // deferred RBF of block row K+3 (its tiles are first read by step K+1's hand-over)
-  if constexpr (K + 3 < NB) {
+  if constexpr (K + 3 < NB && !GPK_RBF_UPFRONT) {
     constexpr int RLO = plan_P<NB>(K + 3), RHI = plan_P<NB>(K + 2) - 1;
     constexpr int SLO = RLO / WK;
     constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
@@ -932,7 +998,12 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     auto upd = [&](f32x4& d, auto I) {
       constexpr int s = decltype(I)::value;
       const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(wv + WK * s);
-      d = pan_mma(pan_load(pprev + (p & 255) * 256, lane), pprev + (p >> 8) * 256, lane, d);
+      if constexpr (GPK_KO & 128) {   // knockout: one LDS operand per tile update
+        const pan_op_t q = pan_load(pprev + (p & 255) * 256, lane);
+        d = pan_mma_op(q, q, d);
+      } else {
+        d = pan_mma(pan_load(pprev + (p & 255) * 256, lane), pprev + (p >> 8) * 256, lane, d);
+      }
     };
     constexpr int Pkm1 = plan_P<NB>(K - 1);
     constexpr int NALL = Pkm1 / WK;
@@ -953,32 +1024,45 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
 #if GPK_EXACT_PRIO_RHS
   __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // zero-L + right-hand side lead into the TRSM
 #endif
-  // zero L's strictly-upper part of block-row K (streams out behind the MFMAs)
+  // zero L's strictly-upper part of one block row (streams out behind the MFMAs): block row K
+  // (GPK_ZL_ORDER 0), or NB-2-K (1: the zero runs grow as the TRSM row shrinks, so every step
+  // writes the same number of L bytes; measured no faster)
   if (!(GPK_KO & 4) && x.Lb != nullptr) {
-    const int N = FULL ? 16 * NB : x.N;
-    const int c0 = 16 * (K + 1);
-    for (int q = wv; q < 16; q += WK) {
-      const int row = 16 * K + q;
-      if (row < N) {
-        if ((N & 3) == 0) {
-          for (int cc = c0 + 4 * lane; cc < N; cc += 256)
-            *(f32x4*)&x.Lb[(size_t)row * N + cc] = f32x4{0.f, 0.f, 0.f, 0.f};
-        } else {
-          for (int cc = c0 + lane; cc < N; cc += 64) x.Lb[(size_t)row * N + cc] = 0.f;
-        }
-      }
-    }
+    constexpr int KZ = GPK_ZL_ORDER == 1 ? NB - 2 - K : K;
+    if constexpr (KZ >= 0) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, KZ, wv, WK, lane);
   }
   // right-hand side, block rows i >= K owned by this wave: rw_i += R_{K-1,i}^T z_{K-1}
   // (rw holds -(y - c); only column 0 of the tile is live, so it round-trips
   // through LDS on the c == 0 lanes)
   const int rfirst = K + (((wv - K) % WK) + WK) % WK;
-  if constexpr (K > 0 && !(GPK_KO & 2)) {
+  if constexpr (K > 0 && !(GPK_KO & 2) && !GPK_RHS_BATCH) {
     for (int i = rfirst; i < NB; i += WK) {
       f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
       d = pan_mma(pan_load(pprev + i * 256, lane), pprev + NB * 256, lane, d);
       if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
+    }
+  }
+  if constexpr (K > 0 && !(GPK_KO & 2) && GPK_RHS_BATCH) {
+    // this wave's rows i = rfirst + u WK < NB (at most UM of them): every LDS operand is
+    // requested before the first MFMA, so the rows cost one round trip, not one each
+    constexpr int UM = (NB - K + WK - 1) / WK;
+    const pan_op_t zk = pan_load(pprev + NB * 256, lane);
+    f32x4 d[UM];
+    pan_op_t pr[UM];
+#pragma unroll
+    for (int u = 0; u < UM; ++u) {
+      const int i = rfirst + u * WK;
+      const int ic = i < NB ? i : NB - 1;
+      d[u] = *(const f32x4*)&x.rw[16 * ic + 4 * grp];
+      pr[u] = pan_load(pprev + ic * 256, lane);
+    }
+#pragma unroll
+    for (int u = 0; u < UM; ++u) {
+      const int i = rfirst + u * WK;
+      if (c != 0) d[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      d[u] = pan_mma_op(pr[u], zk, d[u]);
+      if (c == 0 && i < NB) *(f32x4*)&x.rw[16 * i + 4 * grp] = d[u];
     }
   }
   GPK_WSTAMP(6, 2)  // right-hand side
@@ -989,7 +1073,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // served in order, and the diagonal wave completes its R_KK^{-T} and failure-word writes
   // before it releases the flag, so reads issued after a flag read that sees epoch K see
   // them too (all volatile: the compiler keeps the order). Otherwise: wait, re-read.
-  const float* wbk = x.wbuf + (K & 1) * kWBuf;
+  const float* wbk = x.wbuf + (K % 3) * kWBuf;
   const int flag_now = x.vflag[kFlagFact];
   int fail = x.vflag[kFlagFail + e0 / 32];
   f32x4 q = load_w_v(wbk, c, grp);
@@ -1019,7 +1103,8 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
           const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
           const f32x4 rkj = pan_store(pcur + j * 256, lane, (GPK_KO & 1) ? acc[s] : trsm_tile(wq, acc[s]));
           // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
-          if (!(GPK_KO & 32) && x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
+          if (!GPK_LDEFER && !(GPK_KO & 32) && x.Lb != nullptr)
+            store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
         }
       });
     }
@@ -1044,8 +1129,28 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // does not depend on the other waves (zero-L, deferred RBF) before waiting on it
   worker_arrive(x);
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
+  if constexpr (GPK_LDEFER) {
+    // the L stores of this wave's panel-K tiles, after the arrive: read back from the panel
+    // (hi + lo is exactly the rounded R_Kj), so no store sits inside the TRSM phase
+    if (x.Lb != nullptr && THI >= TLO) {
+      static_for_range<SLO, SHI>([&](auto I) {
+        constexpr int s = decltype(I)::value;
+        const int t = wv + WK * s;
+        if (t >= TLO && t <= THI) {
+          const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
+          const float* tile = pcur + j * 256;
+          const half4_t h = *(const half4_t*)&tile[2 * lane];
+          const half4_t l = *(const half4_t*)&tile[128 + 2 * lane];
+          f32x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = ((float)h[r] + (float)l[r]) * inv_sigma;
+          store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, v);
+        }
+      });
+    }
+  }
   // deferred RBF of block row K+2 (its diagonal tile is handed over at step K+1)
-  if constexpr (K + 2 < NB && !(GPK_KO & 8)) {
+  if constexpr (K + 2 < NB && !(GPK_KO & 8) && !GPK_RBF_UPFRONT) {
     constexpr int RLO = plan_P<NB>(K + 2), RHI = plan_P<NB>(K + 1) - 1;
     constexpr int SLO = RLO / WK;
     constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
@@ -1065,15 +1170,295 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Column-ownership worker plan (GPK_EXACT_COL: NB = 16 with 7 worker waves, the headline
+// N = 256 shape). Worker w owns the block columns A = 15 - w and B = w + 1 of the upper
+// triangle (16 - w + w + 2 = 18 tiles for every wave) plus rows {w, w + 7} <= 8 of the
+// middle column 8. Slots: (i, A) -> i, (i, B) -> 17 - i, (w, 8) -> 18, (w + 7, 8) -> 19, so
+// the tiles of one block row sit in COMPILE-TIME slots (guarded by wave-uniform compares)
+// and a column's panel tile R_{k-1,j} -- the P operand of every update of column j -- is
+// read from LDS once per step instead of once per tile. Per step the workers synchronise
+// through per-column panel flags (kFlagPan + j), the z flag and two monotone counters
+// (TRSM phases done / panel reads done) instead of a workgroup-wide step barrier:
+//   1. hand-over HO_K: (K, K+1) and (K+1, K+1) through panel K-1, by the owner of column
+//      K+1, as soon as R_{K-1,K} is out;
+//   2. the other tiles of block row K through panel K-1 (this step's TRSM inputs);
+//   3. right-hand side row K (owner of column K);
+//   4. TRSM of row K with R_KK^{-T} (+ z_K): panel K, flags; the panel buffer is reused
+//      only once every wave has finished reading panel K-2 (kFlagBulk);
+//   5. the rest of the trailing update through panel K-1 once panel K-1 is complete
+//      (kFlagTrsm), one P load per column;
+//   6. right-hand side rows > K of the owned columns; count the panel reads done;
+//   7. deferred RBF of block row K+2, zero-L.
+// ---------------------------------------------------------------------------
+constexpr int kColSlots = 20;
+
+template <int K>
+struct ColOwners {
+  // owner (wave) of block column j's HO / RHS duties
+  static constexpr int col_owner(int j) { return j >= 9 ? 15 - j : (j >= 1 && j <= 7 ? j - 1 : (j == 8 ? 1 : 0)); }
+};
+
+GPK_DEVICE f32x4 pan_mma2(const pan_op_t q, const pan_op_t p_hl, const pan_op_t p_lh, f32x4 d) {
+#if GPK_SPLIT_UPDATE
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q, p_hl, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q, p_lh, d, 0, 0, 0);
+  return d;
+#else
+  (void)p_lh;
+  return mma_tn(q, p_hl, d);
+#endif
+}
+GPK_DEVICE pan_op_t pan_swap(const pan_op_t p) {
+#if GPK_SPLIT_UPDATE
+  return pan_op_t{p[4], p[5], p[6], p[7], p[0], p[1], p[2], p[3]};
+#else
+  return p;
+#endif
+}
+
+GPK_DEVICE void count_in(WorkerCtx& x, int idx) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (x.lane == 0)
+    (void)__atomic_fetch_add((__attribute__((address_space(3))) int*)&x.vflag[idx], 1, __ATOMIC_RELAXED);
+}
+
 template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL>
+GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
+  static_assert(NB == 16 && WK == 7 && SLOTS == kColSlots, "column plan: NB = 16, 7 workers");
+  const int wv = launder_s(x.wv);
+  const int e0 = launder_s(x.epoch0);
+  int lane = x.lane;
+  asm volatile("" : "+v"(lane));
+  const int c = lane & 15, grp = lane >> 4;
+  const int jA = 15 - wv, jB = wv + 1;
+  const float* pprev = x.panel + ((K + 1) & 1) * (NB + 1) * 256;   // panel K-1
+  float* pcur = x.panel + (K & 1) * (NB + 1) * 256;                // panel K
+  float* hA = x.hbuf + (K & 1) * 512;
+  constexpr int OWN_K = ColOwners<K>::col_owner(K);                 // RHS row K, column K
+  if constexpr (ST) {
+    if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8] = __builtin_amdgcn_s_memtime();
+  }
+  auto upd = [&](f32x4& d, const float* qt, const pan_op_t p_hl, const pan_op_t p_lh) {
+    d = pan_mma2(pan_load(qt, lane), p_hl, p_lh, d);
+  };
+  // ---- 1. hand-over HO_K = (K, K+1), (K+1, K+1) through panel K-1
+  if constexpr (K > 0 && K + 1 < NB) {
+    constexpr int HAW = K <= 6 ? K : (K == 7 ? 0 : 14 - K);   // owner of (K, K+1)
+    constexpr int HBW = K <= 6 ? K : (K == 7 ? 1 : 14 - K);   // owner of (K+1, K+1)
+    constexpr int SA = K <= 6 ? 17 - K : (K == 7 ? 19 : K);
+    constexpr int SB = K <= 6 ? 16 - K : (K == 7 ? 19 : K + 1);
+    if (wv == HAW || wv == HBW) {
+      if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);
+      spin_until(x.vflag, kFlagPan + K + 1, e0 + K - 1);
+      const pan_op_t p = pan_load(pprev + (K + 1) * 256, lane);
+      const pan_op_t pl = pan_swap(p);
+      if (wv == HAW) {
+        spin_until(x.vflag, kFlagPan + K, e0 + K - 1);
+        upd(acc[SA], pprev + K * 256, p, pl);
+        publish_tile(hA, lane, acc[SA], x.vflag, kFlagHA, e0 + K);
+      }
+      if (wv == HBW) {
+        acc[SB] = pan_mma2(p, p, pl, acc[SB]);
+        publish_tile(hA + 256, lane, acc[SB], x.vflag, kFlagHB, e0 + K);
+      }
+      if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  // ---- 2. the other tiles of row K (K, j), j >= K+2, through panel K-1
+  if constexpr (K > 0) {
+    const bool a_row = (K + 2 <= jA);                 // (K, A), A >= K+2
+    const bool b_row = (K + 2 <= jB);                 // (K, B)
+    constexpr bool C8 = (K + 2 <= 8);                 // (K, 8): slot 18 of wave K (K <= 6)
+    const bool c_row = C8 && (wv == K);
+    if (a_row || b_row || c_row) {
+      spin_until(x.vflag, kFlagPan + K, e0 + K - 1);
+      if (c_row) spin_until(x.vflag, kFlagPan + 8, e0 + K - 1);
+      const float* qt = pprev + K * 256;
+      if (a_row) {
+        const pan_op_t p = pan_load(pprev + jA * 256, lane);
+        upd(acc[K], qt, p, pan_swap(p));
+      }
+      if constexpr (17 - K >= 0 && 17 - K < 18) {
+        if (b_row) {
+          const pan_op_t p = pan_load(pprev + jB * 256, lane);
+          upd(acc[17 - K], qt, p, pan_swap(p));
+        }
+      }
+      if constexpr (C8) {
+        if (c_row) {
+          const pan_op_t p = pan_load(pprev + 8 * 256, lane);
+          upd(acc[18], qt, p, pan_swap(p));
+        }
+      }
+    }
+  }
+  // ---- 3. right-hand side row K: rw_K += R_{K-1,K}^T z_{K-1} (owner of column K)
+  if constexpr (K > 0) {
+    if (wv == OWN_K) {
+      spin_until(x.vflag, kFlagZ, e0 + K - 1);
+      if constexpr (K == 8) spin_until(x.vflag, kFlagPan + 8, e0 + K - 1);
+      f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
+      if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+      d = pan_mma(pan_load(pprev + K * 256, lane), pprev + NB * 256, lane, d);
+      if (c == 0) *(f32x4*)&x.rw[16 * K + 4 * grp] = d;
+    }
+  }
+  GPK_WSTAMP(6, 2)  // hand-over + row K + RHS row K
+  // ---- 4. TRSM of row K with R_KK^{-T} (panel K) and z_K
+  const float* wbk = x.wbuf + (K % 3) * kWBuf;
+  const int flag_now = x.vflag[kFlagFact];
+  int fail = x.vflag[kFlagFail + e0 / 32];
+  f32x4 q = load_w_v(wbk, c, grp);
+  const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
+  if (flag_now < e0 + K) {
+    spin_until(x.vflag, kFlagFact, e0 + K);
+    fail = x.vflag[kFlagFail + e0 / 32];
+    q = load_w_v(wbk, c, grp);
+  }
+  GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
+  if (GPK_KO == 0 && fail != 0) return 1;
+  if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);
+  // panel buffer K & 1 held panel K-2 (read in step K-1): every wave must be past step K-1's
+  // panel reads (one kFlagBulk add per wave per step)
+  if constexpr (K >= 2) spin_until(x.vflag, kFlagBulk, WK * K);
+  {
+    const WOp wq = w_split(q);
+    const bool a_t = (K + 1 <= jA), b_t = (K + 1 <= jB);
+    if (a_t) {
+      const f32x4 r = pan_store(pcur + jA * 256, lane, trsm_tile(wq, acc[K]));
+      if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * jA + c, 16 * K + 4 * grp, r * inv_sigma);
+    }
+    if constexpr (17 - K >= 0 && 17 - K < 18) {
+      if (b_t) {
+        const f32x4 r = pan_store(pcur + jB * 256, lane, trsm_tile(wq, acc[17 - K]));
+        if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * jB + c, 16 * K + 4 * grp, r * inv_sigma);
+      }
+    }
+    constexpr int C8S = K <= 6 ? 18 : (K == 7 ? 19 : -1);      // (K, 8): wave K slot 18, or wave 0 slot 19
+    constexpr int C8W = K <= 6 ? K : 0;
+    if constexpr (C8S >= 0) {
+      if (wv == C8W) {
+        const f32x4 r = pan_store(pcur + 8 * 256, lane, trsm_tile(wq, acc[C8S]));
+        if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * 8 + c, 16 * K + 4 * grp, r * inv_sigma);
+      }
+    }
+    if (wv == OWN_K) {   // z_K = R_KK^{-T} rw_K
+      f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
+      if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 zk = pan_store(pcur + NB * 256, lane, trsm_tile_f32(q, d));   // (y unbounded: fp32)
+      if (c == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
+        if (x.zout != nullptr) {
+          const int row = 16 * K + 4 * grp;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (FULL || row + r < x.N) x.zout[(size_t)x.b * x.N + row + r] = zk[r];
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (x.lane == 0) {
+      if (a_t) x.vflag[kFlagPan + jA] = e0 + K;
+      if (b_t) x.vflag[kFlagPan + jB] = e0 + K;
+      if constexpr (C8S >= 0) {
+        if (wv == C8W) x.vflag[kFlagPan + 8] = e0 + K;
+      }
+      if (wv == OWN_K) x.vflag[kFlagZ] = e0 + K;
+    }
+    count_in(x, kFlagTrsm);
+  }
+  if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
+  GPK_WSTAMP(4, 5)  // TRSM
+  if constexpr (K + 1 == NB) return 0;
+  // ---- 5. the rest of the trailing update through panel K-1: rows K+1 .. of the owned columns
+  if constexpr (K > 0) {
+    spin_until(x.vflag, kFlagTrsm, WK * K);   // panel K-1 complete
+    // column A (rows K+1 .. jA; (K+1, K+1) is HB: done)
+    if (K + 1 <= jA) {
+      const pan_op_t p = pan_load(pprev + jA * 256, lane);
+      const pan_op_t pl = pan_swap(p);
+      static_for_range<K + 1, 15>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if (i <= jA && !(i == K + 1 && jA == K + 1)) upd(acc[i], pprev + i * 256, p, pl);
+      });
+    }
+    // column B (rows K+1 .. jB <= 7)
+    if constexpr (K + 1 <= 7) {
+      if (K + 1 <= jB) {
+        const pan_op_t p = pan_load(pprev + jB * 256, lane);
+        const pan_op_t pl = pan_swap(p);
+        static_for_range<K + 1, 7>([&](auto I) {
+          constexpr int i = decltype(I)::value;
+          if (i <= jB && !(i == K + 1 && jB == K + 1)) upd(acc[17 - i], pprev + i * 256, p, pl);
+        });
+      }
+    }
+    // column 8: (w, 8) slot 18 and (w + 7, 8) slot 19
+    if constexpr (K + 1 <= 8) {
+      const bool s18 = (wv >= K + 1);                             // row w <= 6 < 8
+      const bool s19 = (wv <= 1) && (wv + 7 >= K + 1) && !(wv + 7 == 8 && K + 1 == 8);
+      if (s18 || s19) {
+        const pan_op_t p = pan_load(pprev + 8 * 256, lane);
+        const pan_op_t pl = pan_swap(p);
+        if (s18) upd(acc[18], pprev + wv * 256, p, pl);
+        if (s19) upd(acc[19], pprev + (wv + 7) * 256, p, pl);
+      }
+    }
+    GPK_WSTAMP(2, 1)  // trailing update
+    // ---- 6. right-hand side rows > K of the owned columns: rw_j += R_{K-1,j}^T z_{K-1}
+    auto rhs = [&](int j) {
+      f32x4 d = *(const f32x4*)&x.rw[16 * j + 4 * grp];
+      if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+      d = pan_mma(pan_load(pprev + j * 256, lane), pprev + NB * 256, lane, d);
+      if (c == 0) *(f32x4*)&x.rw[16 * j + 4 * grp] = d;
+    };
+    spin_until(x.vflag, kFlagZ, e0 + K - 1);
+    if (K + 1 <= jA) rhs(jA);
+    if (K + 1 <= jB) rhs(jB);
+    if constexpr (K + 1 <= 8) {
+      if (wv == 1) rhs(8);
+    }
+  }
+  count_in(x, kFlagBulk);   // this wave is done reading panel K-1
+  GPK_WSTAMP(5, 6)
+  // ---- 7. deferred RBF of block row K+2 and L's upper zeros
+  if constexpr (K + 2 < NB && !GPK_RBF_UPFRONT) {
+    constexpr int R = K + 2;
+    const RbfK rk = read_rbfk(x.smem + x.rbfc);
+    if (R <= jA) acc[R] += rbf_tile<NB, FULL>(x.smem, rk, R, jA, lane, x.N);
+    if constexpr (17 - R >= 0 && R <= 7) {
+      if (R <= jB) acc[17 - R] += rbf_tile<NB, FULL>(x.smem, rk, R, jB, lane, x.N);
+    }
+    if constexpr (R <= 6) {
+      if (wv == R) acc[18] += rbf_tile<NB, FULL>(x.smem, rk, R, 8, lane, x.N);
+    }
+    if constexpr (R == 7 || R == 8) {
+      if (wv == R - 7) acc[19] += rbf_tile<NB, FULL>(x.smem, rk, R, 8, lane, x.N);
+    }
+  }
+  if (x.Lb != nullptr) {
+    constexpr int KZ = GPK_ZL_ORDER == 1 ? NB - 2 - K : K;
+    if constexpr (KZ >= 0 && KZ + 1 < NB) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, KZ, wv, WK, lane);
+  }
+  GPK_WSTAMP(3, 3)  // RBF + zero-L
+  return 0;
+}
+
+template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL, bool COL>
 GPK_DEVICE int worker_steps(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   if constexpr (K < NB) {
+    if constexpr (COL) {
+      if (worker_step_col<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
+    } else {
 #if GPK_EXACT_FLOW
-    if (worker_step<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
+      if (worker_step<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
 #else
-    if (worker_step_split<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
+      if (worker_step_split<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
 #endif
-    return worker_steps<NB, WK, SLOTS, K + 1, ST, FULL>(acc, x);
+    }
+    return worker_steps<NB, WK, SLOTS, K + 1, ST, FULL, COL>(acc, x);
   } else {
     return 0;
   }
@@ -1092,7 +1477,8 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   constexpr int NT = ExactPlan<NB>::NT;
   const int N = FULL ? 16 * NB : N_in;  // FULL: no padded rows anywhere
   constexpr int WK = W - 1;                  // worker waves; wave WK is the diagonal wave
-  constexpr int SLOTS = (NT + WK - 1) / WK;
+  constexpr bool COL = GPK_EXACT_COL && NB == 16 && WK == 7;   // column-ownership worker plan
+  constexpr int SLOTS = COL ? kColSlots : (NT + WK - 1) / WK;
   constexpr int T = 64 * W;
   // Diagnostic-only phase clocks (STAMPS build): wave 0 lane 0 of each workgroup.
   unsigned long long st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0, st_t0 = 0, st_rt0 = 0;
@@ -1243,6 +1629,9 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       flag[kFlagHB] = -1;
       flag[kFlagSync] = 0;
       flag[kFlagTmo] = 0;
+      for (int qq = kFlagPan; qq <= kFlagZ; ++qq) flag[qq] = -1;
+      flag[kFlagTrsm] = 0;
+      flag[kFlagBulk] = 0;
       flag[kFlagInvSigma] = __builtin_bit_cast(int, inv_sigma);
       smem[lay.rbfc + 1] = s2;
       ((int*)smem)[lay.rbfc + 3] = lay.nrm | (((DC + 1) / 2) << 20);
@@ -1378,6 +1767,9 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       flag[kFlagHB] = -1;
       flag[kFlagSync] = 0;
       flag[kFlagTmo] = 0;
+      for (int qq = kFlagPan; qq <= kFlagZ; ++qq) flag[qq] = -1;
+      flag[kFlagTrsm] = 0;
+      flag[kFlagBulk] = 0;
       flag[kFlagInvSigma] = __builtin_bit_cast(int, inv_sigma);  // read back per step (SGPR budget)
       smem[lay.rbfc + 1] = s2;
       ((int*)smem)[lay.rbfc + 3] = lay.nrm | (((DC + 1) / 2) << 20);
@@ -1501,7 +1893,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       spin_until(vflag, kFlagT00, 32 * attempt);
       for (int k = 0; k < NB; ++k) {
         const int epoch = 32 * attempt + k;
-        float* wb = wbuf + (k & 1) * kWBuf;
+        float* wb = wbuf + (k % 3) * kWBuf;
         unsigned long long dt0 = 0;
         if constexpr (STAMPS) {
           dt0 = __builtin_amdgcn_s_memtime();
@@ -1578,9 +1970,20 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         diagval = diagval + (float)(jn - jit_prev) * sigma2;
         jit_prev = jn;
       }
-      // right-hand side: this wave's block rows of rw <- -(y - c) (fresh per attempt)
-      for (int i = wave; i < NB; i += WK)
-        if (lane < 16) rw[16 * i + lane] = -rv[16 * i + lane];
+      // right-hand side: this wave's block rows of rw <- -(y - c) (fresh per attempt); in the
+      // column plan each row is initialised by the wave that owns it (columns A, B; 8: wave 1)
+      if constexpr (COL) {
+        const int wv = launder_s(wave);
+        if (lane < 16) {
+          rw[16 * (15 - wv) + lane] = -rv[16 * (15 - wv) + lane];
+          rw[16 * (wv + 1) + lane] = -rv[16 * (wv + 1) + lane];
+          if (wv == 1) rw[16 * 8 + lane] = -rv[16 * 8 + lane];
+          if (wv == 0) rw[lane] = -rv[lane];
+        }
+      } else {
+        for (int i = wave; i < NB; i += WK)
+          if (lane < 16) rw[16 * i + lane] = -rv[16 * i + lane];
+      }
       // ---- 4. RBF of block rows 0-2 (the rest is deferred into the
       // factorisation steps); the owners of (0,0), (0,1), (1,1) build and hand
       // those over first, so the diagonal wave starts right away.
@@ -1591,10 +1994,31 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         if (lane == 0) *(__attribute__((address_space(3))) volatile float*)&smem[lay.rbfc + 2] = diagval;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         const RbfK rk = read_rbfk(smem + lay.rbfc);
+        if constexpr (COL) {
+          // (0,0) is built by wave 6 and handed over (column 0 has no worker); (0,1), (1,1) --
+          // column 1 = B of wave 0 -- first, then rows 0-1 of every owned column
+          const int e0 = 32 * attempt;
+          const int jA = 15 - wv, jB = wv + 1;
+          if (wv == 6) {
+            const f32x4 t00 = rbf_tile<NB, FULL>(smem, rk, 0, 0, lane, N);
+            publish_tile(dsc, lane, t00, vflag, kFlagT00, e0);
+          }
+          acc[17] = rbf_tile<NB, FULL>(smem, rk, 0, jB, lane, N);
+          acc[16] = rbf_tile<NB, FULL>(smem, rk, 1, jB, lane, N);
+          if (wv == 0) {
+            publish_tile(hbuf, lane, acc[17], vflag, kFlagHA, e0);
+            publish_tile(hbuf + 256, lane, acc[16], vflag, kFlagHB, e0);
+          }
+          acc[0] = rbf_tile<NB, FULL>(smem, rk, 0, jA, lane, N);
+          acc[1] = rbf_tile<NB, FULL>(smem, rk, 1, jA, lane, N);
+          acc[18] = wv <= 1 ? rbf_tile<NB, FULL>(smem, rk, wv, 8, lane, N) : f32x4{0.f, 0.f, 0.f, 0.f};
+          static_for_range<2, 15>([&](auto I) { acc[decltype(I)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
+          acc[19] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
         constexpr int P0 = plan_P<NB>(0);
         constexpr int P1 = NB > 1 ? plan_P<NB>(1) : 0;
         // rows 0-2 now and row k+3 at step k (FLOW), rows 0-1 and row k+2 (split order)
-        constexpr int P2 = GPK_EXACT_FLOW ? (NB > 2 ? plan_P<NB>(2) : 0) : P1;
+        constexpr int P2 = GPK_RBF_UPFRONT ? 0 : (GPK_EXACT_FLOW ? (NB > 2 ? plan_P<NB>(2) : 0) : P1);
         constexpr int T01 = P0 + 1;
         const int e0 = 32 * attempt;
         if (wv == P0 % WK) {
@@ -1629,6 +2053,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
             }
           }
         });
+        }
       }
       GPK_STAMP(1)
       wx.epoch0 = 32 * attempt;
@@ -1637,12 +2062,19 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         wx.st = wst;
         wst[8] = st_last;
       }
-      failed = worker_steps<NB, WK, SLOTS, 0, STAMPS, FULL>(acc, wx);
+      failed = worker_steps<NB, WK, SLOTS, 0, STAMPS, FULL, COL>(acc, wx);
       if constexpr (STAMPS) st_last = wst[8];
       sumz2 = wx.sumz2;
       if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
       // every worker has left the failed attempt before anyone rebuilds
       worker_sync<WK>(wx);
+      if constexpr (COL) {   // the column plan's per-attempt counters restart from 0
+        if (wave == 0 && lane == 0) {
+          vflag[kFlagTrsm] = 0;
+          vflag[kFlagBulk] = 0;
+        }
+        worker_sync<WK>(wx);
+      }
     }
     if constexpr (STAMPS) {
       for (int q = 2; q < 8; ++q) st_acc[q] += wst[q];
@@ -1745,8 +2177,8 @@ int gpk_launch_exact(const GpkExactArgs& a, hipStream_t stream) {
   const int NB = (a.N + 15) / 16;
   switch (NB) {
 #define GPK_CASE(nb) case nb: return launch_exact_any<nb>(a, stream);
-#if GPK_EXACT_DEV  // development A/B builds: the N=256 instantiation only (fast compile)
-    GPK_CASE(16)
+#if GPK_EXACT_DEV  // development A/B builds: the N=128 / N=256 instantiations only (fast compile)
+    GPK_CASE(8) GPK_CASE(16)
 #else
     GPK_CASE(1) GPK_CASE(2) GPK_CASE(3) GPK_CASE(4) GPK_CASE(5) GPK_CASE(6)
     GPK_CASE(7) GPK_CASE(8) GPK_CASE(9) GPK_CASE(10) GPK_CASE(11) GPK_CASE(12)

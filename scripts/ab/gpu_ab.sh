@@ -1,0 +1,13 @@
+#!/bin/bash
+# time (and with a trailing '+' in the name: stamp) every _lib_ab/<name> given
+set -o pipefail
+R="$GRAFT_REPO_ROOT"; cd "$R"; O=gpurun_out/ab; mkdir -p $O
+for spec in "$@"; do
+  v=${spec%+}
+  export GPK_LIB=$R/fine_grained_gaussian_process_forcasting_amd/_lib_ab/$v/libgpk.so
+  timeout -k 10 150 python scripts/ab/ko_time.py >> $O/ab.jsonl 2> $O/err_$v.log || { echo "$v FAILED"; tail -20 $O/err_$v.log; exit 1; }
+  tail -1 $O/ab.jsonl
+  if [ "$spec" != "$v" ]; then
+    timeout -k 10 150 python scripts/stamps_exact.py 512 > $O/tl_$v.txt 2>&1 || { echo "$v STAMPS FAILED"; tail -20 $O/tl_$v.txt; exit 2; }
+  fi
+done

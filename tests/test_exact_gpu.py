@@ -205,3 +205,40 @@ def test_exact_cfg2_full_batch(cuda_device):
     assert _rel_fro(out.L.cpu().double().numpy(), ref.L).max() <= 1e-4
     mll = out.mll.cpu().double().numpy()
     assert np.max(np.abs(mll - ref.mll) / np.abs(ref.mll)) <= 1e-4
+
+
+def test_exact_two_windows_per_cu_layout_ladder_and_failures(cuda_device):
+    """B > CUs selects the two-windows-per-CU layout (8 waves per window, the headline's):
+    a batch mixing singular windows (duplicate points, zero noise: the fp32 jitter ladder
+    restarts them in-kernel), a NaN window (info > 0) and regular windows. Checks every
+    window's info code, the regular windows against the fp64 oracle and the laddered ones'
+    factor against K + jitter I -- the restart path of that layout's worker protocol."""
+    B, N, D = 320, 256, 8
+    X, y = _inputs(B, N, D, seed=21)
+    dup = [3, 100, 257]
+    for b in dup:
+        X[b] = X[b, :1].expand(N, D)       # all points equal: K = s2 * ones, singular
+    X[50, 7, 2] = float("nan")
+    noise, ls = 0.0, 0.3             # regular windows: K close to I, no jitter needed
+    out = _run(cuda_device, X, y, ls, 1.0, 0.0, noise)
+    info = out.info.cpu().numpy()
+    for b in dup:
+        assert info[b] < 0, (b, info[b])
+    assert info[50] > 0
+    good = [b for b in range(B) if b not in dup and b != 50]
+    assert (info[good] <= 0).all()
+    sel = good[::29] + [B - 1]
+    ref = O.exact_mll(X[sel].double().numpy(), y[sel].double().numpy(), ls, 1.0, 0.0, noise,
+                      raise_on_fail=False)
+    ok = [i for i, b in enumerate(sel) if info[b] == 0 and ref.info[i] == 0]
+    assert len(ok) == len(sel)
+    L = out.L.cpu().double().numpy()
+    assert _rel_fro(L[[sel[i] for i in ok]], ref.L[ok]).max() <= 1e-4
+    mll = out.mll.cpu().double().numpy()[[sel[i] for i in ok]]
+    assert np.max(np.abs(mll - ref.mll[ok]) / np.abs(ref.mll[ok])) <= 1e-4
+    for b in dup:
+        t = -int(info[b])
+        jit = 1e-6 * 10 ** (t - 1)
+        K = np.ones((N, N)) + jit * np.eye(N)
+        err = np.linalg.norm(L[b] @ L[b].T - K) / np.linalg.norm(K)
+        assert err <= 1e-5, (b, t, err)
