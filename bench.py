@@ -312,6 +312,25 @@ def elbo_rel_err(X, y, Z, ls, w, vm, vs, ell_gpu, num_data, n=32):
     return float(np.max(np.abs(got - want) / np.abs(want)))
 
 
+def variant_leg(name, B, N, D, steps):
+    """Kernel time of a measurement-only variant build of the exact kernel (build_native.VARIANTS)
+    on the headline shape, timed in a child process that loads that build (GPK_LIB)."""
+    import subprocess
+    lib = os.path.join(ROOT, "fine_grained_gaussian_process_forcasting_amd", "_lib_variants", name, "libgpk.so")
+    if not os.path.exists(lib):
+        return {"error": f"variant build {name} not present (build_native.build_variant)"}
+    env = dict(os.environ, GPK_LIB=lib)
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "time_exact.py"), str(B), str(N), str(D),
+                            str(steps)], env=env, capture_output=True, text=True, timeout=300)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"error": (r.stderr or r.stdout)[-400:]}
+        return json.loads(lines[-1])
+    except Exception as e:  # a side leg never takes the headline line down
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def e2e_leg(steps=10):
     """the cfg-3 forecast -> GP blur -> denoise train step (b=256, enc 192 /
     dec 96, d 32, M 256), eager (the reference's loop) and HIP-graph captured
@@ -347,6 +366,8 @@ def main():
     ap.add_argument("--no-grad", action="store_true", help="skip the backward side measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end train-step side leg")
     ap.add_argument("--no-cfg2", action="store_true", help="skip the B=128 N=128 side leg")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the measurement-only variant builds (e.g. under rocprofv3)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend (nccl = RCCL; gloo only for the one-GPU world-2 test)")
     ap.add_argument("--share-device", action="store_true",
@@ -513,6 +534,15 @@ def main():
                          "fp32_frac": fpw * B / (kern_ms * 1e-3) / FP32_PEAK},
             "mean_mll": mean_mll,
         }
+        if world == 1 and not args.no_variants:
+            v = variant_leg("f32update", B, N, D, args.steps)
+            if "kernel_ms" in v:
+                v["hbm_frac"] = bpw * B / (v["kernel_ms"] * 1e-3) / HBM_PEAK
+                v["slowdown_vs_split_f16"] = v["kernel_ms"] / kern_ms
+            v["note"] = ("the same kernel with the trailing Cholesky updates on fp32 MFMA "
+                         "(mfma_f32_16x16x4f32, 24-bit operands) instead of split-f16: a separate "
+                         "build (build_native.VARIANTS), timed in a child process; not the headline")
+            line["fp32_update"] = v
         if rank_times is not None:
             line["rank_times"] = {"ms_per_step": [r[0] / args.steps * 1e3 for r in rank_times],
                                   "kernel_ms": [r[1] for r in rank_times],

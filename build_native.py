@@ -102,6 +102,40 @@ def build(force: bool = False, verbose: bool = True, defines=(), out_dir: str = 
     return lib_path
 
 
+# Measurement-only variant builds of the exact kernel (bench.py's "fp32_update" note: the
+# pure-fp32 MFMA trailing update beside the split-f16 product path). Only gpk_exact.hip is
+# recompiled (N = 128 / 256 instantiations); the other objects of the main build are linked in.
+VARIANTS = {"f32update": ["GPK_SPLIT_UPDATE=0", "GPK_EXACT_DEV=1"]}
+
+
+def build_variant(name: str, verbose: bool = True) -> str:
+    main_lib = build(force=False, verbose=verbose)
+    out_dir = os.path.join(PKG, "_lib_variants", name)
+    os.makedirs(out_dir, exist_ok=True)
+    lib_path = os.path.join(out_dir, "libgpk.so")
+    src = os.path.join(CSRC, "gpk_exact.hip")
+    obj = os.path.join(out_dir, "gpk_exact.hip.o")
+    flags = FLAGS + [f"-D{d}" for d in VARIANTS[name]]
+    dig = _digest([src] + sorted(included(src)), " ".join(flags) + main_lib)
+    stamp = obj + ".sha"
+    if os.path.exists(lib_path) and os.path.exists(stamp) and open(stamp).read() == dig:
+        return lib_path
+    cmd = [HIPCC, *flags, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+    if verbose:
+        print("[build variant]", name, " ".join(VARIANTS[name]), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for the {name} variant:\n{r.stderr}")
+    objs = [os.path.join(OUT_DIR, os.path.basename(x) + ".o") for x in sources() if not x.endswith("gpk_exact.hip")]
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, obj, "-o", lib_path],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed for the {name} variant:\n{r.stderr}")
+    with open(stamp, "w") as f:
+        f.write(dig)
+    return lib_path
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")

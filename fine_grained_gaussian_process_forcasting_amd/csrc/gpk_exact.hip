@@ -187,6 +187,9 @@ GPK_DEVICE void barrier_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+#ifndef GPK_TMO_DEBUG
+#define GPK_TMO_DEBUG 0   // 1 (debug builds): a timed-out window's info = flag index | target << 8
+#endif
 #ifndef GPK_EXACT_COL
 #define GPK_EXACT_COL 0   // 1: column-ownership worker plan for N = 256 at 8 waves (worker_step_col)
 #endif
@@ -349,6 +352,7 @@ enum : int {
   kFlagZ = 80,      // z_k of the latest step k is out                               (epoch)
   kFlagTrsm = 81,   // worker TRSM phases completed in this attempt (one add per wave per step)
   kFlagBulk = 82,   // worker steps whose panel reads are all done (one add per wave per step)
+  kFlagRst = 83,    // restart barrier (two adds per wave per failed attempt, never reset)
 };
 
 // Poll an LDS flag until it reaches `target`. Every wait is bounded: after
@@ -365,11 +369,43 @@ GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
     // clocks between polls -- the wake-up latency sits on every hand-off
     if (++n > (1 << 18)) {
       flags[kFlagTmo] = 1;
+      if (GPK_TMO_DEBUG) flags[kFlagTmo + 1] = idx | (target << 8);   // which wait expired
       break;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+
+// spin_until that also watches this attempt's failure word (fidx): returns true -- without
+// waiting for `target` -- once the diagonal wave has reported the attempt failed. Every
+// worker wait goes through it, so a worker can never sit in a wait that the failed attempt
+// will not satisfy (the restart then needs no assumption about where each worker saw it).
+GPK_DEVICE bool spin_until_f(lds_vint* flags, int idx, int target, int fidx) {
+  int n = 0;
+  bool failed = false;
+  while (true) {
+    const int v = flags[idx];
+    const int f = flags[fidx];
+    if (v >= target) break;
+    if (f != 0) { failed = true; break; }
+    if ((n & 255) == 255 && flags[kFlagTmo] != 0) break;
+    if (++n > (1 << 18)) {
+      flags[kFlagTmo] = 1;
+      if (GPK_TMO_DEBUG) flags[kFlagTmo + 1] = idx | (target << 8);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  return failed;
+}
+
+// A worker wait inside a factorisation step: leaves the step (failed attempt) when the
+// diagonal wave has reported a failure instead of waiting for something that will not come.
+#define GPK_WAITF(idx, target)                                                   \
+  if (spin_until_f(x.vflag, (idx), (target), kFlagFail + e0 / 32)) {             \
+    __builtin_amdgcn_s_setprio(0);                                               \
+    return 1;                                                                    \
+  }
 
 GPK_DEVICE void publish_tile(float* dst, int lane, const f32x4 v, lds_vint* flags, int idx, int value) {
   *(f32x4*)&dst[lane * 4] = v;
@@ -736,13 +772,17 @@ GPK_DEVICE void worker_arrive(WorkerCtx& x) {
                              __ATOMIC_RELAXED);
 }
 template <int WK>
-GPK_DEVICE void worker_wait(WorkerCtx& x) {
-  spin_until(x.vflag, kFlagSync, WK * x.nsync);
+GPK_DEVICE bool worker_wait(WorkerCtx& x) {   // true: the attempt failed meanwhile
+  return spin_until_f(x.vflag, kFlagSync, WK * x.nsync, kFlagFail + x.epoch0 / 32);
 }
+// Restart barrier after a failed attempt (jitter ladder), on its own monotone counter: r-th
+// barrier of the launch. Between its two uses the per-attempt counters are reset.
 template <int WK>
-GPK_DEVICE void worker_sync(WorkerCtx& x) {
-  worker_arrive(x);
-  worker_wait<WK>(x);
+GPK_DEVICE void restart_sync(WorkerCtx& x, int r) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (x.lane == 0)
+    (void)__atomic_fetch_add((__attribute__((address_space(3))) int*)&x.vflag[kFlagRst], 1, __ATOMIC_RELAXED);
+  spin_until(x.vflag, kFlagRst, WK * r);
 }
 
 // One right-looking step K for the worker waves (panel K is produced and applied in
@@ -802,7 +842,7 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
   const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
   if (flag_now < e0 + K) {
-    spin_until(x.vflag, kFlagFact, e0 + K);
+    (void)spin_until_f(x.vflag, kFlagFact, e0 + K, kFlagFail + e0 / 32);
     fail = x.vflag[kFlagFail + e0 / 32];
     q = load_w_v(wbk, c, grp);
   }
@@ -845,7 +885,8 @@ GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   GPK_WSTAMP(4, 2)  // TRSM
   if constexpr (LAST) return 0;
   // ---- 2. panel K complete
-  worker_sync<WK>(x);
+  worker_arrive(x);
+  if (worker_wait<WK>(x)) return 1;
   GPK_WSTAMP(5, 3)  // step counter
   // ---- 3. hand-over for the diagonal wave's look-ahead at step K+1
   // (compile-time (i, j): no plan lookup, so nothing wave-specialised gets hoisted)
@@ -1080,7 +1121,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
   const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
   if (flag_now < e0 + K) {
-    spin_until(x.vflag, kFlagFact, e0 + K);
+    (void)spin_until_f(x.vflag, kFlagFact, e0 + K, kFlagFail + e0 / 32);
     fail = x.vflag[kFlagFail + e0 / 32];
     q = load_w_v(wbk, c, grp);
   }
@@ -1165,7 +1206,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     });
   }
   GPK_WSTAMP(3, 3)  // deferred RBF (after the arrive)
-  worker_wait<WK>(x);
+  if (worker_wait<WK>(x)) return 1;
   GPK_WSTAMP(5, 6)  // worker barrier
   return 0;
 }
@@ -1250,11 +1291,11 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     constexpr int SB = K <= 6 ? 16 - K : (K == 7 ? 19 : K + 1);
     if (wv == HAW || wv == HBW) {
       if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);
-      spin_until(x.vflag, kFlagPan + K + 1, e0 + K - 1);
+      GPK_WAITF(kFlagPan + K + 1, e0 + K - 1)
       const pan_op_t p = pan_load(pprev + (K + 1) * 256, lane);
       const pan_op_t pl = pan_swap(p);
       if (wv == HAW) {
-        spin_until(x.vflag, kFlagPan + K, e0 + K - 1);
+        GPK_WAITF(kFlagPan + K, e0 + K - 1)
         upd(acc[SA], pprev + K * 256, p, pl);
         publish_tile(hA, lane, acc[SA], x.vflag, kFlagHA, e0 + K);
       }
@@ -1272,8 +1313,8 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     constexpr bool C8 = (K + 2 <= 8);                 // (K, 8): slot 18 of wave K (K <= 6)
     const bool c_row = C8 && (wv == K);
     if (a_row || b_row || c_row) {
-      spin_until(x.vflag, kFlagPan + K, e0 + K - 1);
-      if (c_row) spin_until(x.vflag, kFlagPan + 8, e0 + K - 1);
+      GPK_WAITF(kFlagPan + K, e0 + K - 1)
+      if (c_row) { GPK_WAITF(kFlagPan + 8, e0 + K - 1) }
       const float* qt = pprev + K * 256;
       if (a_row) {
         const pan_op_t p = pan_load(pprev + jA * 256, lane);
@@ -1296,8 +1337,8 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // ---- 3. right-hand side row K: rw_K += R_{K-1,K}^T z_{K-1} (owner of column K)
   if constexpr (K > 0) {
     if (wv == OWN_K) {
-      spin_until(x.vflag, kFlagZ, e0 + K - 1);
-      if constexpr (K == 8) spin_until(x.vflag, kFlagPan + 8, e0 + K - 1);
+      GPK_WAITF(kFlagZ, e0 + K - 1)
+      if constexpr (K == 8) { GPK_WAITF(kFlagPan + 8, e0 + K - 1) }
       f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
       d = pan_mma(pan_load(pprev + K * 256, lane), pprev + NB * 256, lane, d);
@@ -1312,7 +1353,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   f32x4 q = load_w_v(wbk, c, grp);
   const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
   if (flag_now < e0 + K) {
-    spin_until(x.vflag, kFlagFact, e0 + K);
+    (void)spin_until_f(x.vflag, kFlagFact, e0 + K, kFlagFail + e0 / 32);
     fail = x.vflag[kFlagFail + e0 / 32];
     q = load_w_v(wbk, c, grp);
   }
@@ -1321,7 +1362,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);
   // panel buffer K & 1 held panel K-2 (read in step K-1): every wave must be past step K-1's
   // panel reads (one kFlagBulk add per wave per step)
-  if constexpr (K >= 2) spin_until(x.vflag, kFlagBulk, WK * K);
+  if constexpr (K >= 2) { GPK_WAITF(kFlagBulk, WK * K) }
   {
     const WOp wq = w_split(q);
     const bool a_t = (K + 1 <= jA), b_t = (K + 1 <= jB);
@@ -1374,7 +1415,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   if constexpr (K + 1 == NB) return 0;
   // ---- 5. the rest of the trailing update through panel K-1: rows K+1 .. of the owned columns
   if constexpr (K > 0) {
-    spin_until(x.vflag, kFlagTrsm, WK * K);   // panel K-1 complete
+    GPK_WAITF(kFlagTrsm, WK * K)   // panel K-1 complete
     // column A (rows K+1 .. jA; (K+1, K+1) is HB: done)
     if (K + 1 <= jA) {
       const pan_op_t p = pan_load(pprev + jA * 256, lane);
@@ -1414,7 +1455,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       d = pan_mma(pan_load(pprev + j * 256, lane), pprev + NB * 256, lane, d);
       if (c == 0) *(f32x4*)&x.rw[16 * j + 4 * grp] = d;
     };
-    spin_until(x.vflag, kFlagZ, e0 + K - 1);
+    GPK_WAITF(kFlagZ, e0 + K - 1)
     if (K + 1 <= jA) rhs(jA);
     if (K + 1 <= jB) rhs(jB);
     if constexpr (K + 1 <= 8) {
@@ -1632,6 +1673,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       for (int qq = kFlagPan; qq <= kFlagZ; ++qq) flag[qq] = -1;
       flag[kFlagTrsm] = 0;
       flag[kFlagBulk] = 0;
+      flag[kFlagRst] = 0;
       flag[kFlagInvSigma] = __builtin_bit_cast(int, inv_sigma);
       smem[lay.rbfc + 1] = s2;
       ((int*)smem)[lay.rbfc + 3] = lay.nrm | (((DC + 1) / 2) << 20);
@@ -1770,6 +1812,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       for (int qq = kFlagPan; qq <= kFlagZ; ++qq) flag[qq] = -1;
       flag[kFlagTrsm] = 0;
       flag[kFlagBulk] = 0;
+      flag[kFlagRst] = 0;
       flag[kFlagInvSigma] = __builtin_bit_cast(int, inv_sigma);  // read back per step (SGPR budget)
       smem[lay.rbfc + 1] = s2;
       ((int*)smem)[lay.rbfc + 3] = lay.nrm | (((DC + 1) / 2) << 20);
@@ -1951,6 +1994,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
       info_w = failed;
     }
+    if (GPK_TMO_DEBUG && lane == 0) vflag[24] = att_end;
     __builtin_amdgcn_s_setprio(0);
   } else {
     // ================================================= worker program
@@ -2066,16 +2110,18 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       if constexpr (STAMPS) st_last = wst[8];
       sumz2 = wx.sumz2;
       if (!failed) { info_w = attempt > 0 ? -attempt : 0; break; }
-      // every worker has left the failed attempt before anyone rebuilds
-      worker_sync<WK>(wx);
-      if constexpr (COL) {   // the column plan's per-attempt counters restart from 0
-        if (wave == 0 && lane == 0) {
-          vflag[kFlagTrsm] = 0;
-          vflag[kFlagBulk] = 0;
-        }
-        worker_sync<WK>(wx);
+      // every worker has left the failed attempt before anyone rebuilds; the per-attempt
+      // counters restart from 0 between the two restart barriers
+      restart_sync<WK>(wx, 2 * attempt + 1);
+      if (wave == 0 && lane == 0) {
+        vflag[kFlagSync] = 0;
+        vflag[kFlagTrsm] = 0;
+        vflag[kFlagBulk] = 0;
       }
+      wx.nsync = 0;
+      restart_sync<WK>(wx, 2 * attempt + 2);
     }
+    if (GPK_TMO_DEBUG && wave == 0 && lane == 0) vflag[23] = att_end;
     if constexpr (STAMPS) {
       for (int q = 2; q < 8; ++q) st_acc[q] += wst[q];
     }
@@ -2089,7 +2135,9 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   if (tid == 0) {
     const int fcol = vflag[kFlagFail + att_end];
     if (vflag[kFlagTmo] != 0) {
-      info[b] = kInfoTimeout;
+      info[b] = GPK_TMO_DEBUG ? ((1 << 30) | ((int)vflag[23] << 26) | ((int)vflag[24] << 22) |
+                                 (((int)vflag[kFlagSync] & 0x3f) << 16) | ((int)vflag[kFlagTmo + 1] & 0xffff))
+                              : kInfoTimeout;
       mll[b] = __builtin_nanf("");
     } else if (fcol != 0) {
       info[b] = fcol;

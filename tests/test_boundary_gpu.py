@@ -193,3 +193,36 @@ def test_forward_gp_branch_vs_oracle(cuda_device):
                              jitter=1e-4)
     assert _rel(dec.grad.cpu(), 1.5 + gr["X"]) <= TOL
     assert enc.grad is None or float(enc.grad.abs().max()) == 0.0
+
+
+def test_layer_forward_returns_prior_and_exact_prior_variance(cuda_device):
+    """Reference surface details: ToyDeepGPHiddenLayer.forward(x) is the layer's PRIOR
+    MultivariateNormal(mean_module(x), covar_module(x)) (DeepGP.py:51-54) -- here its mean and
+    the kernel diagonal (outputscale) -- while calling the layer gives q(f); and an exact-GP
+    prior's .variance is diag K(x, x) = outputscale (+ noise through the likelihood)."""
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.DeepGP import DeepGPp
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.GPModel import ExactGPModel
+    from fine_grained_gaussian_process_forcasting_amd.likelihoods import GaussianLikelihood
+    d = 8
+    model = DeepGPp(d, 3).to(cuda_device)
+    hl = model.hidden_layer
+    x = torch.randn(2, 5, d, device=cuda_device)
+    prior = hl.forward(x)
+    want_mean = (x @ hl.mean_module.weights).squeeze(-1) + hl.mean_module.bias
+    assert torch.allclose(prior.mean, want_mean, rtol=1e-5, atol=1e-6)
+    s2 = float(hl.covar_module.outputscale.item())
+    assert torch.allclose(prior.variance, torch.full((2, 5), s2, device=cuda_device), rtol=1e-6)
+    # the exact model's train-mode prior
+    X = torch.randn(3, 16, 2, device=cuda_device)
+    y = torch.randn(3, 16, device=cuda_device)
+    lik = GaussianLikelihood().to(cuda_device)
+    em = ExactGPModel(X, y, lik).to(cuda_device)
+    em.train()
+    out = em(X)
+    s2e = float(em.covar_module.outputscale.item())
+    assert torch.allclose(out.variance, torch.full((3, 16), s2e, device=cuda_device), rtol=1e-6)
+    noisy = lik(out)
+    assert torch.allclose(noisy.variance, torch.full((3, 16), s2e + float(lik.noise.item()), device=cuda_device),
+                          rtol=1e-6)
+    out.variance.sum().backward()   # differentiable in the outputscale
+    assert em.covar_module.raw_outputscale.grad is not None
