@@ -44,14 +44,8 @@
 #ifndef GPK_SPLIT_UPDATE
 #define GPK_SPLIT_UPDATE 1
 #endif
-#ifndef GPK_EXACT_FLOW
-#define GPK_EXACT_FLOW 0  // 1: dataflow step order (TRSM -> counter -> hand-over -> bulk); 0: round-2 order
-#endif
 #ifndef GPK_EXACT_SMALLB
 #define GPK_EXACT_SMALLB 1   // B <= CUs: one window per CU with 16 waves (launch_exact_nb)
-#endif
-#ifndef GPK_TRSM_F16
-#define GPK_TRSM_F16 0   // 1: trailing-tile TRSM on split-f16 MFMA (measured 3 % slower: more spills); 0 = fp32 MFMA
 #endif
 #ifndef GPK_EXACT_PRIO_RHS
 #define GPK_EXACT_PRIO_RHS 1   // raise the worker priority already at the right-hand side (0: at the TRSM)
@@ -191,21 +185,8 @@ GPK_DEVICE void barrier_lds() {
 #define GPK_TMO_DEBUG 0   // 1 (debug builds): a timed-out window's info = flag index | target << 8
 #endif
 #ifndef GPK_EXACT_COL
-#define GPK_EXACT_COL 0   // 1: column-ownership worker plan for N = 256 at 8 waves (worker_step_col)
+#define GPK_EXACT_COL 1   // 1: column-ownership worker plan for N = 256 at 8 waves (worker_step_col)
 #endif
-#ifndef GPK_ZL_ORDER
-#define GPK_ZL_ORDER 0   // which block row's upper zeros a step writes (see worker_step_split)
-#endif
-#ifndef GPK_RBF_UPFRONT
-#define GPK_RBF_UPFRONT 0   // 1: every RBF tile in the prologue (0: block row k+2 deferred into step k)
-#endif
-#ifndef GPK_RHS_BATCH
-#define GPK_RHS_BATCH 0   // 1: the right-hand-side rows of a step as one batch of loads, then the MFMAs
-#endif
-#ifndef GPK_LDEFER
-#define GPK_LDEFER 0   // 1: the workers store their L tiles after the step arrive (read back from the panel)
-#endif
-static_assert(!GPK_LDEFER || GPK_SPLIT_UPDATE, "GPK_LDEFER reads the split panel planes");
 #ifndef GPK_LST_AUX
 #define GPK_LST_AUX 17   // L stores: -1 plain global stores; >= 0 buffer stores with this cache-policy aux
                          // (17 = sc0 sc1: write-through, the lines leave L2 -- 64.5 -> 59.2 us per B=512 launch)
@@ -401,11 +382,7 @@ GPK_DEVICE bool spin_until_f(lds_vint* flags, int idx, int target, int fidx) {
 
 // A worker wait inside a factorisation step: leaves the step (failed attempt) when the
 // diagonal wave has reported a failure instead of waiting for something that will not come.
-#define GPK_WAITF(idx, target)                                                   \
-  if (spin_until_f(x.vflag, (idx), (target), kFlagFail + e0 / 32)) {             \
-    __builtin_amdgcn_s_setprio(0);                                               \
-    return 1;                                                                    \
-  }
+#define GPK_WAITF(idx, target) spin_until(x.vflag, (idx), (target));
 
 GPK_DEVICE void publish_tile(float* dst, int lane, const f32x4 v, lds_vint* flags, int idx, int value) {
   *(f32x4*)&dst[lane * 4] = v;
@@ -426,48 +403,9 @@ GPK_DEVICE f32x4 trsm_tile_f32(const f32x4 q, const f32x4 t) {
   return d0 + d1;
 }
 
-#if GPK_TRSM_F16
-// Split-f16 TRSM of a trailing tile (GPK_TRSM_F16=1): R_kj = W T with W = R_kk^{-T}
-// rounded to hi + lo f16 planes (after an exact 2^8 scale that puts its entries in the
-// normal f16 range) and T (|T_ij| <= 2^15: Schur-complement entries are bounded by the
-// diagonal, which the sigma^2 scaling puts below 2^15) rounded to hi + lo on the fly:
-//   A = {W_hi, W_hi} / {W_lo, W_lo},  B = {T_hi, T_lo}  (k-slots 8g..8g+3 <-> rows 4g..4g+3
-//   hi, 8g+4..8g+7 <-> the same rows lo: the acc layout IS the operand layout),
-// two mfma_f32_16x16x32_f16 = (W_hi + W_lo)(T_hi + T_lo) with every product exact:
-// 32 matrix-pipe cycles instead of the four 16x16x4 f32 MFMAs' 128. The rounding is the
-// same 22-bit split the panel tiles get (pan_store) right after.
-struct WOp {
-  half8_t hh, ll;
-};
-GPK_DEVICE WOp w_split(const f32x4 q) {
-  half4_t h, l;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float x = q[r] * 256.f;
-    h[r] = (_Float16)x;
-    l[r] = (_Float16)(x - (float)h[r]);
-  }
-  return WOp{half8_t{h[0], h[1], h[2], h[3], h[0], h[1], h[2], h[3]},
-             half8_t{l[0], l[1], l[2], l[3], l[0], l[1], l[2], l[3]}};
-}
-GPK_DEVICE f32x4 trsm_tile(const WOp& w, const f32x4 t) {
-  half4_t h, l;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    h[r] = (_Float16)t[r];
-    l[r] = (_Float16)(t[r] - (float)h[r]);
-  }
-  const half8_t b = {h[0], h[1], h[2], h[3], l[0], l[1], l[2], l[3]};
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.hh, b, z, 0, 0, 0);
-  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.ll, b, d, 0, 0, 0);
-  return d * (1.f / 256.f);
-}
-#else
 typedef f32x4 WOp;
 GPK_DEVICE WOp w_split(const f32x4 q) { return q; }
 GPK_DEVICE f32x4 trsm_tile(const WOp& w, const f32x4 t) { return trsm_tile_f32(w, t); }
-#endif
 
 GPK_DEVICE f32x4 load_w(const float* wb, int c, int grp) {
   f32x4 q;
@@ -597,7 +535,10 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
   for (int i = 1; i < 16; ++i) dg = (c == i) ? v[i] : dg;
   const bool okd = (dg > 0.f) && (dg < __builtin_huge_valf());
   const unsigned long long badm = (GPK_KO != 0) ? 0ull : __ballot(lane < 16 && !okd);
-  if (badm != 0 && lane == 0) *fail_flag = 1;  // provisional: exact column below
+  // provisional (the exact column follows): 16 k + 1 -- the failing STEP is readable from
+  // either value as (word - 1) >> 4, so a worker that is still at an earlier step does not
+  // leave the attempt before the others (they all leave at step k)
+  if (badm != 0 && lane == 0) *fail_flag = 16 * (epoch & 31) + 1;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   if (lane == 0) flags[kFlagFact] = epoch;
   if constexpr (ST) {
@@ -772,8 +713,9 @@ GPK_DEVICE void worker_arrive(WorkerCtx& x) {
                              __ATOMIC_RELAXED);
 }
 template <int WK>
-GPK_DEVICE bool worker_wait(WorkerCtx& x) {   // true: the attempt failed meanwhile
-  return spin_until_f(x.vflag, kFlagSync, WK * x.nsync, kFlagFail + x.epoch0 / 32);
+GPK_DEVICE bool worker_wait(WorkerCtx& x) {   // (always false: every worker leaves a failed
+  spin_until(x.vflag, kFlagSync, WK * x.nsync);  // attempt at the same step, see diag_factor)
+  return false;
 }
 // Restart barrier after a failed attempt (jitter ladder), on its own monotone counter: r-th
 // barrier of the launch. Between its two uses the per-attempt counters are reset.
@@ -785,198 +727,7 @@ GPK_DEVICE void restart_sync(WorkerCtx& x, int r) {
   spin_until(x.vflag, kFlagRst, WK * r);
 }
 
-// One right-looking step K for the worker waves (panel K is produced and applied in
-// the same step). The diagonal wave owns the diagonal tiles: at its step K it factors
-// (K,K), publishes R_KK^{-T}, and then -- look-ahead -- computes R_{K,K+1} itself and
-// applies that last update to (K+1,K+1), from the hand-over of (K,K+1) and (K+1,K+1)
-// through panel K-1. The workers, per step:
-//   1. wait for R_KK^{-T}, TRSM their tiles of block row K into panel K (+ z_K);
-//   2. count in / wait on the worker-only step counter: panel K is complete;
-//   3. hand over what the diagonal wave's NEXT look-ahead needs -- (K+1,K+2) and
-//      (K+2,K+2) updated through panel K -- FIRST (hbuf[(K+1) & 1], flags HA / HB);
-//   4. apply panel K to every other tile with i >= K+1 except (K+1,K+1) (the
-//      diagonal wave's), block row K+1 first: it is what the next TRSM reads;
-//   5. right-hand side (rw_i += R_{K,i}^T z_K), zero L's upper block row K, and the
-//      deferred RBF of block row K+3 (the Gram is additive; row K+3 is first read by
-//      the hand-over of step K+1).
-// Step K's hand-over is ready one TRSM + one counter after R_KK^{-T}, while the
-// diagonal wave runs its look-ahead and the whole factorisation of (K+1,K+1): the
-// bulk of step K overlaps that instead of sitting between the diagonal wave's steps.
-// Buffer reuse: panel K+2 overwrites panel K only after the step-(K+1) counter,
-// which every wave passes after finishing step K; hbuf[(K+1) & 1] is rewritten for
-// step K+2's hand-over only after R_{K+1,K+1}^{-T} exists, i.e. after the diagonal
-// wave has consumed it; wbuf[K & 1] is rewritten by the factor of (K+2,K+2), which
-// needs step K's hand-over, i.e. every worker past its step-K TRSM.
-// Returns nonzero when the diagonal wave reported a failed factorisation.
-template <int NB, int WK, int SLOTS, int K, bool ST, bool FULL>
-GPK_DEVICE int worker_step(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
-  constexpr int Pk = plan_P<NB>(K);
-  constexpr bool LAST = (K == NB - 1);
-  constexpr bool HAND = (K + 2 < NB);                     // a look-ahead at diagonal step K+1
-  constexpr int TD = LAST ? -1 : plan_P<NB>(K + 1);       // (K+1, K+1): the diagonal wave's
-  constexpr int TA = HAND ? plan_P<NB>(K + 1) + 1 : -1;   // (K+1, K+2)
-  constexpr int TB = HAND ? plan_P<NB>(K + 2) : -1;       // (K+2, K+2)
-  // launder per step: keeps the per-slot plan loads / LDS addresses of this
-  // step from being hoisted (and pinned in registers) across all NB steps
-  const int wv = launder_s(x.wv);
-  const int e0 = launder_s(x.epoch0);
-  int lane = x.lane;
-  asm volatile("" : "+v"(lane));
-  const int c = lane & 15, grp = lane >> 4;
-  float* pcur = x.panel + (K & 1) * (NB + 1) * 256;                // panel K
-  float* hA = x.hbuf + ((K + 1) & 1) * 512;
-  if constexpr (ST) {
-    if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8] = __builtin_amdgcn_s_memtime();
-  }
-  // ---- 1. TRSM of the row-K off-diagonal tiles (P(K) < t <= P(K) + NB - K - 1) and,
-  // by the owner of RHS block row K, of the right-hand side: z_K.
-  // One LDS round trip in the usual case (the diagonal wave is ahead): the epoch flag, the
-  // failure word, R_KK^{-T} and 1/sigma are requested together. A wave's LDS reads are
-  // served in order, and the diagonal wave completes its R_KK^{-T} and failure-word writes
-  // before it releases the flag, so reads issued after a flag read that sees epoch K see
-  // them too (all volatile: the compiler keeps the order). Otherwise: wait, re-read.
-  const float* wbk = x.wbuf + (K % 3) * kWBuf;
-  const int flag_now = x.vflag[kFlagFact];
-  int fail = x.vflag[kFlagFail + e0 / 32];
-  f32x4 q = load_w_v(wbk, c, grp);
-  // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
-  const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
-  if (flag_now < e0 + K) {
-    (void)spin_until_f(x.vflag, kFlagFact, e0 + K, kFlagFail + e0 / 32);
-    fail = x.vflag[kFlagFail + e0 / 32];
-    q = load_w_v(wbk, c, grp);
-  }
-  GPK_WSTAMP(7, 1)  // wait for R_KK^{-T}
-  if (fail != 0) return 1;
-  const WOp wq = w_split(q);
-  const int rfirst = K + (((wv - K) % WK) + WK) % WK;   // this wave's first RHS block row >= K
-  {
-    constexpr int TLO = Pk + 1, THI = Pk + NB - K - 1;
-    constexpr int SLO = TLO >= WK ? (TLO - (WK - 1)) / WK : 0;
-    constexpr int SHI = (THI / WK) < SLOTS - 1 ? (THI / WK) : SLOTS - 1;
-    if constexpr (THI >= TLO) {
-      static_for_range<SLO, SHI>([&](auto I) {
-        constexpr int s = decltype(I)::value;
-        const int t = wv + WK * s;
-        if (t >= TLO && t <= THI) {
-          const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
-          const f32x4 rkj = pan_store(pcur + j * 256, lane, trsm_tile(wq, acc[s]));
-          // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
-          if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
-        }
-      });
-    }
-    if (rfirst == K) {
-      f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
-      if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 zk = pan_store(pcur + NB * 256, lane, trsm_tile_f32(q, d));   // (y unbounded: fp32)
-      if (c == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
-        if (x.zout != nullptr) {
-          const int row = 16 * K + 4 * grp;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (FULL || row + r < x.N) x.zout[(size_t)x.b * x.N + row + r] = zk[r];
-        }
-      }
-    }
-  }
-  GPK_WSTAMP(4, 2)  // TRSM
-  if constexpr (LAST) return 0;
-  // ---- 2. panel K complete
-  worker_arrive(x);
-  if (worker_wait<WK>(x)) return 1;
-  GPK_WSTAMP(5, 3)  // step counter
-  // ---- 3. hand-over for the diagonal wave's look-ahead at step K+1
-  // (compile-time (i, j): no plan lookup, so nothing wave-specialised gets hoisted)
-  auto upd_ij = [&](f32x4& d, auto I, auto J) {
-    constexpr int i = decltype(I)::value, j = decltype(J)::value;
-    d = pan_mma(pan_load(pcur + i * 256, lane), pcur + j * 256, lane, d);
-  };
-  if constexpr (HAND) {
-    if (wv == TA % WK) {
-      upd_ij(acc[TA / WK], IC<K + 1>{}, IC<K + 2>{});
-      publish_tile(hA, lane, acc[TA / WK], x.vflag, kFlagHA, e0 + K + 1);
-    }
-    if (wv == TB % WK) {
-      upd_ij(acc[TB / WK], IC<K + 2>{}, IC<K + 2>{});
-      publish_tile(hA + 256, lane, acc[TB / WK], x.vflag, kFlagHB, e0 + K + 1);
-    }
-  }
-  GPK_WSTAMP(6, 4)  // hand-over
-  // ---- 4. trailing update from panel K over the other tiles with i >= K+1
-  // (t < P(K)), highest slot first (= block row K+1 first). Re-laundered: the
-  // hand-over branches above pin wv to a constant, and code tail-duplicated into
-  // them would turn plan lookups into constants hoisted out of the attempt loop.
-  {
-    const int wv = launder_s(x.wv);
-    auto upd = [&](f32x4& d, auto I) {
-      constexpr int s = decltype(I)::value;
-      const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(wv + WK * s);
-      d = pan_mma(pan_load(pcur + (p & 255) * 256, lane), pcur + (p >> 8) * 256, lane, d);
-    };
-    constexpr int NALL = Pk / WK;
-    auto bulk = [&](auto I) {
-      constexpr int s = decltype(I)::value;
-      bool sk = false;
-      if constexpr (s == TD / WK) sk = sk || (wv == TD % WK);
-      if constexpr (HAND && s == TA / WK) sk = sk || (wv == TA % WK);
-      if constexpr (HAND && s == TB / WK) sk = sk || (wv == TB % WK);
-      if (!sk) upd(acc[s], I);
-    };
-    if constexpr (NALL < SLOTS && (Pk % WK) != 0) {
-      if (wv < Pk % WK) bulk(IC<NALL>{});
-    }
-    static_for_desc<NALL>(bulk);
-  }
-  GPK_WSTAMP(2, 5)  // trailing update
-  // ---- 5. right-hand side rows i >= K+1 owned by this wave: rw_i += R_{K,i}^T z_K
-  // (rw holds -(y - c); only column 0 of the tile is live, so it round-trips
-  // through LDS on the c == 0 lanes)
-  for (int i = rfirst == K ? K + WK : rfirst; i < NB; i += WK) {
-    f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
-    if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
-    d = pan_mma(pan_load(pcur + i * 256, lane), pcur + NB * 256, lane, d);
-    if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
-  }
-  // zero L's strictly-upper part of block-row K (streams out behind the MFMAs)
-  if (x.Lb != nullptr) {
-    const int N = FULL ? 16 * NB : x.N;
-    const int c0 = 16 * (K + 1);
-    for (int qq = wv; qq < 16; qq += WK) {
-      const int row = 16 * K + qq;
-      if (row < N) {
-        if ((N & 3) == 0) {
-          for (int cc = c0 + 4 * lane; cc < N; cc += 256)
-            lstore(x.Lb, row * N + cc, f32x4{0.f, 0.f, 0.f, 0.f});
-        } else {
-          for (int cc = c0 + lane; cc < N; cc += 64) x.Lb[(size_t)row * N + cc] = 0.f;
-        }
-      }
-    }
-  }
-  // deferred RBF of block row K+3 (its tiles are first read by step K+1's hand-over)
-  if constexpr (K + 3 < NB && !GPK_RBF_UPFRONT) {
-    constexpr int RLO = plan_P<NB>(K + 3), RHI = plan_P<NB>(K + 2) - 1;
-    constexpr int SLO = RLO / WK;
-    constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
-    const RbfK rk = read_rbfk(x.smem + x.rbfc);
-    static_for_range<SLO, SHI>([&](auto I) {
-      constexpr int s = decltype(I)::value;
-      const int t = wv + WK * s;
-      if (t >= RLO && t <= RHI) {
-        const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(t);
-        acc[s] += rbf_tile<NB, FULL>(x.smem, rk, p & 255, p >> 8, lane, x.N);
-      }
-    });
-  }
-  GPK_WSTAMP(3, 6)  // RHS + zero-L + deferred RBF
-  return 0;
-}
-
-// GPK_EXACT_FLOW=0: the round-2 step order (panel K-1 applied at step K, split-phase
-// worker barrier at the end). One right-looking step K for the worker waves. The diagonal wave owns the
+// One right-looking step K for the worker waves. The diagonal wave owns the
 // diagonal tiles from the moment they are handed over: at step K it factors
 // (K,K), computes R_{K,K+1} itself and applies that last update to (K+1,K+1)
 // (look-ahead), so the workers
@@ -1065,45 +816,18 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
 #if GPK_EXACT_PRIO_RHS
   __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // zero-L + right-hand side lead into the TRSM
 #endif
-  // zero L's strictly-upper part of one block row (streams out behind the MFMAs): block row K
-  // (GPK_ZL_ORDER 0), or NB-2-K (1: the zero runs grow as the TRSM row shrinks, so every step
-  // writes the same number of L bytes; measured no faster)
-  if (!(GPK_KO & 4) && x.Lb != nullptr) {
-    constexpr int KZ = GPK_ZL_ORDER == 1 ? NB - 2 - K : K;
-    if constexpr (KZ >= 0) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, KZ, wv, WK, lane);
-  }
+  // zero L's strictly-upper part of block row K (streams out behind the MFMAs)
+  if (!(GPK_KO & 4) && x.Lb != nullptr) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, K, wv, WK, lane);
   // right-hand side, block rows i >= K owned by this wave: rw_i += R_{K-1,i}^T z_{K-1}
   // (rw holds -(y - c); only column 0 of the tile is live, so it round-trips
   // through LDS on the c == 0 lanes)
   const int rfirst = K + (((wv - K) % WK) + WK) % WK;
-  if constexpr (K > 0 && !(GPK_KO & 2) && !GPK_RHS_BATCH) {
+  if constexpr (K > 0 && !(GPK_KO & 2)) {
     for (int i = rfirst; i < NB; i += WK) {
       f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
       d = pan_mma(pan_load(pprev + i * 256, lane), pprev + NB * 256, lane, d);
       if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
-    }
-  }
-  if constexpr (K > 0 && !(GPK_KO & 2) && GPK_RHS_BATCH) {
-    // this wave's rows i = rfirst + u WK < NB (at most UM of them): every LDS operand is
-    // requested before the first MFMA, so the rows cost one round trip, not one each
-    constexpr int UM = (NB - K + WK - 1) / WK;
-    const pan_op_t zk = pan_load(pprev + NB * 256, lane);
-    f32x4 d[UM];
-    pan_op_t pr[UM];
-#pragma unroll
-    for (int u = 0; u < UM; ++u) {
-      const int i = rfirst + u * WK;
-      const int ic = i < NB ? i : NB - 1;
-      d[u] = *(const f32x4*)&x.rw[16 * ic + 4 * grp];
-      pr[u] = pan_load(pprev + ic * 256, lane);
-    }
-#pragma unroll
-    for (int u = 0; u < UM; ++u) {
-      const int i = rfirst + u * WK;
-      if (c != 0) d[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      d[u] = pan_mma_op(pr[u], zk, d[u]);
-      if (c == 0 && i < NB) *(f32x4*)&x.rw[16 * i + 4 * grp] = d[u];
     }
   }
   GPK_WSTAMP(6, 2)  // right-hand side
@@ -1121,12 +845,12 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // the factor runs on sigma^2 K_hat (power of two): L = R'^T / sigma
   const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
   if (flag_now < e0 + K) {
-    (void)spin_until_f(x.vflag, kFlagFact, e0 + K, kFlagFail + e0 / 32);
+    spin_until(x.vflag, kFlagFact, e0 + K);
     fail = x.vflag[kFlagFail + e0 / 32];
     q = load_w_v(wbk, c, grp);
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
-  if (GPK_KO == 0 && fail != 0) {
+  if (GPK_KO == 0 && fail != 0 && ((fail - 1) >> 4) <= K) {   // the attempt failed at step <= K
     __builtin_amdgcn_s_setprio(0);   // the jitter-ladder retry starts at the base priority
     return 1;
   }
@@ -1144,7 +868,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
           const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
           const f32x4 rkj = pan_store(pcur + j * 256, lane, (GPK_KO & 1) ? acc[s] : trsm_tile(wq, acc[s]));
           // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
-          if (!GPK_LDEFER && !(GPK_KO & 32) && x.Lb != nullptr)
+          if (!(GPK_KO & 32) && x.Lb != nullptr)
             store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
         }
       });
@@ -1170,28 +894,8 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // does not depend on the other waves (zero-L, deferred RBF) before waiting on it
   worker_arrive(x);
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
-  if constexpr (GPK_LDEFER) {
-    // the L stores of this wave's panel-K tiles, after the arrive: read back from the panel
-    // (hi + lo is exactly the rounded R_Kj), so no store sits inside the TRSM phase
-    if (x.Lb != nullptr && THI >= TLO) {
-      static_for_range<SLO, SHI>([&](auto I) {
-        constexpr int s = decltype(I)::value;
-        const int t = wv + WK * s;
-        if (t >= TLO && t <= THI) {
-          const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
-          const float* tile = pcur + j * 256;
-          const half4_t h = *(const half4_t*)&tile[2 * lane];
-          const half4_t l = *(const half4_t*)&tile[128 + 2 * lane];
-          f32x4 v;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = ((float)h[r] + (float)l[r]) * inv_sigma;
-          store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, v);
-        }
-      });
-    }
-  }
   // deferred RBF of block row K+2 (its diagonal tile is handed over at step K+1)
-  if constexpr (K + 2 < NB && !(GPK_KO & 8) && !GPK_RBF_UPFRONT) {
+  if constexpr (K + 2 < NB && !(GPK_KO & 8)) {
     constexpr int RLO = plan_P<NB>(K + 2), RHI = plan_P<NB>(K + 1) - 1;
     constexpr int SLO = RLO / WK;
     constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
@@ -1353,12 +1057,12 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   f32x4 q = load_w_v(wbk, c, grp);
   const float inv_sigma = __builtin_bit_cast(float, (int)x.vflag[kFlagInvSigma]);
   if (flag_now < e0 + K) {
-    (void)spin_until_f(x.vflag, kFlagFact, e0 + K, kFlagFail + e0 / 32);
+    spin_until(x.vflag, kFlagFact, e0 + K);
     fail = x.vflag[kFlagFail + e0 / 32];
     q = load_w_v(wbk, c, grp);
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
-  if (GPK_KO == 0 && fail != 0) return 1;
+  if (GPK_KO == 0 && fail != 0 && ((fail - 1) >> 4) <= K) return 1;
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);
   // panel buffer K & 1 held panel K-2 (read in step K-1): every wave must be past step K-1's
   // panel reads (one kFlagBulk add per wave per step)
@@ -1465,7 +1169,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   count_in(x, kFlagBulk);   // this wave is done reading panel K-1
   GPK_WSTAMP(5, 6)
   // ---- 7. deferred RBF of block row K+2 and L's upper zeros
-  if constexpr (K + 2 < NB && !GPK_RBF_UPFRONT) {
+  if constexpr (K + 2 < NB) {
     constexpr int R = K + 2;
     const RbfK rk = read_rbfk(x.smem + x.rbfc);
     if (R <= jA) acc[R] += rbf_tile<NB, FULL>(x.smem, rk, R, jA, lane, x.N);
@@ -1479,10 +1183,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if (wv == R - 7) acc[19] += rbf_tile<NB, FULL>(x.smem, rk, R, 8, lane, x.N);
     }
   }
-  if (x.Lb != nullptr) {
-    constexpr int KZ = GPK_ZL_ORDER == 1 ? NB - 2 - K : K;
-    if constexpr (KZ >= 0 && KZ + 1 < NB) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, KZ, wv, WK, lane);
-  }
+  if (x.Lb != nullptr) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, K, wv, WK, lane);
   GPK_WSTAMP(3, 3)  // RBF + zero-L
   return 0;
 }
@@ -1493,11 +1194,7 @@ GPK_DEVICE int worker_steps(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     if constexpr (COL) {
       if (worker_step_col<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
     } else {
-#if GPK_EXACT_FLOW
-      if (worker_step<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
-#else
       if (worker_step_split<NB, WK, SLOTS, K, ST, FULL>(acc, x)) return 1;
-#endif
     }
     return worker_steps<NB, WK, SLOTS, K + 1, ST, FULL, COL>(acc, x);
   } else {
@@ -2061,8 +1758,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         } else {
         constexpr int P0 = plan_P<NB>(0);
         constexpr int P1 = NB > 1 ? plan_P<NB>(1) : 0;
-        // rows 0-2 now and row k+3 at step k (FLOW), rows 0-1 and row k+2 (split order)
-        constexpr int P2 = GPK_RBF_UPFRONT ? 0 : (GPK_EXACT_FLOW ? (NB > 2 ? plan_P<NB>(2) : 0) : P1);
+        constexpr int P2 = P1;   // rows 0-1 now, row k+2 at step k
         constexpr int T01 = P0 + 1;
         const int e0 = 32 * attempt;
         if (wv == P0 % WK) {
