@@ -18,10 +18,12 @@
 //   gpk_grad_solve_kernel  one workgroup (16 waves) per window: alpha = L^-T z, dy, and the
 //       lower block tiles of K^-1: wave J solves block column J with its tiles in registers
 //         forward   V_I = -Linv_II sum_{K=J}^{I-1} L_IK V_K       (I > J, V_J = Linv_JJ)
+//                   alpha_J += V_IJ^T z_I                          (alpha = V^T z, block J)
 //         backward  U_I =  Linv_II^T (V_I - sum_{K>I} L_KI^T U_K)  (I = NB-1 .. J)
-//       fp32 MFMA; all waves step together and each step's block row / column of L is
-//       staged once in LDS by the workgroup, fetched two steps ahead (double buffer);
-//       the diagonal-block inverses Linv_II live in LDS. U_I = K^-1_IJ -> workspace.
+//       split-f16 MFMA (GPK_GRAD_SPLIT); all waves step together and each step's block row /
+//       column of L is staged once in LDS (as split planes) by the workgroup, fetched two
+//       steps ahead (double buffer); the diagonal-block inverses Linv_II live in LDS.
+//       U_I = K^-1_IJ -> workspace.
 //   gpk_grad_gram_kernel   one wave per (window, block row I), no atomics: for every J the
 //       tile K^-1_JI (stored, or the transpose of the stored K^-1_IJ), the RBF tile
 //       recomputed from xs (fp32-MFMA Gram), G, W and Wx_I += W_JI^T xs_J (MFMA), w1_I;
@@ -31,12 +33,26 @@
 #include "gpk_internal.h"
 
 #include <mutex>
+#include <type_traits>
 
 // Timing experiments only (A/B builds of the solve kernel; results are wrong when set):
 // bit 1 skips the phase-1 tile math, 2 the phase-2 tile math, 4 the L staging, 8 the
-// K^-1 tile stores, 16 the alpha wave, 32 the phase-2 staging stores.
+// K^-1 tile stores, 16 the alpha products, 32 the phase-2 staging stores.
 #ifndef GPK_GRAD_SKIP
 #define GPK_GRAD_SKIP 0
+#endif
+// 1: the solve's tile products on split-f16 MFMA (operands rounded to hi + lo f16, 22
+// significant bits; every product exact, fp32 accumulation -- the forward's trailing-update
+// scheme); 0: fp32 MFMA (mfma_f32_16x16x4f32). B=512 N=256 D=32 backward:
+// 0.153 ms split vs 0.184 ms fp32 (scripts/ab/gpu_grad_abt.sh), same accuracy vs the oracle.
+#ifndef GPK_GRAD_SPLIT
+#define GPK_GRAD_SPLIT 1
+#endif
+// Timeline builds (GPK_GRAD_STAMPS=1, timing only): the solve kernel writes s_memtime
+// stamps into dX (which the gram kernel then leaves alone): per window, per step s (0..2NB-1),
+// per wave, 4 events (step start, math done, barrier passed, staging stored).
+#ifndef GPK_GRAD_STAMPS
+#define GPK_GRAD_STAMPS 0
 #endif
 
 namespace {
@@ -65,6 +81,30 @@ __host__ __device__ inline GradWs grad_ws(int N) {
 }
 GPK_DEVICE int tile_index(int I, int J) { return I * (I + 1) / 2 + J; }
 
+// D += Q^T P with Q, P split-f16 operands in registers ({hi, lo} per lane, acc layout):
+// hi.hi + lo.lo, then lo.hi + hi.lo -- two K=32 f16 MFMAs, every product exact.
+GPK_DEVICE f32x4 mma_split(const half8_t q, const half8_t p, f32x4 d) {
+  const half8_t q_lh = {q[4], q[5], q[6], q[7], q[0], q[1], q[2], q[3]};
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q, p, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(q_lh, p, d, 0, 0, 0);
+  return d;
+}
+GPK_DEVICE half8_t to_split(const f32x4 v) {
+  half4_t h, l;
+  (void)round_split_f16(v, h, l);
+  return half8_t{h[0], h[1], h[2], h[3], l[0], l[1], l[2], l[3]};
+}
+GPK_DEVICE f32x4 from_split(const half8_t v) {
+  return f32x4{(float)v[0] + (float)v[4], (float)v[1] + (float)v[5], (float)v[2] + (float)v[6],
+               (float)v[3] + (float)v[7]};
+}
+// Operand tile -> LDS split planes: the value of (lane l, reg r) of the acc layout.
+GPK_DEVICE void put_split_elem(float* tile, int l, int r, float v) {
+  const _Float16 h = (_Float16)v;
+  ((_Float16*)tile)[4 * l + r] = h;
+  ((_Float16*)(tile + 128))[4 * l + r] = (_Float16)(v - (float)h);
+}
+
 GPK_DEVICE f32x4 mfma4(const f32x4 a, const f32x4 b, f32x4 d) {
   d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], d, 0, 0, 0);
   d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], d, 0, 0, 0);
@@ -73,10 +113,29 @@ GPK_DEVICE f32x4 mfma4(const f32x4 a, const f32x4 b, f32x4 d) {
   return d;
 }
 
+// Compile-time loop A..B inclusive (register-array indices stay constants: a rolled loop
+// would index X[] dynamically and move it to scratch)
+template <int V>
+struct IdxC { static constexpr int value = V; };
+template <int A, int B, typename F>
+GPK_DEVICE void sfor(F&& f) {
+  if constexpr (A <= B) {
+    f(IdxC<A>{});
+    sfor<A + 1, B>(f);
+  }
+}
+
 // Uniform value the compiler must treat as unknown at this point: keeps per-tile
 // addresses from being hoisted out of their step (live addresses would spill).
 GPK_DEVICE int opaque_s(int v) {
   asm volatile("" : "+s"(v));
+  return v;
+}
+
+// Per-lane value the compiler must treat as unknown here (keeps a per-lane address from
+// being hoisted out of its step and kept live -- or spilled -- across the whole kernel).
+GPK_DEVICE int opaque_v(int v) {
+  asm volatile("" : "+v"(v));
   return v;
 }
 
@@ -93,14 +152,16 @@ GPK_DEVICE float row16_sum(float v) {
 // 1. solve: alpha, dy and the lower tiles of K^-1
 // ======================================================================================
 struct SolveLds {
-  int dinv, stg, sv, alpha, red, total;
+  int dinv, dsa, dsb, stg, sv, alpha, red, total;
 };
 __host__ __device__ inline SolveLds solve_lds(int NB) {
   SolveLds o;
   const int TS = (NB > 1 ? NB - 1 : 1) * 256;
   const int stg = 2 * TS > NB * 256 ? 2 * TS : NB * 256;   // (prologue: diagonal blocks of L)
   o.dinv = 0;                     // NB x 16 x 16 row-major Linv_II
-  o.stg = o.dinv + NB * 256;
+  o.dsa = o.dinv + NB * 256;      // GPK_GRAD_SPLIT: Linv_II^T as split planes (phase-1 operand)
+  o.dsb = o.dsa + (GPK_GRAD_SPLIT ? NB * 256 : 0);   // Linv_II as split planes (phase 2)
+  o.stg = o.dsb + (GPK_GRAD_SPLIT ? NB * 256 : 0);
   o.sv = o.stg + stg;             // NP
   o.alpha = o.sv + 16 * NB;       // NP
   o.red = o.alpha + 16 * NB;      // kST column-sum partials + 64
@@ -110,6 +171,7 @@ __host__ __device__ inline SolveLds solve_lds(int NB) {
 
 template <int NB, bool FULL>
 __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs a) {
+  constexpr bool SPLIT = GPK_GRAD_SPLIT && NB > 0;   // (dependent: the other branch is discarded)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NP = 16 * NB;
   constexpr int TS = (NB > 1 ? NB - 1 : 1) * 256;
@@ -175,6 +237,13 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
       }
 #pragma unroll
       for (int m = 0; m < 16; ++m) dinv[bi * 256 + m * 16 + cc] = x[m];
+      if constexpr (SPLIT) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          put_split_elem(smem + lay.dsa + bi * 256, 16 * (cc >> 2) + m, cc & 3, x[m]);   // Linv^T
+          put_split_elem(smem + lay.dsb + bi * 256, 16 * (m >> 2) + cc, m & 3, x[m]);    // Linv
+        }
+      }
     }
     if (tid < kMaxD) {
       float s = 0.f;
@@ -187,16 +256,27 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
   //      together through 2 NB steps with the step's L tiles staged in LDS
   const int J = wave;
   const bool live = J < NB;
-  constexpr int AW = NB < kSW ? NB : kSW - 1;   // the wave that also solves alpha
   const float gw = a.gout[b];
   const float invN = 1.f / (float)N;
-  float asum = 0.f;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  // The staging prefetch of a step is issued and consumed under wave-uniform branches; at the
+  // join the compiler cannot tell that the load was consumed, and waits for vmcnt(0) (this
+  // step's fresh prefetch included) the first time it reuses the old destination registers --
+  // at the start of the step's math, exposing the whole global latency every step. An
+  // unconditional vmcnt(0) right after the staging store (where the wave waits anyway)
+  // retires the old load on every path.
+  // window's L as a buffer resource (FULL: N*N*4 bytes < 2^31)
+  const __amdgpu_buffer_rsrc_t lrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Lb, 0, 0x7fffffff, 0x00020000);
+  auto lbuf_load = [&](int off) -> f32x4 {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lrsrc, 4 * off, 0, 0));
+  };
+  auto vm_drain = [&]() { __builtin_amdgcn_s_waitcnt(0x0F70); };   // vmcnt(0) only
   auto fetch_row = [&](const int I) -> f32x4 {    // tiles (I, K < I), row-major
     if (tid >= I * 64 || (GPK_GRAD_SKIP & 4)) return z4;
     const int K = tid >> 6, q = tid & 63, m = q >> 2, cg = (q & 3) * 4;
     const int row = 16 * I + m, col0 = 16 * K + cg;
-    if (FULL) return *(const f32x4*)&Lb[(size_t)row * N + col0];
+    if (FULL) return lbuf_load(row * N + col0);
     f32x4 v;
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = (row < N && col0 + j < N) ? Lb[(size_t)row * N + col0 + j] : 0.f;
@@ -205,13 +285,19 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
   auto put_row = [&](float* buf, const int I, const f32x4 v) {
     if (tid >= I * 64) return;
     const int K = tid >> 6, q = tid & 63, m = q >> 2, cg = (q & 3) * 4;
-    *(f32x4*)&buf[K * 256 + m * 16 + cg] = v;
+    if constexpr (SPLIT) {   // reader lane (g, c) = (q & 3, m) takes row m, columns 4g..4g+3
+      half4_t h, l;
+      (void)round_split_f16(v, h, l);
+      store_split_planes(buf + K * 256, 16 * (q & 3) + m, h, l);
+    } else {
+      *(f32x4*)&buf[K * 256 + m * 16 + cg] = v;
+    }
   };
   auto fetch_col = [&](const int I) -> f32x4 {    // tiles (K > I, I), read by rows
     if (tid >= (NB - 1 - I) * 64 || (GPK_GRAD_SKIP & 4)) return z4;
     const int sl = tid >> 6, q = tid & 63, k = q >> 2, cg = (q & 3) * 4;
     const int row = 16 * (I + 1 + sl) + k, col0 = 16 * I + cg;
-    if (FULL) return *(const f32x4*)&Lb[(size_t)row * N + col0];
+    if (FULL) return lbuf_load(row * N + col0);
     f32x4 v;
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = (row < N && col0 + j < N) ? Lb[(size_t)row * N + col0 + j] : 0.f;
@@ -221,102 +307,163 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
     if (tid >= (NB - 1 - I) * 64) return;
     const int sl = tid >> 6, q = tid & 63, k = q >> 2, cg = (q & 3) * 4;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) buf[sl * 256 + (cg + j) * 16 + k] = v[j];
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (SPLIT)   // element (k, cg + j) is reg k & 3 of lane 16 (k >> 2) + cg + j
+        put_split_elem(buf + sl * 256, 16 * (k >> 2) + cg + j, k & 3, v[j]);
+      else
+        buf[sl * 256 + (cg + j) * 16 + k] = v[j];
+    }
   };
-  f32x4 X[NB];
+  // X[K]: the wave's tile of block row K (V, then U = K^-1), an MFMA B operand: fp32 acc
+  // layout, or split-f16 {hi, lo} (GPK_GRAD_SPLIT)
+  using XT = typename std::conditional<SPLIT, half8_t, f32x4>::type;
+  constexpr int NCH = SPLIT ? 2 : 4;   // independent MFMA accumulator chains
+  // X[K < J] stay zero: a wave may run the products of a whole group of 4 tiles (below)
+  XT X[NB];
+  sfor<0, NB - 1>([&](auto Kc) { X[decltype(Kc)::value] = XT{}; });
+  const float* dsa = smem + lay.dsa;
+  const float* dsb = smem + lay.dsb;
+  // s[K % NCH] += Q_K^T X[K] for K in [KLO, KHI], Q_K the staged tile at base + (K - KOFS)
+  // tiles, in groups of 4 tiles (one wave-uniform branch per group, kmin <= the group's last
+  // K): the group's LDS operands are all loaded before its MFMAs, so the LDS latency is paid
+  // once per group, not once per product
+  auto prod_range = [&](f32x4* s, const float* base, auto KLOc, auto KHIc, auto KOFSc, int kmin) {
+    constexpr int KLO = decltype(KLOc)::value, KHI = decltype(KHIc)::value;
+    constexpr int KOFS = decltype(KOFSc)::value;
+    sfor<0, (KHI - KLO + 4) / 4 - 1>([&](auto Qc) {
+      constexpr int K0 = KLO + 4 * decltype(Qc)::value;
+      constexpr int K1 = (K0 + 3 < KHI) ? K0 + 3 : KHI;
+      if (kmin <= K1) {
+        XT op[4];
+        sfor<K0, K1>([&](auto Kc) {
+          constexpr int K = decltype(Kc)::value;
+          const float* tile = base + (K - KOFS) * 256;
+          if constexpr (SPLIT) op[K - K0] = load_split_hl(tile, lane);
+          else op[K - K0] = *(const f32x4*)&tile[c * 16 + 4 * g];
+        });
+        sfor<K0, K1>([&](auto Kc) {
+          constexpr int K = decltype(Kc)::value;
+          if constexpr (SPLIT) s[K % NCH] = mma_split(op[K - K0], X[K], s[K % NCH]);
+          else s[K % NCH] = mfma4(op[K - K0], X[K], s[K % NCH]);
+        });
+      }
+    });
+  };
   // Step s reads buffer s & 1: phase 1 step I (s = I) block row I, phase 2 step I
   // (s = 2NB-1-I) block column I. The tiles of step s+2 are fetched during step s and
   // written into buffer s & 1 after the step's barrier (everyone is done reading it).
+  unsigned long long* stamps = (unsigned long long*)(a.dX + (size_t)b * N * D);
+  auto stamp = [&](int st, int ev) {
+    if constexpr (GPK_GRAD_STAMPS) {
+      if (lane == 0) stamps[(st * kSW + wave) * 4 + ev] = __builtin_amdgcn_s_memtime();
+    }
+  };
+  f32x4 al = z4;   // alpha block J (column 0 of the acc tile)
   if (NB > 1) put_row(stg + TS, 1, fetch_row(1));
   lds_barrier();
-#pragma unroll
-  for (int I = 0; I < NB; ++I) {
+  sfor<0, NB - 1>([&](auto Ic) {
+    constexpr int I = decltype(Ic)::value;
+    stamp(I, 0);
     const f32x4 nxt = (I + 2 < NB) ? fetch_row(I + 2) : ((I + 2 == NB + 1 && NB >= 2) ? fetch_col(NB - 2) : z4);
     const float* buf = stg + (I & 1) * TS;
     const int I16 = opaque_s(16 * I);
     if (live && !(GPK_GRAD_SKIP & 1)) {
       if (I == J) {
+        if constexpr (SPLIT) {
+          X[I] = load_split_hl(dsb + I16 * 16, lane);
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) X[I][r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
+          for (int r = 0; r < 4; ++r) X[I][r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
+        }
       } else if (I > J) {
         f32x4 s[4] = {z4, z4, z4, z4};   // 4 independent MFMA chains
-#pragma unroll
-        for (int K = 0; K < I; ++K) {
-          if (K >= J) {
-            const f32x4 la = *(const f32x4*)&buf[K * 256 + c * 16 + 4 * g];
-            s[K & 3] = mfma4(la, X[K], s[K & 3]);
-          }
+        prod_range(s, buf, IdxC<0>{}, IdxC<I - 1>{}, IdxC<0>{}, J);
+        const f32x4 t = (NCH == 4 ? (s[0] + s[1]) + (s[2] + s[3]) : (NCH == 2 ? s[0] + s[1] : s[0]));
+        if constexpr (SPLIT) {
+          X[I] = to_split(-mma_split(load_split_hl(dsa + I16 * 16, lane), to_split(t), z4));
+        } else {
+          const f32x4 di = *(const f32x4*)&dinv[I16 * 16 + c * 16 + 4 * g];
+          X[I] = -mfma4(di, t, z4);
         }
-        const f32x4 di = *(const f32x4*)&dinv[I16 * 16 + c * 16 + 4 * g];
-        X[I] = -mfma4(di, (s[0] + s[1]) + (s[2] + s[3]), z4);
+      }
+      // alpha_J += V_IJ^T z_I  (alpha = L^-T z = V^T z, block J; z_I in column 0 of a tile)
+      if (I >= J && !(GPK_GRAD_SKIP & 16)) {
+        f32x4 zt;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zt[r] = c == 0 ? sv[16 * I + 4 * g + r] : 0.f;
+        if constexpr (SPLIT) al = mma_split(X[I], to_split(zt), al);
+        else al = mfma4(X[I], zt, al);
       }
     }
+    stamp(I, 1);
     lds_barrier();
+    stamp(I, 2);
     if (I + 2 < NB) put_row(stg + (I & 1) * TS, I + 2, nxt);
     else if (I + 2 == NB + 1 && NB >= 2) put_col(stg + (I & 1) * TS, NB - 2, nxt);   // step 2NB-1-(NB-2)
+    vm_drain();
+    stamp(I, 3);
+  });
+  // alpha block J -> workspace, dy; per-wave partial of sum(alpha) (summed after phase 2)
+  if (live) {
+    float asp = 0.f;
+    if (c == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * J + 4 * g + r;
+        const float an = al[r];
+        wsb[ws.alpha + n] = an;
+        if (FULL || n < N) {
+          asp += an;
+          if (a.dy != nullptr) a.dy[(size_t)b * N + n] = -gw * an * invN;
+        }
+      }
+    }
+    asp = wave_sum(asp);
+    if (lane == 0) red[J] = asp;
   }
   lds_barrier();
+  // U_I = Linv_II^T t  (Q = Linv_II)
+  auto back_tile = [&](const int I16, const f32x4 t) -> f32x4 {
+    if constexpr (SPLIT) {
+      return mma_split(load_split_hl(dsb + I16 * 16, lane), to_split(t), z4);
+    } else {
+      f32x4 dt;
 #pragma unroll
-  for (int I = NB - 1; I >= 0; --I) {
+      for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
+      return mfma4(dt, t, z4);
+    }
+  };
+  auto as_f32 = [&](const XT& x) -> f32x4 {
+    if constexpr (SPLIT) return from_split(x); else return x;
+  };
+  auto as_x = [&](const f32x4 v) -> XT {
+    if constexpr (SPLIT) return to_split(v); else return v;
+  };
+  sfor<0, NB - 1>([&](auto Tc) {
+    constexpr int I = NB - 1 - decltype(Tc)::value;
     const int st = 2 * NB - 1 - I;
+    stamp(st, 0);
     const f32x4 nxt = (I > 1) ? fetch_col(I - 2) : z4;
     const float* buf = stg + (st & 1) * TS;
     const int I16 = opaque_s(16 * I);
     if (live && I >= J && !(GPK_GRAD_SKIP & 2)) {
       f32x4 s[4] = {z4, z4, z4, z4};   // 4 independent MFMA chains
-#pragma unroll
-      for (int K = I + 1; K < NB; ++K) {
-        const f32x4 la = *(const f32x4*)&buf[(K - I - 1) * 256 + c * 16 + 4 * g];
-        s[K & 3] = mfma4(la, X[K], s[K & 3]);
-      }
-      const f32x4 t = X[I] - ((s[0] + s[1]) + (s[2] + s[3]));
-      f32x4 dt;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
-      const f32x4 U = mfma4(dt, t, z4);
-      X[I] = U;
+      prod_range(s, buf, IdxC<I + 1>{}, IdxC<NB - 1>{}, IdxC<I + 1>{}, 0);
+      const f32x4 U = back_tile(I16, as_f32(X[I]) - ((NCH == 4 ? (s[0] + s[1]) + (s[2] + s[3]) : (NCH == 2 ? s[0] + s[1] : s[0]))));
+      X[I] = as_x(U);
       if (!(GPK_GRAD_SKIP & 8)) *(f32x4*)&wsb[ws.kinv + (size_t)tile_index(I, J) * 256 + lane * 4] = U;
     }
-    // alpha = L^-T z by the same back substitution (right-hand side z in column 0 of the
-    // tiles), run by wave AW: an idle wave when NB < 16, else wave 15 once its own
-    // column (one tile, step NB-1) is done
-    if (wave == AW && !(GPK_GRAD_SKIP & 18)) {
-      if (I == NB - 1) {
-#pragma unroll
-        for (int K = 0; K < NB; ++K)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) X[K][r] = c == 0 ? sv[16 * K + 4 * g + r] : 0.f;
-      }
-      f32x4 s[4] = {z4, z4, z4, z4};   // 4 independent MFMA chains
-#pragma unroll
-      for (int K = I + 1; K < NB; ++K) {
-        const f32x4 la = *(const f32x4*)&buf[(K - I - 1) * 256 + c * 16 + 4 * g];
-        s[K & 3] = mfma4(la, X[K], s[K & 3]);
-      }
-      const f32x4 t = X[I] - ((s[0] + s[1]) + (s[2] + s[3]));
-      f32x4 dt;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dt[r] = dinv[I16 * 16 + (4 * g + r) * 16 + c];
-      X[I] = mfma4(dt, t, z4);
-      if (c == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = 16 * I + 4 * g + r;
-          const float an = X[I][r];
-          wsb[ws.alpha + n] = an;
-          if (FULL || n < N) {
-            asum += an;
-            if (a.dy != nullptr) a.dy[(size_t)b * N + n] = -gw * an * invN;
-          }
-        }
-      }
-    }
+    stamp(st, 1);
     lds_barrier();
+    stamp(st, 2);
     if (I > 1 && !(GPK_GRAD_SKIP & 32)) put_col(stg + (st & 1) * TS, I - 2, nxt);
-  }
-  if (wave == AW) {
-    asum = wave_sum(asum);
-    if (lane == 0) wsb[ws.asum] = asum;
+    vm_drain();
+    stamp(st, 3);
+  });
+  if (tid == 0) {   // fixed-order sum of the per-block partials (deterministic)
+    float asum = 0.f;
+    for (int j = 0; j < NB; ++j) asum += red[j];
+    wsb[ws.asum] = asum;
   }
 }
 
@@ -449,7 +596,7 @@ __global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : 8) gpk_grad_gram_kerne
       const float x = xs[row * XS + d];
       const float e = x * w1r[r] - wx[q][r];   // = -dxs / 2
       if ((FULL || row < N) && d < D) {
-        if (a.dX != nullptr) a.dX[((size_t)b * N + row) * D + d] = -2.f * e * ilq;
+        if (a.dX != nullptr && !GPK_GRAD_STAMPS) a.dX[((size_t)b * N + row) * D + d] = -2.f * e * ilq;
         lp = __builtin_fmaf(x, e, lp);
       }
     }

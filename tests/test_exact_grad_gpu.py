@@ -156,3 +156,34 @@ def test_exact_grad_full_bench_batch(cuda_device):
         for k in got:
             e = _rel(got[k], ref[k])
             assert e <= TOL, (w, k, e)
+
+
+@pytest.mark.parametrize("noise", [1e-2, 1e-3])
+def test_exact_grad_ill_conditioned_vs_fp32_reference(cuda_device, noise):
+    """Small noise (cond(K_hat) ~ 1e3..1e4 at N=128): the HIP backward's error vs the fp64
+    oracle must stay within 1e-4 or within 3x of what the reference's own fp32 arithmetic
+    (torch fp32 autograd through cholesky) achieves on the same windows."""
+    from fine_grained_gaussian_process_forcasting_amd import ops
+    B, N, D = 2, 128, 8
+    g = torch.Generator().manual_seed(77)
+    X = torch.randn(B, N, D, generator=g) / np.sqrt(D)
+    y = torch.randn(B, N, generator=g)
+    s2, c = 1.0, 0.1
+    gout = torch.rand(B, generator=g) + 0.5
+    dev = cuda_device
+    hyper = ops.pack_exact_hyper(s2, noise, c, LN2, dev)
+    fw = ops.exact_mll(X.to(dev), y.to(dev), None, None, None, None, hyper=hyper, want_L=True, want_z=True)
+    assert (fw.info.cpu() == 0).all()
+    gr = ops.exact_mll_grad(X.to(dev), fw.L, fw.z, hyper, gout.to(dev))
+    torch.cuda.synchronize()
+    ref = O.exact_mll_grads(X.double().numpy(), y.double().numpy(), LN2, s2, c, noise,
+                            gout=gout.double().numpy())
+    dh = gr.dhyp.sum(0).cpu().double().numpy()
+    got = {"X": gr.dX.cpu().numpy(), "y": gr.dy.cpu().numpy(), "outputscale": dh[0], "noise": dh[1],
+           "mean_constant": dh[2], "lengthscale": dh[3]}
+    f32 = _fp32_torch_grads(X, y, LN2, s2, c, noise, gout)
+    for k in got:
+        e = _rel(got[k], ref[k])
+        e32 = _rel(f32[k], ref[k])
+        print(f"noise={noise} {k:14s} hip {e:.2e}   torch-fp32 {e32:.2e}")
+        assert e <= max(TOL, 3 * e32), (k, e, e32)
