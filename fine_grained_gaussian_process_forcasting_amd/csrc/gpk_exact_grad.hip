@@ -14,7 +14,7 @@
 // linear_operator inv_quad_logdet + psd_safe_cholesky backward) when train.py:166
 // calls loss.backward(); oracle: oracle/gp_oracle.py::exact_mll_grads.
 //
-// Three launches, inputs are the forward's L and z (nothing is refactored):
+// Two launches (three in the fp32 form), inputs are the forward's L and z (nothing is refactored):
 //   gpk_grad_solve_kernel  one workgroup (16 waves) per window: alpha = L^-T z, dy, and the
 //       lower block tiles of K^-1: wave J solves block column J with its tiles in registers
 //         forward   V_I = -Linv_II sum_{K=J}^{I-1} L_IK V_K       (I > J, V_J = Linv_JJ)
@@ -24,11 +24,12 @@
 //       column of L is staged once in LDS (as split planes) by the workgroup, fetched two
 //       steps ahead (double buffer); the diagonal-block inverses Linv_II live in LDS.
 //       U_I = K^-1_IJ -> workspace.
-//   gpk_grad_gram_kernel   one wave per (window, block row I), no atomics: for every J the
-//       tile K^-1_JI (stored, or the transpose of the stored K^-1_IJ), the RBF tile
-//       recomputed from xs (fp32-MFMA Gram), G, W and Wx_I += W_JI^T xs_J (MFMA), w1_I;
-//       then dX of rows I and the block row's partials of ds2, dnoise, dl.
-//   gpk_grad_fin_kernel    fixed-order sums of the partials -> dhyp (deterministic).
+//   gpk_grad_gram_split_kernel (gpk_grad_gram_kernel: the fp32 form) one wave per (window,
+//       block row I), no atomics: for every J the tile K^-1_JI (stored, or the transpose of
+//       the stored K^-1_IJ), the RBF tile recomputed from xs (split-f16 MFMA Gram), G, W and
+//       Wx_I += W_JI^T xs_J (split-f16 MFMA, W scaled by a power of two), w1_I; then dX of
+//       rows I and the block row's partials of ds2, dnoise, dl, summed in a fixed order by
+//       the same workgroup -> dhyp (deterministic; gpk_grad_fin_kernel in the fp32 form).
 #include "gpk_common.h"
 #include "gpk_internal.h"
 
@@ -51,6 +52,10 @@
 // Timeline builds (GPK_GRAD_STAMPS=1, timing only): the solve kernel writes s_memtime
 // stamps into dX (which the gram kernel then leaves alone): per window, per step s (0..2NB-1),
 // per wave, 4 events (step start, math done, barrier passed, staging stored).
+#ifndef GPK_GRAM_WPE
+#define GPK_GRAM_WPE 4   // split gram kernel, D <= 32: waves per SIMD it is compiled for (8: spills,
+                         // 0.167 vs 0.139 ms for the whole backward)
+#endif
 #ifndef GPK_GRAD_STAMPS
 #define GPK_GRAD_STAMPS 0
 #endif
@@ -612,6 +617,252 @@ __global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : 8) gpk_grad_gram_kerne
   }
 }
 
+// Split-f16 form of the same contractions (GPK_GRAD_SPLIT): xs is staged ONCE as hi + lo f16
+// planes in two layouts -- rows (the Gram operands: lane (g, c) takes dims 8g..8g+7 of a row)
+// and columns (the Wx operand: lane (g, c) takes rows 4g..4g+3 of a dim) -- so the RBF Gram
+// is 3 K=32 f16 MFMAs per 32 dims (hi.hi + hi.lo + lo.hi, as the forward builds K) and
+// Wx_I += W_JI^T xs_J is 2 per 16 dims (exact products of the split W and xs), against 8 + 8
+// fp32 MFMAs. Norms and the dX epilogue use the rounded xs^ = hi + lo (22 bits).
+struct GramLds {
+  int RS, TSd, xh, xl, th, tl, nrm, al, bmax, part, total_bytes;
+};
+__host__ __device__ inline GramLds gram_lds(int NP, int DQ) {
+  GramLds o;
+  const int DP = 16 * DQ, DW = DP < 32 ? 32 : DP;
+  o.RS = DW + 8;          // row-plane stride (halves): 16-B reads of 8 rows conflict-free
+  o.TSd = NP + 16;        // column-plane stride (halves): 8-B reads of 32 lanes conflict-free
+  o.xh = 0;               // offsets in halves
+  o.xl = o.xh + NP * o.RS;
+  o.th = o.xl + NP * o.RS;
+  o.tl = o.th + DP * o.TSd;
+  const int fl = ((o.tl + DP * o.TSd) * 2 + 15) / 16 * 4;   // float offset, 16-B aligned
+  o.nrm = fl;
+  o.al = o.nrm + NP;
+  o.bmax = o.al + NP;          // 2 x 16 block-max slots
+  o.part = o.bmax + 32;        // NB x (2 + DP) block-row partials (ds2, dnoise, dl[d])
+  o.total_bytes = (o.part + (NP / 16) * (2 + DP)) * 4;
+  return o;
+}
+
+template <int DQ, bool FULL>
+__global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : GPK_GRAM_WPE) gpk_grad_gram_split_kernel(GpkExactGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int DP = 16 * DQ, DW = DP < 32 ? 32 : DP, KC = DW / 32;
+  const int N = a.N, D = a.D;
+  const GradWs ws = grad_ws(N);
+  const int NB = ws.NB, NP = 16 * NB;
+  const GramLds lay = gram_lds(NP, DQ);
+  const int RS = lay.RS, TSd = lay.TSd;
+  _Float16* hs = (_Float16*)smem;
+  _Float16* xh = hs + lay.xh;
+  _Float16* xl = hs + lay.xl;
+  _Float16* th = hs + lay.th;
+  _Float16* tl = hs + lay.tl;
+  float* nrm = smem + lay.nrm;
+  float* al = smem + lay.al;
+  const int tid = threadIdx.x, lane = tid & 63, I = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const float* Xb = a.X + (size_t)b * N * D;
+  const float* wsb = a.ws + (size_t)b * ws.per;
+  const float* hyp = a.hyp;
+  const bool ard = a.n_ls > 1;
+  // xs = x / l - mean -> split planes (rows: dims 0..DW-1, zero padded; columns: dims < DP)
+  for (int base = 0; base < NP * DW; base += 4 * 64 * kGW) {
+    float v[4], l[4], mu[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = base + u * 64 * kGW + tid, n = e / DW, d = e - n * DW;
+      const bool ok = e < NP * DW && (FULL || n < N) && d < D;
+      v[u] = Xb[ok ? (size_t)n * D + d : 0];
+      l[u] = hyp[3 + ((ok && ard) ? d : 0)];
+      mu[u] = wsb[ws.mean + (ok ? d : 0)];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = base + u * 64 * kGW + tid, n = e / DW, d = e - n * DW;
+      if (e < NP * DW) {
+        const float x = ((FULL || n < N) && d < D) ? v[u] / l[u] - mu[u] : 0.f;
+        const _Float16 h = (_Float16)x, lo = (_Float16)(x - (float)h);
+        xh[n * RS + d] = h;
+        xl[n * RS + d] = lo;
+        if (d < DP) {
+          th[d * TSd + n] = h;
+          tl[d * TSd + n] = lo;
+        }
+      }
+    }
+  }
+  // W = G s2 E is scaled by a power of two S before its hi + lo split, so that its largest
+  // entries sit near 2^10 (f16 keeps their lo part normal; W itself is ~1/N-sized and its lo
+  // part would underflow): |W_ij| <= |gs| s2 (max|alpha|^2 + max_j K^-1_jj)
+  float* bmax = smem + lay.bmax;
+  float* pl = smem + lay.part;
+  float am = 0.f, tm = 0.f;
+  for (int n = tid; n < NP; n += 64 * kGW) {
+    const float an = wsb[ws.alpha + n];
+    al[n] = an;
+    am = __builtin_fmaxf(am, __builtin_fabsf(an));
+    const int Jn = n >> 4, m = n & 15;
+    tm = __builtin_fmaxf(tm, __builtin_fabsf(wsb[ws.kinv + (size_t)tile_index(Jn, Jn) * 256 +
+                                                 (16 * (m >> 2) + m) * 4 + (m & 3)]));
+  }
+  am = wave_max(am);
+  tm = wave_max(tm);
+  if (lane == 0) {
+    bmax[I] = am;
+    bmax[16 + I] = tm;
+  }
+  lds_barrier();
+  for (int n = tid; n < NP; n += 64 * kGW) {
+    float t = 0.f;
+#pragma unroll
+    for (int d = 0; d < DW; ++d) {
+      const float x = (float)xh[n * RS + d] + (float)xl[n * RS + d];
+      t = __builtin_fmaf(x, x, t);
+    }
+    nrm[n] = t;
+  }
+  lds_barrier();
+  const float s2 = hyp[0];
+  const float gw = a.gout[b];
+  const float gs = gw / (2.f * (float)N);
+  float wscale = 1.f;
+  {
+    float amax = 0.f, tmax = 0.f;
+    for (int w = 0; w < kGW; ++w) {
+      amax = __builtin_fmaxf(amax, bmax[w]);
+      tmax = __builtin_fmaxf(tmax, bmax[16 + w]);
+    }
+    const float bound = __builtin_fabsf(gs) * __builtin_fabsf(s2) * (amax * amax + tmax);
+    if (bound > 0.f && bound < 3.0e38f)
+      wscale = __builtin_ldexpf(1.f, 10 - (int)__builtin_ceilf(__builtin_log2f(bound)));
+  }
+  constexpr float nhalf_log2e = -0.72134752044448170f;
+  if (I < NB) {   // wave-uniform (the waves of a short window still meet the final barrier)
+  // Gram B operand for the columns i = 16I + c: dims 32kc + 8g .. +7 of row i
+  half8_t bh[KC], bl[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    bh[kc] = *(const half8_t*)&xh[(16 * I + c) * RS + 32 * kc + 8 * g];
+    bl[kc] = *(const half8_t*)&xl[(16 * I + c) * RS + 32 * kc + 8 * g];
+  }
+  const int col = 16 * I + c;
+  const float ni = nrm[col], ai = al[col];
+  f32x4 wx[DQ];
+#pragma unroll
+  for (int q = 0; q < DQ; ++q) wx[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float w1p = 0.f, ds2 = 0.f, dnz = 0.f;
+  auto load_T = [&](int J) -> f32x4 {   // K^-1_JI in acc layout (rows j, cols i)
+    f32x4 T;
+    if (J >= I) {
+      T = *(const f32x4*)&wsb[ws.kinv + (size_t)tile_index(J, I) * 256 + lane * 4];
+    } else {
+      const float* t = wsb + ws.kinv + (size_t)tile_index(I, J) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[r] = t[((c >> 2) * 16 + 4 * g + r) * 4 + (c & 3)];
+    }
+    return T;
+  };
+  f32x4 Tn = load_T(0);
+  for (int J = 0; J < NB; ++J) {
+    const f32x4 T = Tn;
+    if (J + 1 < NB) Tn = load_T(J + 1);
+    const int j0 = 16 * J;
+    f32x4 gr = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const half8_t ah = *(const half8_t*)&xh[(j0 + c) * RS + 32 * kc + 8 * g];
+      const half8_t alo = *(const half8_t*)&xl[(j0 + c) * RS + 32 * kc + 8 * g];
+      gr = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[kc], gr, 0, 0, 0);
+      gr = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[kc], gr, 0, 0, 0);
+      gr = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[kc], gr, 0, 0, 0);
+    }
+    half8_t pj[DQ];   // xs_J columns 16q + c, rows j0 + 4g .. +3 (hi | lo)
+#pragma unroll
+    for (int q = 0; q < DQ; ++q) {
+      const half4_t h4 = *(const half4_t*)&th[(16 * q + c) * TSd + j0 + 4 * g];
+      const half4_t l4 = *(const half4_t*)&tl[(16 * q + c) * TSd + j0 + 4 * g];
+      pj[q] = half8_t{h4[0], h4[1], h4[2], h4[3], l4[0], l4[1], l4[2], l4[3]};
+    }
+    const f32x4 aj = *(const f32x4*)&al[j0 + 4 * g];
+    const f32x4 nj = *(const f32x4*)&nrm[j0 + 4 * g];
+    f32x4 W;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = j0 + 4 * g + r;
+      float G = (aj[r] * ai - T[r]) * gs;
+      if (!FULL && (row >= N || col >= N)) G = 0.f;
+      float d2 = __builtin_fmaxf(nj[r] + ni - 2.f * gr[r], 0.f);
+      if (row == col) d2 = 0.f;
+      const float E = __builtin_amdgcn_exp2f(d2 * nhalf_log2e);
+      ds2 = __builtin_fmaf(G, E, ds2);
+      if (row == col) dnz += G;
+      W[r] = (row == col) ? 0.f : G * s2 * E;
+    }
+    w1p += (W[0] + W[1]) + (W[2] + W[3]);
+    // Wx_I += W_JI^T xs_J  (rows i, dims): split W times split xs, exact products
+    const half8_t ws8 = to_split(W * wscale);
+#pragma unroll
+    for (int q = 0; q < DQ; ++q) wx[q] = mma_split(ws8, pj[q], wx[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < DQ; ++q) wx[q] = wx[q] * (1.f / wscale);   // (exact: a power of two)
+  w1p += __shfl_xor(w1p, 16, 64);
+  w1p += __shfl_xor(w1p, 32, 64);
+  float w1r[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) w1r[r] = __shfl(w1p, 4 * g + r, 64);
+  float* part = pl + I * (2 + DP);
+#pragma unroll
+  for (int q = 0; q < DQ; ++q) {
+    const int d = 16 * q + c;
+    const float ilq = d < D ? 1.f / hyp[3 + (ard ? d : 0)] : 0.f;
+    float lp = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * I + 4 * g + r;
+      const float x = (float)xh[row * RS + d] + (float)xl[row * RS + d];
+      const float e = x * w1r[r] - wx[q][r];   // = -dxs / 2
+      if ((FULL || row < N) && d < D) {
+        if (a.dX != nullptr && !GPK_GRAD_STAMPS) a.dX[((size_t)b * N + row) * D + d] = -2.f * e * ilq;
+        lp = __builtin_fmaf(x, e, lp);
+      }
+    }
+    lp += __shfl_xor(lp, 16, 64);
+    lp += __shfl_xor(lp, 32, 64);
+    if (g == 0) part[2 + d] = lp;
+  }
+  ds2 = wave_sum(ds2);
+  dnz = wave_sum(dnz);
+  if (lane == 0) {
+    part[0] = ds2;
+    part[1] = dnz;
+  }
+  }
+  // fixed-order sums of the block-row partials -> dhyp (gpk_grad_fin_kernel, fused)
+  lds_barrier();
+  if (tid < 128) {
+    float* o = a.dhyp + (size_t)b * (3 + a.n_ls);
+    const int t = tid;
+    const int f = t < 64 ? (t < D ? 2 + t : -1) : (t == 64 ? 0 : (t == 65 ? 1 : -1));
+    float sacc = 0.f;
+    if (f >= 0)
+      for (int I2 = 0; I2 < NB; ++I2) sacc += pl[I2 * (2 + DP) + f];
+    if (t == 64) o[0] = sacc;
+    if (t == 65) o[1] = sacc;
+    if (t == 66) o[2] = gw * wsb[ws.asum] / (float)N;
+    if (t < 64) {
+      if (a.n_ls == 1) {
+        const float tot = wave_sum(sacc);
+        if (t == 0) o[3] = 2.f * tot / hyp[3];
+      } else if (t < D) {
+        o[3 + t] = 2.f * sacc / hyp[3 + t];
+      }
+    }
+  }
+}
+
 // ======================================================================================
 // 3. fixed-order sums of the block-row partials -> dhyp
 // ======================================================================================
@@ -664,6 +915,23 @@ int launch_solve(const GpkExactGradArgs& a, hipStream_t stream) {
 template <int DQ>
 int launch_gram(const GpkExactGradArgs& a, hipStream_t stream) {
   const int NB = (a.N + 15) / 16;
+  if (GPK_GRAD_SPLIT) {
+    const size_t lds = (size_t)gram_lds(16 * NB, DQ).total_bytes;
+    if (lds > 160 * 1024) return -7;
+    static std::once_flag once_s;
+    std::call_once(once_s, [&] {
+      (void)hipFuncSetAttribute((const void*)gpk_grad_gram_split_kernel<DQ, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)gpk_grad_gram_split_kernel<DQ, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipGetLastError();
+    });
+    if (a.N == 16 * NB)
+      hipLaunchKernelGGL((gpk_grad_gram_split_kernel<DQ, true>), dim3(a.B), dim3(64 * kGW), lds, stream, a);
+    else
+      hipLaunchKernelGGL((gpk_grad_gram_split_kernel<DQ, false>), dim3(a.B), dim3(64 * kGW), lds, stream, a);
+    return (int)hipGetLastError();
+  }
   const size_t lds = sizeof(float) * (size_t)(16 * NB) * (16 * DQ + 4 + 2);
   static std::once_flag once;
   std::call_once(once, [&] {
@@ -699,6 +967,7 @@ int gpk_launch_exact_grad(const GpkExactGradArgs& a, hipStream_t stream) {
   if (rc != 0) return rc;
   rc = a.D <= 16 ? launch_gram<1>(a, stream) : (a.D <= 32 ? launch_gram<2>(a, stream) : launch_gram<4>(a, stream));
   if (rc != 0) return rc;
-  hipLaunchKernelGGL(gpk_grad_fin_kernel, dim3(a.B), dim3(128), 0, stream, a, 0);
+  if (!GPK_GRAD_SPLIT)   // (the split gram kernel sums its partials itself)
+    hipLaunchKernelGGL(gpk_grad_fin_kernel, dim3(a.B), dim3(128), 0, stream, a, 0);
   return (int)hipGetLastError();
 }
