@@ -38,7 +38,8 @@
 
 // Timing experiments only (A/B builds of the solve kernel; results are wrong when set):
 // bit 1 skips the phase-1 tile math, 2 the phase-2 tile math, 4 the L staging, 8 the
-// K^-1 tile stores, 16 the alpha products, 32 the phase-2 staging stores.
+// K^-1 tile stores, 16 the alpha products, 32 the phase-2 staging stores, 64 the split gram
+// kernel's J loop.
 #ifndef GPK_GRAD_SKIP
 #define GPK_GRAD_SKIP 0
 #endif
@@ -765,7 +766,7 @@ __global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : GPK_GRAM_WPE) gpk_grad
     return T;
   };
   f32x4 Tn = load_T(0);
-  for (int J = 0; J < NB; ++J) {
+  for (int J = 0; J < ((GPK_GRAD_SKIP & 64) ? 0 : NB); ++J) {
     const f32x4 T = Tn;
     if (J + 1 < NB) Tn = load_T(J + 1);
     const int j0 = 16 * J;

@@ -50,7 +50,8 @@ def _fp32_torch_grads(X, y, ls, s2, c, noise, gout):
 
 
 @pytest.mark.parametrize("B,N,D,ard", [(3, 16, 4, False), (2, 37, 5, True), (4, 64, 8, False),
-                                       (2, 96, 32, False), (2, 256, 32, False), (2, 250, 7, True)])
+                                       (2, 96, 32, False), (2, 256, 32, False), (2, 250, 7, True),
+                                       (2, 80, 48, True), (2, 256, 64, False)])
 def test_exact_grad_abi_vs_oracle(cuda_device, B, N, D, ard):
     from fine_grained_gaussian_process_forcasting_amd import ops
     g = torch.Generator().manual_seed(B * 100 + N)
