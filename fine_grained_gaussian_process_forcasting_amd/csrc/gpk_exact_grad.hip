@@ -299,25 +299,46 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
       *(f32x4*)&buf[K * 256 + m * 16 + cg] = v;
     }
   };
-  auto fetch_col = [&](const int I) -> f32x4 {    // tiles (K > I, I), read by rows
+  auto fetch_col = [&](const int I) -> f32x4 {    // tiles (K > I, I)
     if (tid >= (NB - 1 - I) * 64 || (GPK_GRAD_SKIP & 4)) return z4;
-    const int sl = tid >> 6, q = tid & 63, k = q >> 2, cg = (q & 3) * 4;
-    const int row = 16 * (I + 1 + sl) + k, col0 = 16 * I + cg;
-    if (FULL) return lbuf_load(row * N + col0);
-    f32x4 v;
+    const int sl = tid >> 6, q = tid & 63;
+    if constexpr (SPLIT) {
+      // lane (g, c) = (q >> 4, q & 15) loads the column segment L_KI[4g .. 4g+3][c] (rows of
+      // the acc layout): 4 dword loads, each 16 lanes reading 64 contiguous bytes, so the
+      // staging store is two 8-byte split-plane writes instead of eight 2-byte scatters
+      const int g4 = 4 * (q >> 4), cc = q & 15;
+      const int row0 = 16 * (I + 1 + sl) + g4, col = 16 * I + cc;
+      f32x4 v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (row < N && col0 + j < N) ? Lb[(size_t)row * N + col0 + j] : 0.f;
-    return v;
+      for (int r = 0; r < 4; ++r) {
+        if (FULL) {
+          v[r] = Lb[opaque_v((row0 + r) * N + col)];
+        } else {
+          v[r] = (row0 + r < N && col < N) ? Lb[(size_t)(row0 + r) * N + col] : 0.f;
+        }
+      }
+      return v;
+    } else {
+      const int k = q >> 2, cg = (q & 3) * 4;
+      const int row = 16 * (I + 1 + sl) + k, col0 = 16 * I + cg;
+      if (FULL) return lbuf_load(row * N + col0);
+      f32x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (row < N && col0 + j < N) ? Lb[(size_t)row * N + col0 + j] : 0.f;
+      return v;
+    }
   };
   auto put_col = [&](float* buf, const int I, const f32x4 v) {   // stored transposed
     if (tid >= (NB - 1 - I) * 64) return;
-    const int sl = tid >> 6, q = tid & 63, k = q >> 2, cg = (q & 3) * 4;
+    const int sl = tid >> 6, q = tid & 63;
+    if constexpr (SPLIT) {   // v is already the acc-layout column segment of lane q
+      half4_t h, l;
+      (void)round_split_f16(v, h, l);
+      store_split_planes(buf + sl * 256, q, h, l);
+    } else {
+      const int k = q >> 2, cg = (q & 3) * 4;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if constexpr (SPLIT)   // element (k, cg + j) is reg k & 3 of lane 16 (k >> 2) + cg + j
-        put_split_elem(buf + sl * 256, 16 * (k >> 2) + cg + j, k & 3, v[j]);
-      else
-        buf[sl * 256 + (cg + j) * 16 + k] = v[j];
+      for (int j = 0; j < 4; ++j) buf[sl * 256 + (cg + j) * 16 + k] = v[j];
     }
   };
   // X[K]: the wave's tile of block row K (V, then U = K^-1), an MFMA B operand: fp32 acc
