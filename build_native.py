@@ -116,7 +116,11 @@ def build_variant(name: str, verbose: bool = True) -> str:
     src = os.path.join(CSRC, "gpk_exact.hip")
     obj = os.path.join(out_dir, "gpk_exact.hip.o")
     flags = FLAGS + [f"-D{d}" for d in VARIANTS[name]]
-    dig = _digest([src] + sorted(included(src)), " ".join(flags) + main_lib)
+    objs = [os.path.join(OUT_DIR, os.path.basename(x) + ".o") for x in sources() if not x.endswith("gpk_exact.hip")]
+    # the digest covers the variant's own source + flags AND the main-build objects it links
+    # in (their .sha stamps), so a change to any other kernel relinks the variant too
+    linked = "".join(open(o + ".sha").read() if os.path.exists(o + ".sha") else o for o in objs)
+    dig = _digest([src] + sorted(included(src)), " ".join(flags) + main_lib + linked)
     stamp = obj + ".sha"
     if os.path.exists(lib_path) and os.path.exists(stamp) and open(stamp).read() == dig:
         return lib_path
@@ -126,7 +130,6 @@ def build_variant(name: str, verbose: bool = True) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for the {name} variant:\n{r.stderr}")
-    objs = [os.path.join(OUT_DIR, os.path.basename(x) + ".o") for x in sources() if not x.endswith("gpk_exact.hip")]
     r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, obj, "-o", lib_path],
                        capture_output=True, text=True)
     if r.returncode != 0:

@@ -316,12 +316,15 @@ GPK_DEVICE void diag_sweep(float (&v)[16]) {
 
 #include "gpk_diag_dpp.inc"
 
-// Flag words (ints in LDS, monotone epochs -- nothing is ever reset within a
-// launch; epoch = 32 * attempt + k):
+// Flag words (ints in LDS). The epoch flags are monotone within a launch (epoch =
+// 32 * attempt + k); the per-attempt counters kFlagSync / kFlagTrsm / kFlagBulk restart
+// from 0 between the two restart barriers of a failed attempt (kFlagRst is never reset):
 enum : int {
   kFlagT00 = 1,     // tile (0,0) of this attempt is in dsc                (32 * attempt)
-  kFlagFact = 2,    // R_kk^{-T} of step k is in wbuf[k & 1]                (epoch)
-  kFlagFail = 3,    // [3 + attempt]: failing column (provisional 1 first)
+  kFlagFact = 2,    // R_kk^{-T} of step k is in wbuf[k % 3]                (epoch)
+  kFlagFail = 3,    // [3 + attempt]: failure verdict of the attempt: provisional 16 k + 1 at
+                    // the failing step k, then 16 k + the failing column; workers decode the
+                    // step as (word - 1) >> 4
   kFlagHA = 18,     // look-ahead tile (k, k+1)   in hbuf[k & 1]            (epoch)
   kFlagHB = 19,     // look-ahead tile (k+1, k+1) in hbuf[k & 1] + 256      (epoch)
   kFlagSync = 20,   // worker-only barrier counter
@@ -357,31 +360,13 @@ GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// spin_until that also watches this attempt's failure word (fidx): returns true -- without
-// waiting for `target` -- once the diagonal wave has reported the attempt failed. Every
-// worker wait goes through it, so a worker can never sit in a wait that the failed attempt
-// will not satisfy (the restart then needs no assumption about where each worker saw it).
-GPK_DEVICE bool spin_until_f(lds_vint* flags, int idx, int target, int fidx) {
-  int n = 0;
-  bool failed = false;
-  while (true) {
-    const int v = flags[idx];
-    const int f = flags[fidx];
-    if (v >= target) break;
-    if (f != 0) { failed = true; break; }
-    if ((n & 255) == 255 && flags[kFlagTmo] != 0) break;
-    if (++n > (1 << 18)) {
-      flags[kFlagTmo] = 1;
-      if (GPK_TMO_DEBUG) flags[kFlagTmo + 1] = idx | (target << 8);
-      break;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-  return failed;
-}
-
-// A worker wait inside a factorisation step: leaves the step (failed attempt) when the
-// diagonal wave has reported a failure instead of waiting for something that will not come.
+// A worker wait inside a factorisation step. It does NOT watch the failure word: the restart
+// is correct because every wait a worker makes in step K is satisfied by work of steps < K of
+// the same attempt (panel / z / counter flags of step K-1 or earlier), while the diagonal wave
+// reports a failure no earlier than at the step it fails at, and a worker leaves the attempt
+// only at the R_KK^{-T} check of a step K >= that step ((fail - 1) >> 4 <= K). So all workers
+// have passed the same waits when they leave, and none waits for a step that never comes.
+// A new wait must keep that step-ordering invariant (else it spins until the 2^18-poll bound).
 #define GPK_WAITF(idx, target) spin_until(x.vflag, (idx), (target));
 
 GPK_DEVICE void publish_tile(float* dst, int lane, const f32x4 v, lds_vint* flags, int idx, int value) {

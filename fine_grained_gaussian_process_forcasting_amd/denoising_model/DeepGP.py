@@ -51,13 +51,16 @@ class ToyDeepGPHiddenLayer(nn.Module):
 
     def forward(self, x):
         """The layer's PRIOR at x, as reference DeepGP.py:51-54 returns it:
-        MultivariateNormal(mean_module(x), covar_module(x)). GPyTorch's VariationalStrategy
-        calls it on the inducing points for the prior; callers that call it directly get the
-        prior marginals here -- the mean and the kernel diagonal (outputscale); the full prior
-        covariance is not materialised on this path (q(f) comes from __call__)."""
+        MultivariateNormal(mean_module(x), covar_module(x)) with the covariance lazy, as in
+        GPyTorch: ``.variance`` is the kernel diagonal (outputscale), ``.covariance_matrix``
+        materialises outputscale * ARD-RBF(x, x), and ``.log_prob`` runs the fused
+        RBF + jittered Cholesky kernel on the residual value - mean(x). (q(f) -- what the
+        reference trains on -- comes from __call__.)"""
         mean_x = self.mean_module(x)
-        var_x = self.covar_module.outputscale.reshape(()).expand(mean_x.shape)
-        return MultivariateNormal(mean_x, var_x)
+        xb = x.reshape(-1, x.shape[-2], x.shape[-1])
+        kern = self.covar_module
+        return MultivariateNormal(mean_x, None,
+                                  exact=(xb, kern.base_kernel.lengthscale, kern.outputscale, None))
 
     def __call__(self, x, *other_inputs, **kwargs):
         """DeepGP.py:56-73 + DeepGPLayer.__call__ (upstream models/deep_gps/deep_gp.py).

@@ -249,6 +249,24 @@ class MultivariateNormal:
     def stddev(self):
         return self.variance.sqrt()
 
+    @property
+    def covariance_matrix(self):
+        """Dense prior covariance of an exact-GP / layer prior, materialised on request
+        (GPyTorch keeps covar_module(x) lazy and evaluates it here): outputscale * RBF with
+        upstream ``_sq_dist`` semantics (inputs centred by their mean, clamp at 0, exact 0 on
+        the diagonal) + the added likelihood noise on the diagonal. Not on the hot path: no
+        reference caller reads it. Variational outputs are diagonal-query (their marginals
+        are what the reference reads) and do not carry a covariance."""
+        if self._exact is None:
+            raise NotImplementedError("covariance_matrix is provided for exact-GP / layer priors; "
+                                      "variational outputs carry their marginal variance only")
+        X, lengthscale, outputscale, _ = self._exact
+        K = rbf_covariance(X, lengthscale, outputscale)
+        if self._added_noise is not None:
+            K = K + torch.diag_embed(torch.as_tensor(self._added_noise, dtype=K.dtype, device=K.device)
+                                     .expand(K.shape[:-1]))
+        return K.reshape(*self._mean.shape, self._mean.shape[-1])
+
     def expand(self, batch_size):
         batch_size = torch.Size(batch_size)
         mean = self._mean.expand(*batch_size, *self.event_shape)
@@ -278,8 +296,29 @@ class MultivariateNormal:
         noise = self._added_noise if self._added_noise is not None else torch.zeros((), device=X.device)
         from .ops_autograd import exact_log_prob
         n = X.shape[-2]
-        res = exact_log_prob(X, value.reshape(X.shape[:-1]), lengthscale, outputscale, constant, noise) * n
+        target = value.reshape(X.shape[:-1])
+        if constant is None:
+            # a general (e.g. LinearMean) prior mean: the fused kernel's constant mean is 0 and
+            # the residual value - mean(x) is its target (the same MVN density)
+            target = target - self._mean.reshape(X.shape[:-1])
+            constant = torch.zeros((), device=X.device)
+        res = exact_log_prob(X, target, lengthscale, outputscale, constant, noise) * n
         return res.reshape(value.shape[:-1])      # (N,) targets of an unbatched model -> scalar
+
+
+def rbf_covariance(X: torch.Tensor, lengthscale, outputscale) -> torch.Tensor:
+    """outputscale * exp(-||x_i - x_j||^2 / (2 l^2)) for X (B, N, D), as GPyTorch's
+    ScaleKernel(RBFKernel) evaluates a lazy kernel tensor (upstream kernels/rbf_kernel.py,
+    kernel.py ``_sq_dist``: inputs divided by the lengthscale and centred by their mean,
+    ||a||^2 + ||b||^2 - 2 a.b clamped at 0, the x1 == x2 diagonal set to exactly 0)."""
+    ls = torch.as_tensor(lengthscale, device=X.device, dtype=X.dtype).reshape(-1)
+    xs = X / ls
+    xs = xs - xs.mean(-2, keepdim=True)
+    nrm = xs.pow(2).sum(-1)
+    d = (nrm.unsqueeze(-1) + nrm.unsqueeze(-2) - 2.0 * xs @ xs.transpose(-1, -2)).clamp_min(0.0)
+    d = d * (1.0 - torch.eye(X.shape[-2], device=X.device, dtype=X.dtype))
+    s2 = torch.as_tensor(outputscale, device=X.device, dtype=X.dtype).reshape(())
+    return s2 * torch.exp(-0.5 * d)
 
 
 # ---------------------------------------------------------------------------

@@ -226,3 +226,35 @@ def test_layer_forward_returns_prior_and_exact_prior_variance(cuda_device):
                           rtol=1e-6)
     out.variance.sum().backward()   # differentiable in the outputscale
     assert em.covar_module.raw_outputscale.grad is not None
+
+
+def test_layer_prior_covariance_and_log_prob(cuda_device):
+    """ToyDeepGPHiddenLayer.forward(x) carries the lazy prior covariance of reference
+    DeepGP.py:51-54: .covariance_matrix = outputscale * ARD-RBF(x, x) (upstream _sq_dist
+    semantics) and .log_prob(v) the MVN density of v under N(mean(x), K), from the fused
+    RBF + Cholesky kernel on the residual, vs the fp64 oracle."""
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.DeepGP import DeepGPp
+    d, n = 8, 24
+    model = DeepGPp(d, 5).to(cuda_device)
+    hl = model.hidden_layer
+    with torch.no_grad():
+        hl.covar_module.base_kernel.raw_lengthscale.copy_(torch.linspace(-0.5, 1.0, d))
+    x = torch.randn(3, n, d, device=cuda_device)
+    prior = hl.forward(x)
+    ls = hl.covar_module.base_kernel.lengthscale.detach().cpu().double().numpy().reshape(-1)
+    s2 = float(hl.covar_module.outputscale.item())
+    X64 = x.cpu().double().numpy()
+    K = O.rbf(X64, X64, ls, s2, x1_eq_x2=True)
+    got = prior.covariance_matrix.detach().cpu().double().numpy()
+    assert got.shape == (3, n, n)
+    assert np.max(np.abs(got - K)) <= 1e-5 * s2
+    v = prior.mean.detach() + 0.3 * torch.randn(3, n, device=cuda_device)
+    lp = prior.log_prob(v)
+    assert lp.shape == (3,)
+    r = (v - prior.mean).detach().cpu().double().numpy()
+    ref = O.exact_mll(X64, r, ls, s2, 0.0, 0.0)
+    want = ref.mll * n
+    assert np.max(np.abs(lp.detach().cpu().double().numpy() - want) / np.abs(want)) <= 1e-4
+    lp.sum().backward()     # differentiable in the kernel and mean parameters
+    assert hl.covar_module.raw_outputscale.grad is not None
+    assert hl.mean_module.weights.grad is not None

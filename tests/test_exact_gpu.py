@@ -207,38 +207,59 @@ def test_exact_cfg2_full_batch(cuda_device):
     assert np.max(np.abs(mll - ref.mll) / np.abs(ref.mll)) <= 1e-4
 
 
-def test_exact_two_windows_per_cu_layout_ladder_and_failures(cuda_device):
-    """B > CUs selects the two-windows-per-CU layout (8 waves per window, the headline's):
-    a batch mixing singular windows (duplicate points, zero noise: the fp32 jitter ladder
-    restarts them in-kernel), a NaN window (info > 0) and regular windows. Checks every
-    window's info code, the regular windows against the fp64 oracle and the laddered ones'
-    factor against K + jitter I -- the restart path of that layout's worker protocol."""
-    B, N, D = 320, 256, 8
-    X, y = _inputs(B, N, D, seed=21)
-    dup = [3, 100, 257]
+def _cumulative_jitter(t):
+    """Total diagonal jitter after t rungs of the fp32 ladder (1e-6, 1e-5, ... added in turn)."""
+    return 1e-6 * 10 ** (t - 1) if t > 0 else 0.0
+
+
+# (B, N, D, dup windows, NaN window): every launch layout of the exact kernel.
+#   B=320 N=256: two windows per CU, 8 waves, column-ownership worker plan (the headline's)
+#   B=320 N=250: the same layout with padded tiles (FULL=false) -- ADVICE r4
+#   B=64  N=256: one window per CU, 16 waves, NB=16 (the strong-scaling shard layout)
+#   B=128 N=128: one window per CU, 16 waves, NB=8 (BASELINE configs[1])
+_LAYOUTS = [
+    (320, 256, 8, [3, 100, 257], 50),
+    (320, 250, 8, [5, 131, 318], 77),
+    (64, 256, 8, [0, 21, 63], 40),
+    (128, 128, 8, [2, 64, 127], 90),
+]
+
+
+@pytest.mark.parametrize("B,N,D,dup,nanw", _LAYOUTS)
+def test_exact_layout_ladder_and_failures(cuda_device, B, N, D, dup, nanw):
+    """A batch mixing singular windows (duplicate points, zero noise: the fp32 jitter ladder
+    restarts them in-kernel), a NaN window (info > 0) and regular windows, in every launch
+    layout. Checks every window's info code, the regular windows' L (upper triangle exactly
+    zero), z and MLL against the fp64 oracle, and the laddered ones' factor against
+    K + jitter I -- the restart path of each layout's worker protocol."""
+    X, y = _inputs(B, N, D, seed=21 + N + B)
     for b in dup:
         X[b] = X[b, :1].expand(N, D)       # all points equal: K = s2 * ones, singular
-    X[50, 7, 2] = float("nan")
+    X[nanw, 7, 2] = float("nan")
     noise, ls = 0.0, 0.3             # regular windows: K close to I, no jitter needed
     out = _run(cuda_device, X, y, ls, 1.0, 0.0, noise)
     info = out.info.cpu().numpy()
     for b in dup:
         assert info[b] < 0, (b, info[b])
-    assert info[50] > 0
-    good = [b for b in range(B) if b not in dup and b != 50]
+    assert info[nanw] > 0
+    good = [b for b in range(B) if b not in dup and b != nanw]
     assert (info[good] <= 0).all()
-    sel = good[::29] + [B - 1]
+    sel = good[::13] + [good[-1]]
     ref = O.exact_mll(X[sel].double().numpy(), y[sel].double().numpy(), ls, 1.0, 0.0, noise,
                       raise_on_fail=False)
     ok = [i for i, b in enumerate(sel) if info[b] == 0 and ref.info[i] == 0]
     assert len(ok) == len(sel)
     L = out.L.cpu().double().numpy()
-    assert _rel_fro(L[[sel[i] for i in ok]], ref.L[ok]).max() <= 1e-4
+    Lg = L[[sel[i] for i in ok]]
+    assert np.all(np.triu(Lg, 1) == 0.0), "upper triangle must be exactly zero"
+    assert _rel_fro(Lg, ref.L[ok]).max() <= 1e-4
+    z = out.z.cpu().double().numpy()[[sel[i] for i in ok]]
+    assert _rel_fro(z, ref.z[ok]).max() <= 1e-4
     mll = out.mll.cpu().double().numpy()[[sel[i] for i in ok]]
     assert np.max(np.abs(mll - ref.mll[ok]) / np.abs(ref.mll[ok])) <= 1e-4
     for b in dup:
         t = -int(info[b])
-        jit = 1e-6 * 10 ** (t - 1)
-        K = np.ones((N, N)) + jit * np.eye(N)
+        K = np.ones((N, N)) + _cumulative_jitter(t) * np.eye(N)
+        assert np.all(np.triu(L[b], 1) == 0.0)
         err = np.linalg.norm(L[b] @ L[b].T - K) / np.linalg.norm(K)
         assert err <= 1e-5, (b, t, err)

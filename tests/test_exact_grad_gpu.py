@@ -159,13 +159,15 @@ def test_exact_grad_full_bench_batch(cuda_device):
             assert e <= TOL, (w, k, e)
 
 
-@pytest.mark.parametrize("noise", [1e-2, 1e-3])
-def test_exact_grad_ill_conditioned_vs_fp32_reference(cuda_device, noise):
-    """Small noise (cond(K_hat) ~ 1e3..1e4 at N=128): the HIP backward's error vs the fp64
-    oracle must stay within 1e-4 or within 3x of what the reference's own fp32 arithmetic
-    (torch fp32 autograd through cholesky) achieves on the same windows."""
+@pytest.mark.parametrize("N,noise", [(128, 1e-2), (128, 1e-3), (256, 1e-3)])
+def test_exact_grad_ill_conditioned_vs_fp32_reference(cuda_device, N, noise):
+    """Small noise (cond(K_hat) ~ 1e3..1e4 at N=128, more at the headline's N=256): the HIP
+    backward's error vs the fp64 oracle must stay within 1e-4 or within 3x of what the
+    reference's own fp32 arithmetic (torch fp32 autograd through cholesky) achieves on the
+    same windows. alpha (hence dy and the mean-constant gradient) comes from V^T z with V
+    the split-f16 explicit L^-1, so N=256 pins its error growth at the bench shape."""
     from fine_grained_gaussian_process_forcasting_amd import ops
-    B, N, D = 2, 128, 8
+    B, D = 2, 8
     g = torch.Generator().manual_seed(77)
     X = torch.randn(B, N, D, generator=g) / np.sqrt(D)
     y = torch.randn(B, N, generator=g)
