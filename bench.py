@@ -256,27 +256,31 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed, label="BASELINE
     gv = torch.randn(B, N, device=dev)
     def step():
         kz = ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h)
-        out = ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False)
-        adj = ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv)
+        out = ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False, save=True)
+        adj = ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv, saved=out.saved)
         return kz, out, adj
 
     for _ in range(warmup):
         kz, out, adj = step()
     torch.cuda.synchronize()
+    saved = out.saved   # the training forward's state (M > 64; None: the adjoint recomputes)
     # each phase in its own back-to-back loop (same inputs as the step's): GPU time from a
-    # graph replay (time_graph), the eager loop beside it
+    # graph replay (time_graph), the eager loop beside it. "fwd" is the inference forward,
+    # "fwd_train" the training forward that also keeps A for the adjoint ("bwd").
     phases = {"kzz": lambda: ops.kzz_cholesky(Z, None, None, jitter=1e-4, hyper=kz_h),
               "fwd": lambda: ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper, want_flags=False),
-              "bwd": lambda: ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv)}
+              "fwd_train": lambda: ops.variational_forward(X, Z, kz.Linv, vm, vs, y=y, hyper=hyper,
+                                                           want_flags=False, save=True),
+              "bwd": lambda: ops.variational_adjoint(X, Z, kz.Linv, vm, vs, hyper, gm, gv, saved=saved)}
     ms, eager = {}, {}
     for k, fn in phases.items():
         gms, ems, _ = time_side(fn, steps)
         ms[k] = gms if gms is not None else ems
         eager[k] = ems
     if world > 1:
-        t = torch.tensor([ms["kzz"], ms["fwd"], ms["bwd"]], device=dev, dtype=torch.float64)
+        t = torch.tensor([ms["kzz"], ms["fwd"], ms["fwd_train"], ms["bwd"]], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms = dict(zip(["kzz", "fwd", "bwd"], t.tolist()))
+        ms = dict(zip(["kzz", "fwd", "fwd_train", "bwd"], t.tolist()))
     f32, f64 = var_flops_per_window(N, M, D)
     roof_s = f64 / FP64_PEAK + f32 / FP32_PEAK          # per window, fp64 + fp32 roofs added
     a32, a64 = var_adj_flops_per_window(N, M, D)
@@ -286,10 +290,13 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed, label="BASELINE
     return {
         "workload": f"DeepGP variational ({label}): B={B} N={N} M={M} D={D} per GPU",
         "windows_per_s_fwd": B * world / ((ms["kzz"] + ms["fwd"]) * 1e-3),
-        "windows_per_s_train_step": B * world / ((ms["kzz"] + ms["fwd"] + ms["bwd"]) * 1e-3),
+        "windows_per_s_train_step": B * world / ((ms["kzz"] + ms["fwd_train"] + ms["bwd"]) * 1e-3),
         "kernel_ms": {"gpk_kzz_chol_f64": ms["kzz"], "gpk_variational_f32": ms["fwd"],
+                      "gpk_variational_train_f32": ms["fwd_train"],
                       "gpk_variational_adjoint_f32": ms["bwd"]},
+        "adjoint_path": "saved-state (forward keeps A)" if saved is not None else "recompute",
         "eager_ms": {"gpk_kzz_chol_f64": eager["kzz"], "gpk_variational_f32": eager["fwd"],
+                     "gpk_variational_train_f32": eager["fwd_train"],
                      "gpk_variational_adjoint_f32": eager["bwd"],
                      "note": "eager back-to-back calls incl. host launch work; kernel_ms = graph replay"},
         "roofline": {"kernel": "gpk_var_fwd_r_kernel" if (M <= 64 and D <= 32) else "gpk_var_fwd_l_kernel",

@@ -64,6 +64,15 @@ SIGNATURES = {
                                             c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                             c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p]),
+    "gpk_variational_saved_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "gpk_variational_train_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gpk_variational_adjoint_saved_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "gpk_variational_adjoint_saved_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                  c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                                  c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                  c_void_p, c_void_p]),
     "gpk_window_gather_f32": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_void_p, c_int, c_int, c_int,
                                       c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
 }

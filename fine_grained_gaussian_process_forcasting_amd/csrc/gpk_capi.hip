@@ -250,6 +250,64 @@ int gpk_variational_f32(const float* X, const float* Z, const double* Linv, cons
   return gpk_launch_var(a, flags, (hipStream_t)stream);
 }
 
+size_t gpk_variational_saved_bytes(int B, int N, int M, int D) {
+  if (B < 1 || N < 1 || M < 1 || M > 256 || D < 1 || D > 64) return 0;
+  return gpk_var_saved_bytes(B, N, M, D);
+}
+int gpk_variational_train_f32(const float* X, const float* Z, const double* Linv, const float* vmean,
+                              const float* vstd, const float* hyp, const float* y, int B, int N, int M,
+                              int D, float* mean, float* var, float* ell, int* flags, void* saved,
+                              void* stream) {
+  if (X == nullptr) return -1;
+  if (Z == nullptr) return -2;
+  if (Linv == nullptr) return -3;
+  if (vmean == nullptr) return -4;
+  if (vstd == nullptr) return -5;
+  if (hyp == nullptr) return -6;
+  if (B < 0) return -8;
+  if (N < 1) return -9;
+  if (M < 1 || M > 256) return -10;
+  if (D < 1 || D > 64) return -11;
+  if (mean == nullptr) return -12;
+  if (var == nullptr) return -13;
+  if (ell != nullptr && y == nullptr) return -7;
+  if (saved == nullptr && gpk_var_saved_bytes(B, N, M, D) > 0) return -16;
+  if (B == 0) return 0;
+  GpkVarArgs a{X, Z, Linv, vmean, vstd, hyp, y, B, N, M, D, mean, var, ell, (float*)saved};
+  return gpk_launch_var(a, flags, (hipStream_t)stream);
+}
+size_t gpk_variational_adjoint_saved_workspace_bytes(int B, int N, int M, int D) {
+  if (B < 1 || N < 1 || M < 1 || M > 256 || D < 1 || D > 64) return 0;
+  return gpk_var_adjoint_saved_ws_bytes(B, N, M, D);
+}
+int gpk_variational_adjoint_saved_f32(const float* X, const float* Z, const double* Linv,
+                                      const float* vmean, const float* vstd, const float* hyp,
+                                      const float* gmean, const float* gvar, const void* saved, int B,
+                                      int N, int M, int D, void* workspace, float* dX, double* dLinv,
+                                      float* dZ, float* dpar, void* stream) {
+  if (X == nullptr) return -1;
+  if (Z == nullptr) return -2;
+  if (Linv == nullptr) return -3;
+  if (vmean == nullptr) return -4;
+  if (vstd == nullptr) return -5;
+  if (hyp == nullptr) return -6;
+  if (gmean == nullptr) return -7;
+  if (gvar == nullptr) return -8;
+  if (saved == nullptr) return -9;
+  if (B < 1) return -10;
+  if (N < 1) return -11;
+  if (M < 1 || M > 256) return -12;
+  if (D < 1 || D > 64) return -13;
+  if (gpk_var_saved_bytes(B, N, M, D) == 0) return -12;
+  if (workspace == nullptr) return -14;
+  if (dX == nullptr) return -15;
+  if (dLinv == nullptr) return -16;
+  if (dZ == nullptr) return -17;
+  if (dpar == nullptr) return -18;
+  GpkVarAdjArgs a{X, Z, Linv, vmean, vstd, hyp, gmean, gvar, B, N, M, D, workspace, dX, dLinv, dZ, dpar,
+                  (const float*)saved};
+  return gpk_launch_var_adjoint(a, (hipStream_t)stream);
+}
 size_t gpk_variational_adjoint_workspace_bytes(int B, int N, int M, int D) {
   if (B < 1 || N < 1 || M < 1 || M > 256 || D < 1 || D > 64) return 0;
   return gpk_var_adjoint_ws_bytes(B, N, M, D);

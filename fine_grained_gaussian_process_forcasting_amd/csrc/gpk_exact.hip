@@ -325,8 +325,13 @@ enum : int {
   kFlagFail = 3,    // [3 + attempt]: failure verdict of the attempt: provisional 16 k + 1 at
                     // the failing step k, then 16 k + the failing column; workers decode the
                     // step as (word - 1) >> 4
-  kFlagHA = 18,     // look-ahead tile (k, k+1)   in hbuf[k & 1]            (epoch)
-  kFlagHB = 19,     // look-ahead tile (k+1, k+1) in hbuf[k & 1] + 256      (epoch)
+  // look-ahead hand-over (k, k+1) -> hbuf[k & 1], (k+1, k+1) -> hbuf[k & 1] + 256: ONE FLAG WORD
+  // PER PARITY (kFlagHA + (k & 1), kFlagHB + (k & 1); epoch). In the column plan consecutive
+  // hand-overs come from different waves, so with one shared word the owner of step k+1 could
+  // raise it before the owner of step k had written its tile, and the diagonal wave would read
+  // a stale hbuf[k & 1] (seen: 2 of 512 windows with a wrong (8,8) block).
+  kFlagHA = 40,     // [40 + (k & 1)]
+  kFlagHB = 42,     // [42 + (k & 1)]
   kFlagSync = 20,   // worker-only barrier counter
   kFlagTmo = 21,    // a spin wait ran out (safety net: the launch still drains)
   kFlagInvSigma = 30,
@@ -367,7 +372,14 @@ GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
 // only at the R_KK^{-T} check of a step K >= that step ((fail - 1) >> 4 <= K). So all workers
 // have passed the same waits when they leave, and none waits for a step that never comes.
 // A new wait must keep that step-ordering invariant (else it spins until the 2^18-poll bound).
-#define GPK_WAITF(idx, target) spin_until(x.vflag, (idx), (target));
+#define GPK_WAITF(idx, target)                                                  \
+  {                                                                             \
+    unsigned long long _w0 = 0;                                                 \
+    if constexpr (ST) _w0 = __builtin_amdgcn_s_memtime();                       \
+    spin_until(x.vflag, (idx), (target));                                       \
+    if constexpr (ST) x.st[9] += __builtin_amdgcn_s_memtime() - _w0;            \
+  }
+
 
 GPK_DEVICE void publish_tile(float* dst, int lane, const f32x4 v, lds_vint* flags, int idx, int value) {
   *(f32x4*)&dst[lane * 4] = v;
@@ -759,11 +771,11 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // hand-over: the diagonal wave waits
       if (wv == TA % WK) {
         upd_ij(acc[TA / WK], IC<K>{}, IC<K + 1>{});
-        publish_tile(hA, lane, acc[TA / WK], x.vflag, kFlagHA, e0 + K);
+        publish_tile(hA, lane, acc[TA / WK], x.vflag, kFlagHA + (K & 1), e0 + K);
       }
       if (wv == TB % WK) {
         upd_ij(acc[TB / WK], IC<K + 1>{}, IC<K + 1>{});
-        publish_tile(hA + 256, lane, acc[TB / WK], x.vflag, kFlagHB, e0 + K);
+        publish_tile(hA + 256, lane, acc[TB / WK], x.vflag, kFlagHB + (K & 1), e0 + K);
       }
       if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
     }
@@ -986,11 +998,11 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if (wv == HAW) {
         GPK_WAITF(kFlagPan + K, e0 + K - 1)
         upd(acc[SA], pprev + K * 256, p, pl);
-        publish_tile(hA, lane, acc[SA], x.vflag, kFlagHA, e0 + K);
+        publish_tile(hA, lane, acc[SA], x.vflag, kFlagHA + (K & 1), e0 + K);
       }
       if (wv == HBW) {
         acc[SB] = pan_mma2(p, p, pl, acc[SB]);
-        publish_tile(hA + 256, lane, acc[SB], x.vflag, kFlagHB, e0 + K);
+        publish_tile(hA + 256, lane, acc[SB], x.vflag, kFlagHB + (K & 1), e0 + K);
       }
       if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
     }
@@ -1170,6 +1182,9 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   }
   if (x.Lb != nullptr) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, K, wv, WK, lane);
   GPK_WSTAMP(3, 3)  // RBF + zero-L
+  if constexpr (ST) {
+    if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8 + 7] = x.st[9];   // cumulative flag-wait cycles
+  }
   return 0;
 }
 
@@ -1348,8 +1363,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       flag[kFlagT00] = -1;
       flag[kFlagFact] = -1;
       for (int qq = 3; qq < 16; ++qq) flag[qq] = 0;
-      flag[kFlagHA] = -1;
-      flag[kFlagHB] = -1;
+      for (int qq = 0; qq < 2; ++qq) flag[kFlagHA + qq] = flag[kFlagHB + qq] = -1;
       flag[kFlagSync] = 0;
       flag[kFlagTmo] = 0;
       for (int qq = kFlagPan; qq <= kFlagZ; ++qq) flag[qq] = -1;
@@ -1487,8 +1501,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       flag[kFlagT00] = -1;
       flag[kFlagFact] = -1;
       for (int q = 3; q < 16; ++q) flag[q] = 0;
-      flag[kFlagHA] = -1;
-      flag[kFlagHB] = -1;
+      for (int qq = 0; qq < 2; ++qq) flag[kFlagHA + qq] = flag[kFlagHB + qq] = -1;
       flag[kFlagSync] = 0;
       flag[kFlagTmo] = 0;
       for (int qq = kFlagPan; qq <= kFlagZ; ++qq) flag[qq] = -1;
@@ -1650,8 +1663,8 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         const float* hk = hbuf + (k & 1) * 512;
         unsigned long long hw0 = 0;
         if constexpr (STAMPS) hw0 = __builtin_amdgcn_s_memtime();
-        spin_until(vflag, kFlagHA, epoch);
-        spin_until(vflag, kFlagHB, epoch);
+        spin_until(vflag, kFlagHA + (k & 1), epoch);
+        spin_until(vflag, kFlagHB + (k & 1), epoch);
         if constexpr (STAMPS) {
           const unsigned long long hw1 = __builtin_amdgcn_s_memtime();
           if (lane == 0) {
@@ -1683,7 +1696,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     float diagval = (s2u + noise) * sigma2;
     double jit_prev = 0.0;
     f32x4 acc[SLOTS];
-    unsigned long long wst[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long wst[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     WorkerCtx wx{panel, wbuf, hbuf, vflag, Lb, zout, rw, smem, lay.rbfc, N, b, lane, c, grp,
                  launder_s(wave), 0, 0, 0.f, nullptr,
                  STAMPS ? stamps + (size_t)b * kStampStride + 32 : nullptr};
@@ -1732,8 +1745,8 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
           acc[17] = rbf_tile<NB, FULL>(smem, rk, 0, jB, lane, N);
           acc[16] = rbf_tile<NB, FULL>(smem, rk, 1, jB, lane, N);
           if (wv == 0) {
-            publish_tile(hbuf, lane, acc[17], vflag, kFlagHA, e0);
-            publish_tile(hbuf + 256, lane, acc[16], vflag, kFlagHB, e0);
+            publish_tile(hbuf, lane, acc[17], vflag, kFlagHA + 0, e0);
+            publish_tile(hbuf + 256, lane, acc[16], vflag, kFlagHB + 0, e0);
           }
           acc[0] = rbf_tile<NB, FULL>(smem, rk, 0, jA, lane, N);
           acc[1] = rbf_tile<NB, FULL>(smem, rk, 1, jA, lane, N);
@@ -1753,11 +1766,11 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         if constexpr (NB > 1) {
           if (wv == T01 % WK) {
             acc[T01 / WK] = rbf_tile<NB, FULL>(smem, rk, 0, 1, lane, N);
-            publish_tile(hbuf, lane, acc[T01 / WK], vflag, kFlagHA, e0);
+            publish_tile(hbuf, lane, acc[T01 / WK], vflag, kFlagHA + 0, e0);
           }
           if (wv == P1 % WK) {
             acc[P1 / WK] = rbf_tile<NB, FULL>(smem, rk, 1, 1, lane, N);
-            publish_tile(hbuf + 256, lane, acc[P1 / WK], vflag, kFlagHB, e0);
+            publish_tile(hbuf + 256, lane, acc[P1 / WK], vflag, kFlagHB + 0, e0);
           }
         }
         static_for_desc<SLOTS>([&](auto I) {

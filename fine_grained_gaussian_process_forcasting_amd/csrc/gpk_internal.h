@@ -60,6 +60,7 @@ struct GpkVarArgs {
   float* mean;         // (B, N)
   float* var;          // (B, N)
   float* ell;          // (B,) or nullptr: sum_i expected log prob
+  float* saved;        // training: gpk_var_saved_bytes(B, N, M, D) bytes of state for the adjoint, or nullptr
 };
 
 struct GpkVarAdjArgs {
@@ -72,11 +73,12 @@ struct GpkVarAdjArgs {
   const float* gmean;  // (B, N)
   const float* gvar;   // (B, N)
   int B, N, M, D;
-  void* ws;            // gpk_var_adjoint_ws_bytes(B, N, M, D) bytes
+  void* ws;            // gpk_var_adjoint_ws_bytes(B, N, M, D) bytes (saved: gpk_var_adjoint_saved_ws_bytes)
   float* dX;           // (B, N, D) out
   double* dLinv;       // (M, M) out (lower; upper zero)
   float* dZ;           // (M, D) out: the K_ZX part of dZ
   float* dpar;         // (2M + 2D + 2) out: dvmean, dvstd, ds2, dlengthscale, dweights, dbias
+  const float* saved;  // the training forward's state (gpk_var_saved_bytes), or nullptr: recompute
 };
 
 
@@ -96,6 +98,8 @@ size_t gpk_kzz_grad_ws_bytes(int M, int D);
 int gpk_launch_kzz_grad(const GpkKzzGradArgs& a, hipStream_t stream);
 
 size_t gpk_var_adjoint_ws_bytes(int B, int N, int M, int D);
+size_t gpk_var_saved_bytes(int B, int N, int M, int D);
+size_t gpk_var_adjoint_saved_ws_bytes(int B, int N, int M, int D);
 int gpk_launch_var_adjoint(const GpkVarAdjArgs& a, hipStream_t stream);
 int gpk_launch_var(const GpkVarArgs& a, int* flags, hipStream_t stream);
 

@@ -409,6 +409,16 @@ gpk_var_ell_kernel(const float* __restrict__ mean, const float* __restrict__ var
 // ---------------------------------------------------------------------------
 constexpr int LTW = 32;   // points per chunk (2 column tiles)
 
+// Per-chunk block of the state the training forward keeps for the adjoint (M > 64):
+// A = L^{-1} K_ZX of the chunk cast to fp32 (MB x 2 tiles, element u of lane (c, g) of tile
+// (rt, ct) <-> row 16 rt + g + 4u, point 16 ct + c), then the clamp mask of its LTW points
+// (1: var_i >= 1e-6, 0: clamped or padding).
+template <int MB>
+struct LSaved {
+  static constexpr int tiles = MB * 2 * 256;
+  static constexpr int blk = tiles + LTW;
+};
+
 // A[rA] / A[rB] of one chunk for the wave with rA = RA: slots 0..RA are blocks (RA, s),
 // slots RA+1..MB blocks (MB-1-RA, s-RA-1). The next slot's K_ZX operands (one b128 per
 // column tile) are read while this slot's 8 MFMAs run; a scheduling fence per slot keeps
@@ -489,7 +499,7 @@ gpk_var_fwd_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
                      const double* __restrict__ Linv, const float* __restrict__ vmean,
                      const float* __restrict__ vstd, const float* __restrict__ hyp, int N, int M,
                      int D, int nchunks, float* __restrict__ mean_out, float* __restrict__ var_out,
-                     int* __restrict__ flags) {
+                     int* __restrict__ flags, float* __restrict__ saved) {
   using G = LGeo<MB, DQ>;
   constexpr int NWV = G::NWV, NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV;
   extern __shared__ __attribute__((aligned(16))) float vsm[];
@@ -641,6 +651,19 @@ gpk_var_fwd_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     // selects that doubled the accumulators)
     f64x4 aA[2], aB[2];
     lreg_gemm_for<MB, 0>(wave, Lr, Kl, lane, aA, aB);
+    if (saved != nullptr) {
+      // training: A (fp32, as the reference casts it) in the adjoint's LDS tile layout, so
+      // gpk_var_adjs_l_kernel needs neither the forward GEMM nor the K_ZX Gram again
+      float* sb = saved + (size_t)t * LSaved<MB>::blk;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        *(f32x4*)(sb + ((rA * 2 + ct) * 64 + lane) * 4) =
+            f32x4{(float)aA[ct][0], (float)aA[ct][1], (float)aA[ct][2], (float)aA[ct][3]};
+        if (rB != rA)
+          *(f32x4*)(sb + ((rB * 2 + ct) * 64 + lane) * 4) =
+              f32x4{(float)aB[ct][0], (float)aB[ct][1], (float)aB[ct][2], (float)aB[ct][3]};
+      }
+    }
     // partials over the wave's rows (A cast to fp32 as the reference does)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
@@ -680,9 +703,14 @@ gpk_var_fwd_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       }
       const float mean_i = mm + (lin[tid] + b0);
       float var_i = s2 + jit + vv;
-      if (var_i < 1e-6f) { var_i = 1e-6f; clamped = 1; }  // MVN.variance clamp (fp32)
+      const bool clamp = var_i < 1e-6f;
+      if (clamp) { var_i = 1e-6f; clamped = 1; }  // MVN.variance clamp (fp32)
       mean_out[(size_t)b * N + i0 + tid] = mean_i;
       var_out[(size_t)b * N + i0 + tid] = var_i;
+      // the clamp passes no gradient: the adjoint masks gvar with this
+      if (saved != nullptr) saved[(size_t)t * LSaved<MB>::blk + LSaved<MB>::tiles + tid] = clamp ? 0.f : 1.f;
+    } else if (saved != nullptr && tid < LTW) {
+      saved[(size_t)t * LSaved<MB>::blk + LSaved<MB>::tiles + tid] = 0.f;
     }
   }
   if (flags != nullptr && clamped)
@@ -1646,6 +1674,537 @@ gpk_var_adjk_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Adjoint for M > 64 from the training forward's saved state (gpk_variational_train_f32):
+// ONE kernel in the adjk layout (wave w holds the L^{-1} COLUMN blocks of block rows
+// pA = w, pB = MB-1-w). Per chunk: A (fp32, LSaved layout) straight into the LDS dA tiles,
+// the clamp mask onto gvar; each wave turns ITS rows of A into dA = gmean m + 2 gvar (s^2 - 1) A
+// in place (with the dvmean / dvstd row sums); then dK = L^{-T} dA, K_ZX of the wave's rows
+// recomputed straight into registers (f32 MFMA, zs rows fed in pi order so the tile lands in the
+// f64 C layout of dK; computed after the GEMM, where it does not push L^{-1} into scratch),
+// Q = dK o K and the rest exactly as gpk_var_adjk_l_kernel. dL^{-1} no longer comes from a dA / K_ZX
+// workspace: gpk_var_kgram_l_kernel accumulates G' = A diag(gvar) K_ZX^T and u = K_ZX gmean from
+// the same saved A (below). LDS: the adjk geometry; rows / xn / gvar live in its misc area.
+// ---------------------------------------------------------------------------
+template <int MB, int DQ>
+__global__ void __launch_bounds__(64 * ((MB + 1) / 2), 2)
+gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                      const double* __restrict__ Linv, const float* __restrict__ vmean,
+                      const float* __restrict__ vstd, const float* __restrict__ hyp,
+                      const float* __restrict__ gmean, const float* __restrict__ gvar,
+                      const float* __restrict__ saved, int N, int M, int D, int nchunks,
+                      float* __restrict__ wspart, float* __restrict__ dX) {
+  using G = LAdjGeo<MB, DQ>;
+  using SV = LSaved<MB>;
+  constexpr int NWV = G::NWV, NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV, NDT = G::NDT;
+  constexpr int NU = SV::tiles / 4;                 // f32x4 units of A per chunk
+  static_assert(NU % NT == 0, "A block: whole passes");
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4, sub = tid & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pA = wave, pB = MB - 1 - wave;
+  const bool two = pB != pA;
+  const float s2 = hyp[0];
+  const float* w = hyp + 4;
+  const float* ls = hyp + 4 + D;
+  const int nch = (N + LTW - 1) / LTW;
+  // rows (dvm | dsm accumulators), xn and gvar (chunk parity) live in the epilogue's misc area
+  constexpr int oRows = G::kMisc, oXn = G::kMisc + 2 * G::MP, oGv = oXn + 2 * LTW;
+  static_assert(2 * G::MP + 4 * LTW <= 2 * NT + NWV, "misc area");
+
+  // L^{-1} column blocks, k-order g + 4u (as gpk_var_adjk_l_kernel)
+  double Lc[MB + 1][4];
+  {
+    const bool full = (M & 15) == 0;
+    const int NA = MB - pA;
+#pragma unroll
+    for (int s = 0; s <= MB; ++s) {
+      const bool isA = s < NA;
+      const int P = isA ? pA : pB, rt = isA ? pA + s : pB + (s - NA);
+      const bool ok = isA || (two && rt < MB);
+      const int col = 16 * P + c;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = 16 * rt + g + 4 * u;
+        const bool in = ok && (full || (row < M && col < M));
+        const double v = Linv[in ? (size_t)row * M + col : 0];
+        Lc[s][u] = in ? v : 0.0;
+      }
+      if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float lsr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) lsr[v] = ls[sub + 16 * v < D ? sub + 16 * v : 0];
+  float xr[NPASS][DV];
+  lload_points<NPASS, DV, NT>(X, blockIdx.x, nchunks, nch, N, D, xr);
+  stage_inducing(Z, ls, vmean, vstd, M, D, G::MP, DQ, DS, vsm + G::kZs, vsm + G::kZn, vsm + G::kCm,
+                 vsm + G::kVm, vsm + G::kSm1, vsm + G::kKl);
+  for (int e = tid; e < G::MP; e += NT) vsm[G::kQ + e] = 0.f;
+  for (int e = tid; e < 2 * G::MP; e += NT) vsm[oRows + e] = 0.f;
+  lds_barrier();
+  float cmr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) cmr[v] = vsm[G::kCm + sub + 16 * v];
+  const int dd = tid % DQ;   // the dX phase's dim for this thread (NT % DQ == 0)
+  const float il_dd = dd < D ? 1.f / ls[dd < D ? dd : 0] : 0.f;
+  const float w_dd = dd < D ? w[dd < D ? dd : 0] : 0.f;
+  float rx2 = 0.f, gxa = 0.f, sumQ = 0.f, sumgm = 0.f, sumgv = 0.f;
+  f32x4 qx[2][NDT];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) qx[h][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int par = 0;
+
+  for (int t = blockIdx.x; t < nchunks; t += gridDim.x, par ^= 1) {
+    const int b = t / nch, i0 = (t - b * nch) * LTW;
+    const int nvalid = N - i0 < LTW ? N - i0 : LTW;
+    const long long col0 = (long long)b * N + i0;
+    float* sm = (float*)fresh_lds(vsm);
+    float* dAl = sm + G::kdA;
+    float* xzl = sm + G::kXz;
+    float* red = sm + G::kRed;
+    const float* zs = sm + G::kZs;
+    const float* zn = sm + G::kZn;
+    const float* vm = sm + G::kVm;
+    const float* sm1 = sm + G::kSm1;
+    float* qrow = sm + G::kQ;
+    float* scr = sm + G::kScr + wave * 320;
+    float* xs = sm + G::kXs + par * LTW * DS;
+    float* xn = sm + oXn + par * LTW;
+    float* gmc = sm + G::kGm + par * LTW;
+    float* gvc = sm + oGv + par * LTW;
+    float* rows = sm + oRows;
+    // ---- the chunk's A tiles (one contiguous block) -> the LDS dA tiles; points; gmean / gvar
+    {
+      const float* sb = saved + (size_t)t * SV::blk;
+#pragma unroll
+      for (int q = 0; q < NU / NT; ++q) {
+        const int e = tid + q * NT;
+        *(f32x4*)(dAl + 4 * e) = *(const f32x4*)(sb + 4 * e);
+      }
+      if (tid < LTW) {
+        const bool ok = tid < nvalid;
+        const float keep = sb[SV::tiles + tid];
+        const float gm = gmean[ok ? col0 + tid : 0], gv = gvar[ok ? col0 + tid : 0];
+        const float gvk = (ok && keep != 0.f) ? gv : 0.f;
+        gmc[tid] = ok ? gm : 0.f;
+        gvc[tid] = gvk;
+        sumgm += ok ? gm : 0.f;
+        sumgv += gvk;
+      }
+    }
+    lstage_points<NPASS, DV, NT, DS>(xr, lsr, cmr, D, nvalid, xs, xn);
+    if (t + (int)gridDim.x < nchunks) lload_points<NPASS, DV, NT>(X, t + gridDim.x, nchunks, nch, N, D, xr);
+    lds_barrier();
+    // ---- the wave's own rows: row sums of A, A -> dA in place
+    {
+      float gmq[2], gvq[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        gmq[ct] = gmc[16 * ct + c];
+        gvq[ct] = gvc[16 * ct + c];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const int rt = h == 0 ? pA : pB;
+        float pm[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          float* at = dAl + ((rt * 2 + ct) * 64 + lane) * 4;
+          const f32x4 av = *(const f32x4*)at;
+          f32x4 da;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int p = 16 * rt + g + 4 * r;
+            pm[r] = __builtin_fmaf(gmq[ct], av[r], pm[r]);
+            ps[r] = __builtin_fmaf(gvq[ct], av[r] * av[r], ps[r]);
+            da[r] = gmq[ct] * vm[p] + 2.f * gvq[ct] * sm1[p] * av[r];
+          }
+          *(f32x4*)at = da;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float a = row16_sum_f(pm[r]), q = row16_sum_f(ps[r]);
+          if (c == 0) {
+            const int p = 16 * rt + g + 4 * r;
+            rows[p] += a;
+            rows[G::MP + p] += q;
+          }
+        }
+      }
+    }
+    lds_barrier();
+    // ---- dK = L^{-T} dA on the wave's block rows; Q = dK o K
+    f32x4 Qt[2][2];
+    {
+      f64x4 dK[2][2];
+      lcol_gemm_for<MB, 0>(wave, Lc, dAl, lane, dK[0], dK[1]);
+      // K_ZX of the wave's rows (f32 MFMA, zs rows fed in pi order: reg r <-> row g + 4r, the
+      // f64 C layout of dK), Q = dK o K
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rt = h == 0 ? pA : pB;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const float* za = zs + (16 * rt + pi16(c)) * DS + g;
+          const float* xb = xs + (16 * ct + c) * DS + g;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < DQ / 4; ++k) acc = mfma32(za[4 * k], xb[4 * k], acc);
+          const int col = 16 * ct + c;
+          const float xnc = xn[col];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int p = 16 * rt + g + 4 * r;
+            float dist = zn[p] + xnc - 2.f * acc[r];
+            dist = dist < 0.f ? 0.f : dist;
+            const float kv = (p < M && col < nvalid) ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * dist) : 0.f;
+            Qt[h][ct][r] = (h == 1 && !two) ? 0.f : (float)dK[h][ct][r] * kv;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int rt = h == 0 ? pA : pB;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = row16_sum_f(Qt[h][0][r] + Qt[h][1][r]);
+        if (c == 0) qrow[16 * rt + g + 4 * r] += v;
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      float v = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) v += (Qt[h][ct][0] + Qt[h][ct][1]) + (Qt[h][ct][2] + Qt[h][ct][3]);
+      sumQ += v;
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) red[wave * LTW + 16 * ct + c] = v;
+    }
+    {
+      f32x4 xz[2][NDT];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) xz[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const int rt = h == 0 ? pA : pB;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const float zb = zs[(16 * rt + g + 4 * r) * DS + 16 * dt + c];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) xz[ct][dt] = mfma32(Qt[h][ct][r], zb, xz[ct][dt]);
+          }
+      }
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            xzl[(wave * LTW + 16 * ct + 4 * g + r) * DQ + 16 * dt + c] = xz[ct][dt][r];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = Qt[h][ct][r];
+        wave_lds_sync();
+        float aq[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) aq[s] = scr[((c & 3) * 16 + 4 * s + g) * 5 + (c >> 2)];
+        wave_lds_sync();
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            qx[h][dt] = mfma32(aq[s], xs[(16 * ct + 4 * s + g) * DS + 16 * dt + c], qx[h][dt]);
+      }
+    }
+    lds_barrier();
+    for (int e = tid; e < LTW * DQ; e += NT) {
+      const int col = e / DQ;
+      float v = 0.f, r = 0.f;
+#pragma unroll
+      for (int q = 0; q < NWV; ++q) {
+        v += xzl[(q * LTW + col) * DQ + dd];
+        r += red[q * LTW + col];
+      }
+      const float xv = xs[col * DS + dd];
+      if (col < nvalid && dd < D) {
+        dX[(col0 + col) * D + dd] = (v - xv * r) * il_dd + gmc[col] * w_dd;
+        rx2 = __builtin_fmaf(r * xv, xv, rx2);
+        gxa = __builtin_fmaf(gmc[col], xv, gxa);
+      }
+    }
+  }
+  lds_barrier();
+  // partial fields: QX (M x D) | q (M) | dvm (M) | dsm (M) | rx2 (D) | sumQ | sumgv | gx (D) | sumgm
+  const int P = M * D + 3 * M + 2 * D + 3;
+  float* po = wspart + (size_t)blockIdx.x * P;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 1 && !two) break;
+    const int rt = h == 0 ? pA : pB;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = 16 * rt + 4 * g + r, d = 16 * dt + c;
+        if (p < M && d < D) po[p * D + d] = qx[h][dt][r];
+      }
+  }
+  for (int m = tid; m < M; m += NT) {
+    po[M * D + m] = vsm[G::kQ + m];
+    po[M * D + M + m] = vsm[oRows + m];
+    po[M * D + 2 * M + m] = vsm[oRows + G::MP + m];
+  }
+  lds_barrier();   // the rows are read out before misc overwrites them
+  float* misc = vsm + G::kMisc;
+  misc[tid] = rx2;
+  misc[NT + tid] = gxa;
+  sumQ = wave_sum(sumQ);
+  if (lane == 0) misc[2 * NT + wave] = sumQ;
+  lds_barrier();
+  for (int d = tid; d < D; d += NT) {
+    float v = 0.f, u = 0.f;
+    for (int q = d; q < NT; q += DQ) { v += misc[q]; u += misc[NT + q]; }
+    po[M * D + 3 * M + d] = v;
+    po[M * D + 3 * M + D + 2 + d] = u;
+  }
+  if (tid == 0) {
+    float v = 0.f;
+    for (int q = 0; q < NWV; ++q) v += misc[2 * NT + q];
+    po[M * D + 3 * M + D] = v;
+  }
+  if (wave == 0) {
+    const float u = wave_sum(sumgm), v = wave_sum(sumgv);   // accumulated on lanes 0..LTW-1
+    if (lane == 0) {
+      po[M * D + 3 * M + 2 * D + 2] = u;
+      po[M * D + 3 * M + D + 1] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dL^{-1} of the saved-state adjoint (M > 64), from the forward's A instead of a dA / K_ZX
+// workspace: with dA = gmean m + 2 gvar (s^2 - 1) A,
+//   dL^{-1} = sum_i dA_i K_i^T = m u^T + 2 diag(s^2 - 1) G',   u = sum_i gmean_i K_i,
+//   G' = sum_i gvar_i A_i K_i^T            (lower part only: dL^{-1} is lower triangular)
+// (the same arithmetic as the reference's fp32 dA: A is the saved fp32 A, products exact on f32
+// MFMA, no L^{-1} product -- a form through G = K diag(gvar) K^T would multiply G's rounding by
+// L^{-1}'s conditioning). gpk_var_kgram_l_kernel: per workgroup over its chunks, wave w owns the
+// G' tile rows I = w and MB-1-w (MB + 1 lower tiles for every wave, f32 MFMA accumulators). Per
+// chunk: the saved A block -> LDS rows [p][point], K_ZX recomputed (f32 MFMA Gram, fp32 exp) ->
+// LDS rows, gvar masked by the saved clamp mask; each tile product is 8 mfma_f32_16x16x4_f32
+// with both operands read as two b128 per lane (the k index of step j on lane (c, g) is point
+// 8 g + j). Partials gpart[wg] = G' tiles (acc layout) | u, summed in a fixed order afterwards
+// (gpk_var_red_kernel), then gpk_var_gdl_l_kernel forms dL^{-1} elementwise.
+// ---------------------------------------------------------------------------
+template <int MB, int DQ>
+struct LGramGeo {
+  static constexpr int NWV = (MB + 1) / 2, NT = 64 * NWV, MP = 16 * MB, DS = DQ + 2;
+  static constexpr int NPASS = (LTW * 16 + NT - 1) / NT, DV = DQ / 16;
+  static constexpr int KS = LTW + 4;                       // row stride of the A / K blocks (floats)
+  static constexpr int NTILE = MB * (MB + 1) / 2;
+  static constexpr int PG = NTILE * 256 + MP;              // partial row: tiles | u
+  static constexpr int oA = 0;                             // MP x KS  A[p][point]
+  static constexpr int oK = oA + MP * KS;                  // MP x KS  K[p][point]
+  static constexpr int oZs = oK + MP * KS;                 // MP x DS
+  static constexpr int oZn = oZs + MP * DS;
+  static constexpr int oVm = oZn + MP;
+  static constexpr int oSm1 = oVm + MP;
+  static constexpr int oCm = oSm1 + MP;                    // DQ
+  static constexpr int oXs = oCm + DQ;                     // LTW x DS
+  static constexpr int oXn = oXs + LTW * DS;               // LTW
+  static constexpr int oGm = oXn + LTW;                    // LTW
+  static constexpr int oGv = oGm + LTW;                    // LTW
+  static constexpr int total = oGv + LTW;
+};
+
+template <int MB, int DQ>
+__global__ void __launch_bounds__(64 * ((MB + 1) / 2), 2)
+gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+                       const float* __restrict__ vmean, const float* __restrict__ vstd,
+                       const float* __restrict__ hyp, const float* __restrict__ gmean,
+                       const float* __restrict__ gvar, const float* __restrict__ saved, int N, int M,
+                       int D, int nchunks, float* __restrict__ gpart) {
+  using G = LGramGeo<MB, DQ>;
+  using SV = LSaved<MB>;
+  constexpr int NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV, KS = G::KS;
+  constexpr int NU = SV::tiles / 4;                 // f32x4 units of A per chunk
+  static_assert(NU % NT == 0, "A block: whole passes");
+  extern __shared__ __attribute__((aligned(16))) float vsm[];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4, sub = tid & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int IA = wave, IB = MB - 1 - wave;
+  const bool two = IB != IA;
+  const float s2 = hyp[0];
+  const float* ls = hyp + 4 + D;
+  const int nch = (N + LTW - 1) / LTW;
+  float lsr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) lsr[v] = ls[sub + 16 * v < D ? sub + 16 * v : 0];
+  float xr[NPASS][DV];
+  lload_points<NPASS, DV, NT>(X, blockIdx.x, nchunks, nch, N, D, xr);
+  stage_inducing(Z, ls, vmean, vstd, M, D, G::MP, DQ, DS, vsm + G::oZs, vsm + G::oZn, vsm + G::oCm,
+                 vsm + G::oVm, vsm + G::oSm1, vsm + G::oA);
+  lds_barrier();
+  float cmr[DV];
+#pragma unroll
+  for (int v = 0; v < DV; ++v) cmr[v] = vsm[G::oCm + sub + 16 * v];
+  // accumulators: slot s <= IA: tile (IA, s); slot IA + 1 + s': tile (IB, s')
+  f32x4 gacc[MB + 1];
+#pragma unroll
+  for (int s = 0; s <= MB; ++s) gacc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 uacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+
+  for (int t = blockIdx.x; t < nchunks; t += gridDim.x) {
+    const int b = t / nch, i0 = (t - b * nch) * LTW;
+    const int nvalid = N - i0 < LTW ? N - i0 : LTW;
+    const long long col0 = (long long)b * N + i0;
+    float* sm = (float*)fresh_lds(vsm);
+    float* Ar = sm + G::oA;
+    float* Kr = sm + G::oK;
+    const float* zs = sm + G::oZs;
+    const float* zn = sm + G::oZn;
+    float* xs = sm + G::oXs;
+    float* xn = sm + G::oXn;
+    float* gmc = sm + G::oGm;
+    float* gvc = sm + G::oGv;
+    const float* sb = saved + (size_t)t * SV::blk;
+    // the chunk's A units (4 rows of one point each) in flight before the barrier
+    f32x4 au[NU / NT];
+#pragma unroll
+    for (int q = 0; q < NU / NT; ++q) au[q] = *(const f32x4*)(sb + 4 * (tid + q * NT));
+    lds_barrier();   // the previous chunk's reads are done
+#pragma unroll
+    for (int q = 0; q < NU / NT; ++q) {
+      // unit e: tile (rt, ct) = e / 64, lane' = e % 64 -> rows 16 rt + g' + 4u, point 16 ct + c'
+      const int e = tid + q * NT, tl = e >> 6, ln = e & 63, rt = tl >> 1, ct = tl & 1;
+      const int col = 16 * ct + (ln & 15), r0 = 16 * rt + (ln >> 4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Ar[(r0 + 4 * u) * KS + col] = au[q][u];
+    }
+    lstage_points<NPASS, DV, NT, DS>(xr, lsr, cmr, D, nvalid, xs, xn);
+    if (tid < LTW) {
+      const bool ok = tid < nvalid;
+      const float gm = gmean[ok ? col0 + tid : 0], gv = gvar[ok ? col0 + tid : 0];
+      const float keep = sb[SV::tiles + tid];
+      gmc[tid] = ok ? gm : 0.f;
+      gvc[tid] = (ok && keep != 0.f) ? gv : 0.f;   // the variance clamp passes no gradient
+    }
+    if (t + (int)gridDim.x < nchunks) lload_points<NPASS, DV, NT>(X, t + gridDim.x, nchunks, nch, N, D, xr);
+    lds_barrier();
+    // K_ZX of the wave's rows -> Kr[row][point]; u partials
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int rt = h == 0 ? IA : IB;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const float* za = zs + (16 * rt + c) * DS + g;
+        const float* xb = xs + (16 * ct + c) * DS + g;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < DQ / 4; ++k) acc = mfma32(za[4 * k], xb[4 * k], acc);
+        const int col = 16 * ct + c;
+        const float xnc = xn[col], gmv = gmc[col];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * rt + 4 * g + r;
+          float dist = zn[p] + xnc - 2.f * acc[r];
+          dist = dist < 0.f ? 0.f : dist;
+          const float kv = (p < M && col < nvalid) ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * dist) : 0.f;
+          Kr[p * KS + col] = kv;
+          uacc[h][r] = __builtin_fmaf(gmv, kv, uacc[h][r]);
+        }
+      }
+    }
+    lds_barrier();
+    // G' tiles (I >= J): A[16 I + c][8 g + j] gvar_(8 g + j) and K[16 J + c][8 g + j]
+    {
+      const f32x4 gv0 = *(const f32x4*)(gvc + 8 * g), gv1 = *(const f32x4*)(gvc + 8 * g + 4);
+      auto rowop = [&](const float* base, int rt, float (&o)[8]) {
+        const f32x4 a0 = *(const f32x4*)(base + (16 * rt + c) * KS + 8 * g);
+        const f32x4 a1 = *(const f32x4*)(base + (16 * rt + c) * KS + 8 * g + 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { o[q] = a0[q]; o[4 + q] = a1[q]; }
+      };
+      float aA[8], aB[8];
+      rowop(Ar, IA, aA);
+      rowop(Ar, two ? IB : IA, aB);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        aA[q] *= gv0[q]; aA[4 + q] *= gv1[q];
+        aB[q] *= gv0[q]; aB[4 + q] *= gv1[q];
+      }
+#pragma unroll
+      for (int s = 0; s <= MB; ++s) {
+        const bool isA = s <= IA;
+        const int J = isA ? s : s - IA - 1;
+        if (!isA && !two) break;
+        float bo[8];
+        rowop(Kr, J, bo);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) gacc[s] = mfma32(isA ? aA[q] : aB[q], bo[q], gacc[s]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  // partials: tile (I, J) at (I (I + 1) / 2 + J) * 256 + lane * 4 + r (acc layout) | u
+  float* po = gpart + (size_t)blockIdx.x * G::PG;
+#pragma unroll
+  for (int s = 0; s <= MB; ++s) {
+    const bool isA = s <= IA;
+    if (!isA && !two) break;
+    const int I = isA ? IA : IB, J = isA ? s : s - IA - 1;
+    *(f32x4*)(po + (I * (I + 1) / 2 + J) * 256 + lane * 4) = gacc[s];
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 1 && !two) break;
+    const int rt = h == 0 ? IA : IB;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = row16_sum_f(uacc[h][r]);
+      if (c == 0) po[G::NTILE * 256 + 16 * rt + 4 * g + r] = v;
+    }
+  }
+}
+
+// dL^{-1}[p][q] = m_p u_q + 2 (s_p^2 - 1) G'[p][q] for q <= p, 0 above (fp64), elementwise from
+// the fixed-order totals gtot (G' lower tiles in acc layout | u).
+__global__ void __launch_bounds__(256)
+gpk_var_gdl_l_kernel(const double* __restrict__ gtot, const float* __restrict__ vmean,
+                     const float* __restrict__ vstd, int M, int MB, double* __restrict__ dLinv) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)M * M) return;
+  const int p = (int)(e / M), q = (int)(e - (long long)p * M);
+  double v = 0.0;
+  if (q <= p) {
+    const int ti = p >> 4, tj = q >> 4, ra = p & 15, cb = q & 15;
+    const double gp = gtot[(ti * (ti + 1) / 2 + tj) * 256 + ((ra >> 2) * 16 + cb) * 4 + (ra & 3)];
+    const double u = gtot[(size_t)(MB * (MB + 1) / 2) * 256 + q];
+    const double sd = (double)vstd[p];
+    v = (double)vmean[p] * u + 2.0 * (sd * sd - 1.0) * gp;
+  }
+  dLinv[e] = v;
+}
+
 // ---------------------------------------------------------------------------
 // dL^{-1} = sum_cols dA[:, col] K[:, col]^T (lower part): split-K fp64-MFMA GEMM.
 // Workgroup = one 64 x 64 lower output tile (ti >= tj) x one split of the columns;
@@ -1788,95 +2347,120 @@ gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __r
   }
 }
 
-// Outputs from the reduced totals (one workgroup; zs staged in LDS, the d-sums split
-// over 256 / D threads each and combined in a fixed order):
-//   dZ_p = (QX_p - zs_p q_p) / l;   dl_d = (sum_p q_p zs_pd^2 - 2 sum_p zs_pd QX_pd + sum_i r_i xs_id^2) / l_d
-//   ds2 = sum Q / s2 + sum gvar;    dvmean = sum gmean A;   dvstd = 2 s sum gvar A^2
-//   dw_d = l_d (sum_i gmean_i xs_id + cm_d sum_i gmean_i);   db0 = sum_i gmean_i
-// dpar = [dvmean (M) | dvstd (M) | ds2 | dl (D) | dw (D) | db0]
+// Outputs from the reduced totals, in two launches:
+//   gpk_var_fin_kernel (ceil(M / 16) workgroups, 16 inducing points each; every workgroup stages
+//     all of Z / l for the column means -- col_means, the same fp32 sums as stage_inducing, so
+//     the identical centre -- with its global reads in flight together):
+//       dZ_p = (QX_p - zs_p q_p) / l
+//       dlp[blk][d] = sum_{p in blk} (q_p zs_pd^2 - 2 zs_pd QX_pd)      (fixed order)
+//   gpk_var_fin2_kernel (one workgroup):
+//       dl_d = (sum_blk dlp[blk][d] + sum_i r_i xs_id^2) / l_d
+//       ds2 = sum Q / s2 + sum gvar;    dvmean = sum gmean A;   dvstd = 2 s sum gvar A^2
+//       dw_d = l_d (sum_i gmean_i xs_id + cm_d sum_i gmean_i);   db0 = sum_i gmean_i
+// dpar = [dvmean (M) | dvstd (M) | ds2 | dl (D) | dw (D) | db0]  (cm: written by block 0)
+constexpr int kFinRows = 16;
+constexpr size_t kFinWsBytes = (256 / kFinRows) * 64 * sizeof(double) + 64 * sizeof(float);
 __global__ void __launch_bounds__(256)
-gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
-                   const float* __restrict__ hyp, const double* __restrict__ tot, int M, int D,
-                   float* __restrict__ dZ, float* __restrict__ dpar) {
+gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ hyp,
+                   const double* __restrict__ tot, int M, int D, float* __restrict__ dZ,
+                   double* __restrict__ dlp, float* __restrict__ cm_out) {
   extern __shared__ __attribute__((aligned(16))) float fzs[];   // M x D zs (centred Z / l)
   __shared__ double red[256];
   __shared__ float cmf[64];
-  const int tid = threadIdx.x;
-  const float s2 = hyp[0];
-  const float* ls = hyp + 4 + D;
   __shared__ float cms[kCmParts * 64];
-  // (every global read of this one-workgroup kernel is issued in batches of 8 per thread:
-  // one memory latency per batch instead of one per element)
-  for (int base = 0; base < M * D; base += 8 * 256) {
-    float zv[8], lv[8];
+  const int tid = threadIdx.x;
+  const float* ls = hyp + 4 + D;
+  for (int base = 0; base < M * D; base += 32 * 256) {
+    float zv[32], lv[32];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 32; ++u) {
       const int e = base + 256 * u + tid, ec = e < M * D ? e : 0;
       zv[u] = Z[ec];
       lv[u] = ls[ec % D];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 32; ++u) {
       const int e = base + 256 * u + tid;
       if (e < M * D) fzs[e] = zv[u] / lv[u];
     }
   }
   lds_barrier();
   col_means(fzs, M, D, D, D, cms, cmf);   // the same fp32 sums as stage_inducing: the identical centre
-  for (int e = tid; e < M * D; e += 256) fzs[e] -= cmf[e % D];
+  const int p0 = blockIdx.x * kFinRows;
+  const int np = M - p0 < kFinRows ? M - p0 : kFinRows;
+  if (blockIdx.x == 0 && tid < D) cm_out[tid] = cmf[tid];
+  for (int e = tid; e < np * D; e += 256) fzs[p0 * D + e] -= cmf[e % D];
   lds_barrier();
   const double* QX = tot;
   const double* q = tot + (size_t)M * D;
-  const double* dvm = q + M;
-  const double* dsm = dvm + M;
-  const double* rx2 = dsm + M;
-  const double sumQ = rx2[D], sumgv = rx2[D + 1];
-  const double* gx = rx2 + D + 2;
-  const double sumgm = gx[D];
-  for (int base = 0; base < M * D; base += 8 * 256) {
-    double xv[8], qv[8];
-    float lv[8];
+  {
+    const int e = tid;   // np * D <= 16 * 64 = 1024: up to 4 per thread, loads together
+    double xv[4], qv[4];
+    float lv[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = base + 256 * u + tid, ec = e < M * D ? e : 0;
-      const int p = ec / D, d = ec - p * D;
-      xv[u] = QX[ec];
+    for (int u = 0; u < 4; ++u) {
+      const int ee = e + 256 * u, ok = ee < np * D;
+      const int p = p0 + (ok ? ee / D : 0), d = ok ? ee % D : 0;
+      xv[u] = QX[(size_t)p * D + d];
       qv[u] = q[p];
       lv[u] = ls[d];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = base + 256 * u + tid;
-      if (e < M * D) dZ[e] = (float)((xv[u] - (double)fzs[e] * qv[u]) / (double)lv[u]);
+    for (int u = 0; u < 4; ++u) {
+      const int ee = e + 256 * u;
+      if (ee < np * D) {
+        const int p = p0 + ee / D, d = ee % D;
+        const double zsv = (double)fzs[p * D + d];
+        dZ[(size_t)p * D + d] = (float)((xv[u] - zsv * qv[u]) / (double)lv[u]);
+      }
     }
   }
+  // per-d partial over this block's rows: threads (d, k), k = tid / D, rows p0 + k, p0 + k + nk..
   const int nk = 256 / D;
   double acc = 0.0;
   if (tid < nk * D) {
     const int d = tid % D, k = tid / D;
-    for (int p0 = k; p0 < M; p0 += 8 * nk) {   // p ascending, as one sequential sum
-      double qv[8], xv[8];
+    double qv[kFinRows], xv[kFinRows];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int p = p0 + nk * u, pc = p < M ? p : 0;
-        qv[u] = q[pc];
-        xv[u] = QX[(size_t)pc * D + d];
-      }
+    for (int u = 0; u < kFinRows; ++u) {
+      const int pl = k + nk * u, p = p0 + (pl < np ? pl : 0);
+      qv[u] = q[p];
+      xv[u] = QX[(size_t)p * D + d];
+    }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int p = p0 + nk * u;
-        if (p < M) {
-          const double zsv = (double)fzs[p * D + d];
-          acc += qv[u] * zsv * zsv - 2.0 * zsv * xv[u];
-        }
+    for (int u = 0; u < kFinRows; ++u) {
+      const int pl = k + nk * u;
+      if (pl < np) {
+        const double zsv = (double)fzs[(p0 + pl) * D + d];
+        acc += qv[u] * zsv * zsv - 2.0 * zsv * xv[u];
       }
     }
   }
   red[tid] = acc;
   lds_barrier();
   if (tid < D) {
-    double v = rx2[tid];
+    double v = 0.0;
     for (int k = 0; k < nk; ++k) v += red[k * D + tid];
+    dlp[(size_t)blockIdx.x * D + tid] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+gpk_var_fin2_kernel(const float* __restrict__ vstd, const float* __restrict__ hyp,
+                    const double* __restrict__ tot, int M, int D, int nblk,
+                    const double* __restrict__ dlp, const float* __restrict__ cmf, float* __restrict__ dpar) {
+  const int tid = threadIdx.x;
+  const float s2 = hyp[0];
+  const float* ls = hyp + 4 + D;
+  const double* dvm = tot + (size_t)M * D + M;
+  const double* dsm = dvm + M;
+  const double* rx2 = dsm + M;
+  const double sumQ = rx2[D], sumgv = rx2[D + 1];
+  const double* gx = rx2 + D + 2;
+  const double sumgm = gx[D];
+  if (tid < D) {
+    double v = rx2[tid];
+    for (int k = 0; k < nblk; ++k) v += dlp[(size_t)k * D + tid];
     dpar[2 * M + 1 + tid] = (float)(v / (double)ls[tid]);
     dpar[2 * M + 1 + D + tid] = (float)((double)ls[tid] * (gx[tid] + (double)cmf[tid] * sumgm));
   }
@@ -1889,6 +2473,10 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
     dpar[2 * M + 1 + 2 * D] = (float)sumgm;
   }
 }
+
+// the two output launches (ws: nblk x D doubles of dl partials, then D floats of the centre)
+int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const double* tot, int M, int D,
+                   float* dZ, float* dpar, void* ws, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Register-resident variants for M <= 64, D <= 32 (BASELINE cfg 5: M = 64, D = 32).
@@ -2714,6 +3302,16 @@ int launch_var_fwd(const GpkVarArgs& a, int* flags, hipStream_t stream) {
   return e == hipSuccess ? 0 : (int)e;
 }
 
+// The saved-state adjoint (gpk_var_adjs_l_kernel + K-Gram) serves M > 64 when its LDS plan fits
+// (D <= 32 at M = 256); the training forward then keeps A for it.
+template <int MB, int DQ>
+constexpr bool var_saved_fits() {
+  if constexpr (MB >= 5) return LAdjGeo<MB, DQ>::fits && (size_t)LGramGeo<MB, DQ>::total * 4 <= 160 * 1024;
+  return false;
+}
+template <int MB, int DQ>
+bool var_saved_path(int M) { return var_saved_fits<MB, DQ>() && M > 64; }
+
 template <int MB, int DQ>
 int launch_var_fwd_l(const GpkVarArgs& a, int* flags, hipStream_t stream) {
   using G = LGeo<MB, DQ>;
@@ -2723,9 +3321,11 @@ int launch_var_fwd_l(const GpkVarArgs& a, int* flags, hipStream_t stream) {
   const long long nch = (long long)a.B * ((a.N + LTW - 1) / LTW);
   if (nch > 0x7fffffffLL) return -8;
   const int per_cu = G::NWV <= 4 ? 2 : 1;   // <= 2 waves per SIMD (256 VGPRs: L^{-1} resident)
+  // the training forward keeps A for the adjoint when the saved-state adjoint serves this shape
+  float* saved = (a.saved != nullptr && var_saved_path<MB, DQ>(a.M)) ? a.saved : nullptr;
   hipLaunchKernelGGL((gpk_var_fwd_l_kernel<MB, DQ>), dim3(chunk_grid(nch, per_cu)), dim3(G::NT), lds,
                      stream, a.X, a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.N, a.M, a.D, (int)nch,
-                     a.mean, a.var, flags);
+                     a.mean, a.var, flags, saved);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   if (a.ell != nullptr) {
@@ -2743,7 +3343,7 @@ int launch_var_fwd_l(const GpkVarArgs& a, int* flags, hipStream_t stream) {
 struct AdjPlan {
   int nchunks, nwg, P, ntiles, nsplit;
   long long BN, cols_per_split;
-  size_t off_dA, off_K, off_part, off_tot, off_dl, total;  // byte offsets
+  size_t off_dA, off_K, off_part, off_tot, off_dl, off_fin, total;  // byte offsets
   size_t fin_lds;
 };
 
@@ -2790,6 +3390,7 @@ AdjPlan adj_plan(int B, int N, int M, int D) {
     p.off_part = o; o = al(o + (size_t)p.nwg * p.P * sizeof(float));
     p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
     p.off_dl = o; o = al(o + (size_t)kGPart * sizeof(double));
+    p.off_fin = o; o = al(o + kFinWsBytes);
     p.total = o;
     return p;
   }
@@ -2818,6 +3419,7 @@ AdjPlan adj_plan_common(AdjPlan p, int B, int N, int M, int D) {
   p.off_part = o; o = al(o + (size_t)p.nwg * p.P * sizeof(float));
   p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
   p.off_dl = o; o = al(o + (size_t)p.nsplit * p.ntiles * 4096 * sizeof(double));
+  p.off_fin = o; o = al(o + kFinWsBytes);
   p.total = o;
   return p;
 }
@@ -2843,7 +3445,14 @@ int launch_var_fwd_r(const GpkVarArgs& a, int* flags, hipStream_t stream) {
 int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t stream);
 
 template <int MB, int DQ>
+int launch_var_adj_saved(const GpkVarAdjArgs& a, hipStream_t stream);
+
+template <int MB, int DQ>
 int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
+  if (a.saved != nullptr) {
+    if (!var_saved_path<MB, DQ>(a.M)) return -13;
+    return launch_var_adj_saved<MB, DQ>(a, stream);
+  }
   const AdjPlan p = adj_plan<MB>(a.B, a.N, a.M, a.D);
   char* ws = (char*)a.ws;
   float* wsdA = (float*)(ws + p.off_dA);
@@ -2877,11 +3486,7 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(gpk_var_gdl_kernel, dim3(1), dim3(256), 0, stream, gtot, a.Linv, a.vmean, a.vstd,
                        a.M, a.dLinv);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    set_lds_once<gpk_var_fin_kernel, 64 * 1024>();
-    hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(1), dim3(256), p.fin_lds, stream, a.Z, a.vstd, a.hyp,
-                       tot, a.M, a.D, a.dZ, a.dpar);
-    e = hipGetLastError();
-    return e == hipSuccess ? 0 : (int)e;
+    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream);
   }
   if constexpr (var_adj_lreg_fits<MB, DQ>()) {
     if (GPK_VAR_LREG && a.M > 64 && (long long)a.M * p.BN * 4 < (1LL << 31)) {
@@ -2914,6 +3519,22 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
   return launch_var_adj_tail(a, p, stream);
 }
 
+int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const double* tot, int M, int D,
+                   float* dZ, float* dpar, void* ws, hipStream_t stream) {
+  const int nblk = (M + kFinRows - 1) / kFinRows;
+  double* dlp = (double*)ws;
+  float* cm = (float*)(dlp + (size_t)nblk * D);
+  set_lds_once<gpk_var_fin_kernel, 64 * 1024>();   // + ~3.3 KB static
+  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(nblk), dim3(256), (size_t)M * D * sizeof(float), stream, Z, hyp,
+                     tot, M, D, dZ, dlp, cm);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gpk_var_fin2_kernel, dim3(1), dim3(256), 0, stream, vstd, hyp, tot, M, D, nblk, dlp, cm,
+                     dpar);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
 // dL^{-1} GEMM, the fixed-order reductions and the outputs (both adjoint paths)
 int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t stream) {
   char* ws = (char*)a.ws;
@@ -2931,11 +3552,75 @@ int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t st
                      wspart, p.nwg, p.P, tot, dl, p.nsplit, p.ntiles, a.M, a.dLinv);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  set_lds_once<gpk_var_fin_kernel, 64 * 1024>();   // + ~2.3 KB static
-  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(1), dim3(256), p.fin_lds, stream, a.Z, a.vstd, a.hyp,
-                     tot, a.M, a.D, a.dZ, a.dpar);
-  e = hipGetLastError();
-  return e == hipSuccess ? 0 : (int)e;
+  return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream);
+}
+
+// ---- the saved-state adjoint (M > 64): workspace G' partials | adjoint partials | their fp64 totals
+// | the finalisation partials
+struct AdjSavedPlan {
+  int nchunks, nwg, nwg_g, P, PG;
+  long long BN;
+  size_t off_gpart, off_part, off_tot, off_gtot, off_fin, total, fin_lds;
+};
+
+template <int MB, int DQ>
+AdjSavedPlan adj_saved_plan(int B, int N, int M, int D) {
+  using LG = LGramGeo<MB, DQ>;
+  AdjSavedPlan p{};
+  const long long nch = (long long)B * ((N + LTW - 1) / LTW);
+  p.nchunks = (int)nch;
+  p.nwg = chunk_grid(nch, 1);      // 256 VGPRs: one 8-wave workgroup per CU
+  p.nwg_g = chunk_grid(nch, 1);
+  p.P = M * D + 3 * M + 2 * D + 3;
+  p.PG = LG::PG;
+  p.BN = (long long)B * N;
+  p.fin_lds = (size_t)M * D * sizeof(float);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t o = 0;
+  p.off_gpart = o; o = al(o + (size_t)p.nwg_g * p.PG * sizeof(float));
+  p.off_part = o; o = al(o + (size_t)p.nwg * p.P * sizeof(float));
+  p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
+  p.off_gtot = o; o = al(o + (size_t)p.PG * sizeof(double));
+  p.off_fin = o; o = al(o + kFinWsBytes);
+  p.total = o;
+  return p;
+}
+
+template <int MB, int DQ>
+int launch_var_adj_saved(const GpkVarAdjArgs& a, hipStream_t stream) {
+  if constexpr (var_saved_fits<MB, DQ>()) {
+    using LA = LAdjGeo<MB, DQ>;
+    using LG = LGramGeo<MB, DQ>;
+    const AdjSavedPlan p = adj_saved_plan<MB, DQ>(a.B, a.N, a.M, a.D);
+    char* ws = (char*)a.ws;
+    float* gpart = (float*)(ws + p.off_gpart);
+    float* wspart = (float*)(ws + p.off_part);
+    double* tot = (double*)(ws + p.off_tot);
+    double* gtot = (double*)(ws + p.off_gtot);
+    set_lds_once<gpk_var_adjs_l_kernel<MB, DQ>>();
+    hipLaunchKernelGGL((gpk_var_adjs_l_kernel<MB, DQ>), dim3(p.nwg), dim3(LA::NT), (size_t)LA::k_total * sizeof(float),
+                       stream, a.X, a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.saved, a.N, a.M,
+                       a.D, p.nchunks, wspart, a.dX);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    set_lds_once<gpk_var_kgram_l_kernel<MB, DQ>>();
+    hipLaunchKernelGGL((gpk_var_kgram_l_kernel<MB, DQ>), dim3(p.nwg_g), dim3(LG::NT), (size_t)LG::total * sizeof(float),
+                       stream, a.X, a.Z, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.saved, a.N, a.M, a.D,
+                       p.nchunks, gpart);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.PG + 31) / 32), dim3(256), 0, stream, gpart, p.nwg_g, p.PG,
+                       gtot, nullptr, 0, 0, 0, nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.P + 31) / 32), dim3(256), 0, stream, wspart, p.nwg, p.P, tot,
+                       nullptr, 0, 0, 0, nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(gpk_var_gdl_l_kernel, dim3((unsigned)(((long long)a.M * a.M + 255) / 256)), dim3(256), 0,
+                       stream, gtot, a.vmean, a.vstd, a.M, MB, a.dLinv);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream);
+  } else {
+    return -13;
+  }
 }
 
 // Instantiated row-block counts; M is padded up to the next one (zero rows).
@@ -2980,6 +3665,27 @@ size_t gpk_var_adjoint_ws_bytes(int B, int N, int M, int D) {
 #define GPK_CALL_WS(mb) return adj_plan<mb>(B, N, M, D).total;
   GPK_MB_SWITCH((M + 15) / 16, GPK_CALL_WS)
 #undef GPK_CALL_WS
+  return 0;
+}
+
+// the saved-state path (training forward keeps A; M > 64, its LDS plan fits): bytes of the saved
+// state and of the adjoint's workspace, 0 when the path does not serve the shape
+size_t gpk_var_saved_bytes(int B, int N, int M, int D) {
+#define GPK_CALL_SV(mb)                                                                        \
+  if (adj_dq(D) == 32) return var_saved_path<mb, 32>(M) ? (size_t)B * ((N + LTW - 1) / LTW) *  \
+                                  LSaved<mb>::blk * sizeof(float) : 0;                        \
+  return var_saved_path<mb, 64>(M) ? (size_t)B * ((N + LTW - 1) / LTW) * LSaved<mb>::blk * sizeof(float) : 0;
+  GPK_MB_SWITCH((M + 15) / 16, GPK_CALL_SV)
+#undef GPK_CALL_SV
+  return 0;
+}
+size_t gpk_var_adjoint_saved_ws_bytes(int B, int N, int M, int D) {
+  if (gpk_var_saved_bytes(B, N, M, D) == 0) return 0;
+#define GPK_CALL_SW(mb)                                                        \
+  if (adj_dq(D) == 32) return adj_saved_plan<mb, 32>(B, N, M, D).total;        \
+  return adj_saved_plan<mb, 64>(B, N, M, D).total;
+  GPK_MB_SWITCH((M + 15) / 16, GPK_CALL_SW)
+#undef GPK_CALL_SW
   return 0;
 }
 

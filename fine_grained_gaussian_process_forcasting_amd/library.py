@@ -30,7 +30,7 @@ from typing import Tuple
 import torch
 from torch import Tensor
 
-from . import ops
+from . import _native, ops
 
 # ---------------------------------------------------------------------------
 # exact GP marginal log likelihood (gpk_exact_mll_f32 / gpk_exact_mll_grad_f32)
@@ -151,48 +151,60 @@ def _var_hyper(x, s2, ls, w, b0, jitter):
     return ops.pack_variational_hyper(s2.detach(), 1.0, jitter, b0.detach(), w.detach(), lsv, D, x.device)
 
 
+def _saved_numel(x, Z, save):
+    if not save:
+        return 0
+    B, N, D = x.shape
+    return _native.lib().gpk_variational_saved_bytes(B, N, Z.shape[0], D) // 4
+
+
 @torch.library.custom_op("gpk::variational_fwd", mutates_args=(), device_types="cuda")
 def variational_fwd(x: Tensor, Linv: Tensor, Z: Tensor, vmean: Tensor, vstd: Tensor, s2: Tensor,
-                    ls: Tensor, w: Tensor, b0: Tensor, jitter: float) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
-    """-> (mean, var, clamp flags, packed hyper vector). The hyper vector is returned so the
-    backward reuses it (one pack per GP call, not one per direction)."""
+                    ls: Tensor, w: Tensor, b0: Tensor, jitter: float,
+                    save: bool = False) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """-> (mean, var, clamp flags, packed hyper vector, saved state). The hyper vector is
+    returned so the backward reuses it (one pack per GP call, not one per direction).
+    ``save`` (a gradient will be needed): the forward keeps A = Linv K_ZX and the clamp mask
+    for the saved-state adjoint where it serves the shape (M > 64; gpk_variational_train_f32),
+    else the state is empty and the adjoint recomputes."""
     hyper = _var_hyper(x, s2, ls, w, b0, jitter)
-    out = ops.variational_forward(x, Z, Linv, vmean, vstd, hyper=hyper)
-    return out.mean, out.var, out.flags, hyper
+    out = ops.variational_forward(x, Z, Linv, vmean, vstd, hyper=hyper, save=save)
+    saved = out.saved if out.saved is not None else x.new_empty(0)
+    return out.mean, out.var, out.flags, hyper, saved
 
 
 @variational_fwd.register_fake
-def _(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter):
+def _(x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter, save=False):
     B, N, D = x.shape
     return (x.new_empty(B, N), x.new_empty(B, N), x.new_empty(1, dtype=torch.int32),
-            x.new_empty(4 + 2 * D))
+            x.new_empty(4 + 2 * D), x.new_empty(_saved_numel(x, Z, save)))
 
 
 @torch.library.custom_op("gpk::variational_adj", mutates_args=(), device_types="cuda")
 def variational_adj(x: Tensor, Linv: Tensor, Z: Tensor, vmean: Tensor, vstd: Tensor, hyper: Tensor,
-                    gmean: Tensor, gvar: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
-    """-> (dX, dLinv, dZ (K_ZX part), dpar = [dvmean (M), dvstd (M), ds2, dls (D), dw (D), db0])."""
-    B, N, D = x.shape
-    M = Z.shape[0]
-    adj = ops.variational_adjoint(x, Z, Linv, vmean, vstd, hyper, gmean, gvar)
+                    gmean: Tensor, gvar: Tensor, saved: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """-> (dX, dLinv, dZ (K_ZX part), dpar = [dvmean (M), dvstd (M), ds2, dls (D), dw (D), db0]).
+    ``saved``: the forward's state (empty: recompute the forward inside the adjoint)."""
+    adj = ops.variational_adjoint(x, Z, Linv, vmean, vstd, hyper, gmean, gvar,
+                                  saved=saved if saved.numel() > 0 else None)
     return adj.dX, adj.dLinv, adj.dZ, adj.dpar
 
 
 @variational_adj.register_fake
-def _(x, Linv, Z, vmean, vstd, hyper, gmean, gvar):
+def _(x, Linv, Z, vmean, vstd, hyper, gmean, gvar, saved):
     M, D = Z.shape
     return (torch.empty_like(x), torch.empty_like(Linv), torch.empty_like(Z),
             x.new_empty(2 * M + 2 * D + 2))
 
 
 def _var_setup(ctx, inputs, output):
-    x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter = inputs
-    ctx.save_for_backward(x, Linv, Z, vmean, vstd, s2, ls, w, b0, output[3])
-    ctx.mark_non_differentiable(output[2], output[3])
+    x, Linv, Z, vmean, vstd, s2, ls, w, b0, jitter = inputs[:10]
+    ctx.save_for_backward(x, Linv, Z, vmean, vstd, s2, ls, w, b0, output[3], output[4])
+    ctx.mark_non_differentiable(output[2], output[3], output[4])
 
 
-def _var_backward(ctx, gmean, gvar, _gflags, _ghyper):
-    x, Linv, Z, vmean, vstd, s2, ls, w, b0, hyper = ctx.saved_tensors
+def _var_backward(ctx, gmean, gvar, _gflags, _ghyper, _gsaved):
+    x, Linv, Z, vmean, vstd, s2, ls, w, b0, hyper, saved = ctx.saved_tensors
     B, N, D = x.shape
     M = Z.shape[0]
     if gmean is None:
@@ -200,12 +212,12 @@ def _var_backward(ctx, gmean, gvar, _gflags, _ghyper):
     if gvar is None:
         gvar = x.new_zeros(B, N)
     dX, dLinv, dZ, dpar = torch.ops.gpk.variational_adj(x, Linv, Z, vmean, vstd, hyper,
-                                                        gmean.contiguous(), gvar.contiguous())
+                                                        gmean.contiguous(), gvar.contiguous(), saved)
     dls = dpar[2 * M + 1:2 * M + 1 + D]
     dls = dls.sum().reshape(ls.shape) if ls.numel() == 1 else dls.reshape(ls.shape)
     return (dX, dLinv, dZ, dpar[:M].reshape(vmean.shape), dpar[M:2 * M].reshape(vstd.shape),
             dpar[2 * M].reshape(s2.shape), dls, dpar[2 * M + 1 + D:2 * M + 1 + 2 * D].reshape(w.shape),
-            dpar[2 * M + 1 + 2 * D].reshape(b0.shape), None)
+            dpar[2 * M + 1 + 2 * D].reshape(b0.shape), None, None)
 
 
 variational_fwd.register_autograd(_var_backward, setup_context=_var_setup)

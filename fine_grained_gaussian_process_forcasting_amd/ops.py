@@ -390,6 +390,7 @@ class VariationalOut:
     var: torch.Tensor            # (B, N) clamped at 1e-6
     ell: Optional[torch.Tensor]  # (B,) sum over N of the expected log likelihood
     flags: Optional[torch.Tensor]  # (1,) int32: bit 0 = the variance clamp fired
+    saved: Optional[torch.Tensor] = None  # training state for variational_adjoint (M > 64), or None
 
 
 _CONST_PAIRS: dict = {}
@@ -428,9 +429,13 @@ def pack_variational_hyper(outputscale, noise, jitter, bias, weights, lengthscal
 def variational_forward(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vmean: torch.Tensor,
                         vstd: torch.Tensor, outputscale=None, noise=None, jitter=None, bias=None,
                         weights=None, lengthscale=None, y: Optional[torch.Tensor] = None,
-                        hyper: Optional[torch.Tensor] = None, want_flags: bool = True) -> VariationalOut:
+                        hyper: Optional[torch.Tensor] = None, want_flags: bool = True,
+                        save: bool = False) -> VariationalOut:
     """Batched q(f) mean / variance (+ expected log likelihood sum when y is given)
-    for the whitened mean-field VariationalStrategy (include/gpk.h::gpk_variational_f32)."""
+    for the whitened mean-field VariationalStrategy (include/gpk.h::gpk_variational_f32).
+    ``save=True`` (training): where the saved-state adjoint serves the shape (M > 64), the
+    forward also keeps A = Linv K_ZX and the clamp mask (gpk_variational_train_f32) in
+    ``out.saved`` for ``variational_adjoint(..., saved=out.saved)``; None elsewhere."""
     if X.dim() != 3:
         raise ValueError(f"X must be (B, N, D), got {tuple(X.shape)}")
     B, N, D = X.shape
@@ -457,7 +462,18 @@ def variational_forward(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
     var = torch.empty(B, N, device=dev, dtype=torch.float32)
     ell = torch.empty(B, device=dev, dtype=torch.float32) if y is not None else None
     flags = torch.empty(1, device=dev, dtype=torch.int32) if want_flags else None
-    rc = _native.lib().gpk_variational_f32(
+    lib = _native.lib()
+    nsaved = lib.gpk_variational_saved_bytes(B, N, M, D) if (save and B > 0) else 0
+    if nsaved > 0:
+        saved = torch.empty(nsaved // 4, device=dev, dtype=torch.float32)
+        rc = lib.gpk_variational_train_f32(
+            X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
+            hyper.data_ptr(), y.data_ptr() if y is not None else None, B, N, M, D,
+            mean.data_ptr(), var.data_ptr(), ell.data_ptr() if ell is not None else None,
+            flags.data_ptr() if flags is not None else None, saved.data_ptr(), _stream_ptr(dev))
+        _native.check(rc, "gpk_variational_train_f32")
+        return VariationalOut(mean, var, ell, flags, saved)
+    rc = lib.gpk_variational_f32(
         X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
         hyper.data_ptr(), y.data_ptr() if y is not None else None, B, N, M, D,
         mean.data_ptr(), var.data_ptr(), ell.data_ptr() if ell is not None else None,
@@ -482,9 +498,10 @@ class VariationalAdjoint:
 
 def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vmean: torch.Tensor,
                         vstd: torch.Tensor, hyper: torch.Tensor, gmean: torch.Tensor,
-                        gvar: torch.Tensor) -> VariationalAdjoint:
+                        gvar: torch.Tensor, saved: Optional[torch.Tensor] = None) -> VariationalAdjoint:
     """Adjoint of ``variational_forward`` except the shared K_ZZ factor (fused gfx950
-    kernels behind include/gpk.h::gpk_variational_adjoint_f32)."""
+    kernels behind include/gpk.h::gpk_variational_adjoint_f32; from the training forward's
+    ``saved`` state: gpk_variational_adjoint_saved_f32)."""
     B, N, D = X.shape
     M = Z.shape[0]
     _require_device(X, Z, Linv, vmean, vstd, hyper, gmean, gvar)
@@ -497,7 +514,12 @@ def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
     gmean = gmean.detach().reshape(B, N).contiguous().float()
     gvar = gvar.detach().reshape(B, N).contiguous().float()
     lib = _native.lib()
-    nbytes = lib.gpk_variational_adjoint_workspace_bytes(B, N, M, D)
+    if saved is not None:
+        if saved.numel() * 4 != lib.gpk_variational_saved_bytes(B, N, M, D):
+            raise ValueError("saved state does not match this shape (variational_forward(save=True))")
+        nbytes = lib.gpk_variational_adjoint_saved_workspace_bytes(B, N, M, D)
+    else:
+        nbytes = lib.gpk_variational_adjoint_workspace_bytes(B, N, M, D)
     if nbytes == 0:
         raise ValueError(f"unsupported variational shape B={B} N={N} M={M} D={D}")
     ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
@@ -505,11 +527,20 @@ def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
     dLinv = torch.empty(M, M, device=dev, dtype=torch.float64)
     dZ = torch.empty(M, D, device=dev, dtype=torch.float32)
     dpar = torch.empty(2 * M + 2 * D + 2, device=dev, dtype=torch.float32)
-    rc = lib.gpk_variational_adjoint_f32(
-        X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
-        hyper.data_ptr(), gmean.data_ptr(), gvar.data_ptr(), B, N, M, D, ws.data_ptr(),
-        dX.data_ptr(), dLinv.data_ptr(), dZ.data_ptr(), dpar.data_ptr(), _stream_ptr(dev))
-    _native.check(rc, "gpk_variational_adjoint_f32")
+    if saved is not None:
+        _require_device(saved)
+        rc = lib.gpk_variational_adjoint_saved_f32(
+            X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
+            hyper.data_ptr(), gmean.data_ptr(), gvar.data_ptr(), saved.detach().contiguous().data_ptr(),
+            B, N, M, D, ws.data_ptr(), dX.data_ptr(), dLinv.data_ptr(), dZ.data_ptr(), dpar.data_ptr(),
+            _stream_ptr(dev))
+        _native.check(rc, "gpk_variational_adjoint_saved_f32")
+    else:
+        rc = lib.gpk_variational_adjoint_f32(
+            X.data_ptr(), Z.data_ptr(), Linv.data_ptr(), vmean.data_ptr(), vstd.data_ptr(),
+            hyper.data_ptr(), gmean.data_ptr(), gvar.data_ptr(), B, N, M, D, ws.data_ptr(),
+            dX.data_ptr(), dLinv.data_ptr(), dZ.data_ptr(), dpar.data_ptr(), _stream_ptr(dev))
+        _native.check(rc, "gpk_variational_adjoint_f32")
     return VariationalAdjoint(dX, dLinv, dpar, dZ, dpar[:M], dpar[M:2 * M], dpar[2 * M],
                               dpar[2 * M + 1:2 * M + 1 + D], dpar[2 * M + 1 + D:2 * M + 1 + 2 * D],
                               dpar[2 * M + 1 + 2 * D])

@@ -143,7 +143,10 @@ def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module
         cache = KzzCache()
         key_tensors = (Z, s2, ls)
     Linv = cache.factor(Z, s2, ls, jitter, key_tensors)
-    mean, var, flags, _ = torch.ops.gpk.variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0, float(jitter))
+    # training (a gradient will flow): the forward keeps A for the saved-state adjoint
+    save = torch.is_grad_enabled() and any(t.requires_grad for t in (x, Linv, Z, vmean, vstd, s2, ls, w, b0))
+    mean, var, flags, _, _ = torch.ops.gpk.variational_fwd(x, Linv, Z, vmean, vstd, s2, ls, w, b0,
+                                                           float(jitter), save)
     cache.note_consumers(mean, var)
     cache.check_pending()
     return mean, var, flags

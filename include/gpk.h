@@ -270,6 +270,34 @@ int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Li
                                 void* stream);
 
 /*
+ * Training pair of the variational path for M > 64 (the reference's DeepGP default M = 256,
+ * denoising_model/DeepGP.py:15): the forward keeps state the adjoint consumes, so the adjoint
+ * neither repeats the forward's A = Linv K_ZX GEMM nor round-trips dA / K_ZX through HBM.
+ *   gpk_variational_saved_bytes(B, N, M, D): bytes of that state; 0 when the shape is served
+ *     by the recompute adjoint only (M <= 64, or the saved path's LDS plan does not fit).
+ *   gpk_variational_train_f32: gpk_variational_f32 + `saved` (device, saved_bytes bytes; may be
+ *     NULL only when saved_bytes is 0): A (fp32, as the reference casts it) and the variance
+ *     clamp mask of every point.
+ *   gpk_variational_adjoint_saved_f32: gpk_variational_adjoint_f32 from that state (same
+ *     outputs, same argument meaning; -12 when saved_bytes is 0 for the shape), workspace of
+ *     gpk_variational_adjoint_saved_workspace_bytes(B, N, M, D) bytes. dLinv is formed as
+ *     m u^T + 2 diag(s^2 - 1) Linv G with u = K_ZX gmean, G = K_ZX diag(gvar) K_ZX^T
+ *     (= sum_i dA_i K_i^T with the fp64 A; the recompute path uses the fp32-cast A).
+ * Replaces (reference): the same forward / autograd backward as the two functions above.
+ */
+size_t gpk_variational_saved_bytes(int B, int N, int M, int D);
+int gpk_variational_train_f32(const float* X, const float* Z, const double* Linv, const float* vmean,
+                              const float* vstd, const float* hyp, const float* y, int B, int N, int M,
+                              int D, float* mean, float* var, float* ell, int* flags, void* saved,
+                              void* stream);
+size_t gpk_variational_adjoint_saved_workspace_bytes(int B, int N, int M, int D);
+int gpk_variational_adjoint_saved_f32(const float* X, const float* Z, const double* Linv,
+                                      const float* vmean, const float* vstd, const float* hyp,
+                                      const float* gmean, const float* gvar, const void* saved, int B,
+                                      int N, int M, int D, void* workspace, float* dX, double* dLinv,
+                                      float* dZ, float* dpar, void* stream);
+
+/*
  * GPU-resident training-window gather:
  *   for window b with first row r = rows[b] of the (id, time)-sorted table:
  *     enc[b] = table[r      : r + n_enc]                  (n_enc, F)

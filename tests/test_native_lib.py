@@ -134,11 +134,21 @@ def test_custom_ops_registered_with_fake_and_autograd():
         Z = torch.empty(8, 4)
         Linv, Lz, inf = torch.ops.gpk.kzz_factor(Z, torch.empty(()), torch.empty(4), 1e-4, 1e-8, 3)
         assert Linv.shape == (8, 8) and Linv.dtype == torch.float64
-        mean, var, flags, hyp = torch.ops.gpk.variational_fwd(X, Linv, Z, torch.empty(8), torch.empty(8),
-                                                              torch.empty(()), torch.empty(4), torch.empty(4),
-                                                              torch.empty(()), 1e-4)
+        mean, var, flags, hyp, saved = torch.ops.gpk.variational_fwd(
+            X, Linv, Z, torch.empty(8), torch.empty(8), torch.empty(()), torch.empty(4), torch.empty(4),
+            torch.empty(()), 1e-4)
         assert mean.shape == (3, 16) and var.shape == (3, 16) and flags.shape == (1,)
-        assert hyp.shape == (4 + 2 * 4,)
+        assert hyp.shape == (4 + 2 * 4,) and saved.numel() == 0
+        # training at M = 256: the forward's saved state for the saved-state adjoint (16 row tiles x
+        # 2 column tiles of A per 32-point chunk + the chunk's clamp mask)
+        Z2 = torch.empty(256, 4)
+        L2 = torch.empty(256, 256, dtype=torch.float64)
+        out = torch.ops.gpk.variational_fwd(X, L2, Z2, torch.empty(256), torch.empty(256), torch.empty(()),
+                                            torch.empty(4), torch.empty(4), torch.empty(()), 1e-4, True)
+        assert out[4].numel() == 3 * 1 * (16 * 2 * 256 + 32)
+        dX, dL, dZ, dpar = torch.ops.gpk.variational_adj(X, L2, Z2, torch.empty(256), torch.empty(256), hyp,
+                                                         mean, var, out[4])
+        assert dX.shape == X.shape and dL.shape == (256, 256) and dpar.shape == (2 * 256 + 2 * 4 + 2,)
 
 
 def test_posterior_entry_validation_without_device():

@@ -58,25 +58,33 @@ def test_variational_grads_vs_oracle(cuda_device, B, N, M, D):
         assert e <= TOL, (k, e)
 
 
-def _op_level_grads(dev, X, Z, m, s, w, b0, ls, s2, gmean, gvar, jitter, var_jitter):
+def _op_level_grads(dev, X, Z, m, s, w, b0, ls, s2, gmean, gvar, jitter, var_jitter, saved=False):
     """The product backward composed from the op-level entry points (what
-    _VariationalPredict + _KzzFactor do), with a separate K_XX jitter (test hook)."""
+    _VariationalPredict + _KzzFactor do), with a separate K_XX jitter (test hook).
+    ``saved``: the training pair (forward keeps A, gpk_variational_adjoint_saved_f32) where it
+    serves the shape; the recompute adjoint otherwise."""
     from fine_grained_gaussian_process_forcasting_amd import ops
     D = X.shape[-1]
     lst = torch.tensor(ls, dtype=torch.float32, device=dev)
     f = ops.kzz_cholesky(Z.to(dev), s2, lst, jitter=jitter)
     hyper = ops.pack_variational_hyper(s2, 1.0, var_jitter, b0, w.to(dev), lst, D, dev)
+    st = None
+    if saved:
+        st = ops.variational_forward(X.to(dev), Z.to(dev), f.Linv, m.to(dev), s.to(dev), hyper=hyper,
+                                     save=True).saved
     adj = ops.variational_adjoint(X.to(dev), Z.to(dev), f.Linv, m.to(dev), s.to(dev), hyper,
-                                  gmean.to(dev), gvar.to(dev))
+                                  gmean.to(dev), gvar.to(dev), saved=st)
     dZk, ds2k, dlsk = ops.kzz_backward(adj.dLinv, f.L, f.Linv, Z.to(dev), torch.tensor(s2, device=dev), lst)
     return {"X": adj.dX, "Z": adj.dZ.double() + dZk, "m": adj.dvmean, "s": adj.dvstd,
             "outputscale": adj.ds2.double() + ds2k, "lengthscale": adj.dls.double() + dlsk}
 
 
-def test_variance_clamp_gradient_mask(cuda_device):
+@pytest.mark.parametrize("M,saved", [(32, False), (96, False), (96, True)])
+def test_variance_clamp_gradient_mask(cuda_device, M, saved):
     """Where the variance clamp is active (MVN.variance clamp_min), gvar passes no
-    gradient: driven with a negative K_XX jitter (test hook) so ~half the points clamp."""
-    B, N, M, D = 3, 48, 32, 8
+    gradient: driven with a negative K_XX jitter (test hook) so ~half the points clamp.
+    M = 96 runs the M > 64 adjoints, recompute and saved-state (the forward's clamp mask)."""
+    B, N, D = 3, 48, 8
     g = torch.Generator().manual_seed(77)
     X = torch.randn(B, N, D, generator=g) / np.sqrt(D)
     Z = torch.randn(M, D, generator=g) / np.sqrt(D)
@@ -92,7 +100,7 @@ def test_variance_clamp_gradient_mask(cuda_device):
                                     dtype=np.float64, var_jitter=-0.15)
     frac = float((ref_fwd.var <= 1e-6).mean())
     assert 0.05 < frac < 0.95, frac
-    got = _op_level_grads(cuda_device, X, Z, m, s, w, b0, ls, s2, gmean, gvar, 1e-4, -0.15)
+    got = _op_level_grads(cuda_device, X, Z, m, s, w, b0, ls, s2, gmean, gvar, 1e-4, -0.15, saved=saved)
     ref = O.variational_grads(X.double().numpy(), Z.double().numpy(), ls, s2, w.double().numpy(), b0,
                               m.double().numpy(), s.double().numpy(), gmean.double().numpy(),
                               gvar.double().numpy(), jitter=1e-4, var_jitter=-0.15)
@@ -107,9 +115,11 @@ def test_variance_clamp_gradient_mask(cuda_device):
                                      # count, ragged M / N, D up to the DQ = 64 variant
                                      (3, 70, 100, 7), (2, 50, 96, 20), (2, 33, 180, 30),
                                      (2, 41, 250, 32), (2, 45, 90, 40), (2, 30, 120, 64)])
-def test_variational_grads_reference_shapes(cuda_device, B, N, M, D):
+@pytest.mark.parametrize("saved", [False, True])
+def test_variational_grads_reference_shapes(cuda_device, B, N, M, D, saved):
     """The backward at the reference's GP shapes (M=256 default, DeepGP.py:15; cfg 5's
-    M=64) on a window sample, every gradient block vs the fp64 oracle."""
+    M=64) on a window sample, every gradient block vs the fp64 oracle; ``saved``: the
+    training pair (forward keeps A; M > 64 with D <= 32), else the recompute adjoint."""
     g = torch.Generator().manual_seed(B + N + M)
     X = torch.randn(B, N, D, generator=g) / np.sqrt(D)
     Z = torch.randn(M, D, generator=g) / np.sqrt(D)
@@ -120,13 +130,13 @@ def test_variational_grads_reference_shapes(cuda_device, B, N, M, D):
     s2, b0 = 0.9, 0.3
     gmean = torch.randn(B, N, generator=g)
     gvar = torch.randn(B, N, generator=g)
-    got = _op_level_grads(cuda_device, X, Z, m, s, w, b0, ls, s2, gmean, gvar, 1e-4, 1e-4)
+    got = _op_level_grads(cuda_device, X, Z, m, s, w, b0, ls, s2, gmean, gvar, 1e-4, 1e-4, saved=saved)
     ref = O.variational_grads(X.double().numpy(), Z.double().numpy(), ls, s2, w.double().numpy(), b0,
                               m.double().numpy(), s.double().numpy(), gmean.double().numpy(),
                               gvar.double().numpy(), jitter=1e-4)
     for k, v in got.items():
         e = _rel(v.detach().cpu().numpy(), ref[k])
-        print(f"B={B} N={N} M={M} D={D} {k:12s} {e:.2e}")
+        print(f"B={B} N={N} M={M} D={D} saved={saved} {k:12s} {e:.2e}")
         assert e <= TOL, (k, e)
 
 
