@@ -1743,6 +1743,19 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
                  vsm + G::kVm, vsm + G::kSm1, vsm + G::kKl);
   for (int e = tid; e < G::MP; e += NT) vsm[G::kQ + e] = 0.f;
   for (int e = tid; e < 2 * G::MP; e += NT) vsm[oRows + e] = 0.f;
+  // A blocks are copied global -> LDS by LDS-DMA (global_load_lds, no registers), double-buffered
+  // over the adjk geometry's dA and K_ZX tile areas (K_ZX lives in registers here): the copy for
+  // chunk t + grid is issued before chunk t's GEMM and retired at chunk t + grid's first barrier
+  auto copy_a = [&](int t, float* buf) {
+    const float* sb = saved + (size_t)t * SV::blk;
+#pragma unroll
+    for (int q = 0; q < NU / NT; ++q) {
+      const int u0 = (q * NWV + wave) * 64;   // this wave-instruction's 64 units (1 KiB)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(sb + 4 * (u0 + lane)),
+                                       (__attribute__((address_space(3))) void*)(buf + 4 * u0), 16, 0, 0);
+    }
+  };
+  copy_a(blockIdx.x, vsm + G::kdA);
   lds_barrier();
   float cmr[DV];
 #pragma unroll
@@ -1763,7 +1776,7 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     const int nvalid = N - i0 < LTW ? N - i0 : LTW;
     const long long col0 = (long long)b * N + i0;
     float* sm = (float*)fresh_lds(vsm);
-    float* dAl = sm + G::kdA;
+    float* dAl = sm + (par ? G::kKl : G::kdA);
     float* xzl = sm + G::kXz;
     float* red = sm + G::kRed;
     const float* zs = sm + G::kZs;
@@ -1777,14 +1790,9 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     float* gmc = sm + G::kGm + par * LTW;
     float* gvc = sm + oGv + par * LTW;
     float* rows = sm + oRows;
-    // ---- the chunk's A tiles (one contiguous block) -> the LDS dA tiles; points; gmean / gvar
+    // ---- the chunk's A tiles are (being) copied into dAl; points; gmean / gvar
     {
       const float* sb = saved + (size_t)t * SV::blk;
-#pragma unroll
-      for (int q = 0; q < NU / NT; ++q) {
-        const int e = tid + q * NT;
-        *(f32x4*)(dAl + 4 * e) = *(const f32x4*)(sb + 4 * e);
-      }
       if (tid < LTW) {
         const bool ok = tid < nvalid;
         const float keep = sb[SV::tiles + tid];
@@ -1798,6 +1806,7 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     }
     lstage_points<NPASS, DV, NT, DS>(xr, lsr, cmr, D, nvalid, xs, xn);
     if (t + (int)gridDim.x < nchunks) lload_points<NPASS, DV, NT>(X, t + gridDim.x, nchunks, nch, N, D, xr);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's A copy has landed
     lds_barrier();
     // ---- the wave's own rows: row sums of A, A -> dA in place
     {
@@ -1842,6 +1851,9 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     f32x4 Qt[2][2];
     {
       f64x4 dK[2][2];
+      // the next chunk's A into the other buffer (its last reader, the previous chunk's GEMM,
+      // is behind this chunk's barriers); it lands while this chunk's GEMM runs
+      if (t + (int)gridDim.x < nchunks) copy_a(t + gridDim.x, sm + (par ? G::kdA : G::kKl));
       lcol_gemm_for<MB, 0>(wave, Lc, dAl, lane, dK[0], dK[1]);
       // K_ZX of the wave's rows (f32 MFMA, zs rows fed in pi order: reg r <-> row g + 4r, the
       // f64 C layout of dK), Q = dK o K
@@ -2071,6 +2083,14 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 #pragma unroll
   for (int s = 0; s <= MB; ++s) gacc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 uacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  // the chunk's A units (4 rows of one point each): loaded one chunk ahead (registers)
+  f32x4 au[NU / NT];
+  auto load_a = [&](int t) {
+    const float* sb = saved + (size_t)(t < nchunks ? t : 0) * SV::blk;
+#pragma unroll
+    for (int q = 0; q < NU / NT; ++q) au[q] = *(const f32x4*)(sb + 4 * (tid + q * NT));
+  };
+  load_a(blockIdx.x);
 
   for (int t = blockIdx.x; t < nchunks; t += gridDim.x) {
     const int b = t / nch, i0 = (t - b * nch) * LTW;
@@ -2086,10 +2106,6 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     float* gmc = sm + G::oGm;
     float* gvc = sm + G::oGv;
     const float* sb = saved + (size_t)t * SV::blk;
-    // the chunk's A units (4 rows of one point each) in flight before the barrier
-    f32x4 au[NU / NT];
-#pragma unroll
-    for (int q = 0; q < NU / NT; ++q) au[q] = *(const f32x4*)(sb + 4 * (tid + q * NT));
     lds_barrier();   // the previous chunk's reads are done
 #pragma unroll
     for (int q = 0; q < NU / NT; ++q) {
@@ -2107,7 +2123,10 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       gmc[tid] = ok ? gm : 0.f;
       gvc[tid] = (ok && keep != 0.f) ? gv : 0.f;   // the variance clamp passes no gradient
     }
-    if (t + (int)gridDim.x < nchunks) lload_points<NPASS, DV, NT>(X, t + gridDim.x, nchunks, nch, N, D, xr);
+    if (t + (int)gridDim.x < nchunks) {
+      lload_points<NPASS, DV, NT>(X, t + gridDim.x, nchunks, nch, N, D, xr);
+      load_a(t + gridDim.x);   // (au was consumed by the LDS stores above)
+    }
     lds_barrier();
     // K_ZX of the wave's rows -> Kr[row][point]; u partials
 #pragma unroll
