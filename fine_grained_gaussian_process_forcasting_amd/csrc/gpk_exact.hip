@@ -35,32 +35,7 @@
 #include "gpk_common.h"
 #include "gpk_internal.h"
 
-#ifndef GPK_EXACT_WBIG
-#define GPK_EXACT_WBIG 8
-#endif
-#ifndef GPK_EXACT_DEV
-#define GPK_EXACT_DEV 0
-#endif
-#ifndef GPK_SPLIT_UPDATE
-#define GPK_SPLIT_UPDATE 1
-#endif
-#ifndef GPK_EXACT_SMALLB
-#define GPK_EXACT_SMALLB 1   // B <= CUs: one window per CU with 16 waves (launch_exact_nb)
-#endif
-#ifndef GPK_EXACT_PRIO_RHS
-#define GPK_EXACT_PRIO_RHS 1   // raise the worker priority already at the right-hand side (0: at the TRSM)
-#endif
-#ifndef GPK_EXACT_PRIO
-#define GPK_EXACT_PRIO 1   // workers raise their issue priority to this for the hand-over and the TRSM
-                           // (0: off; 1 measured 2.5 % faster per launch, scripts/gpu_ab_prio.sh)
-#endif
-#ifndef GPK_KO
-#define GPK_KO 0   // development knockouts (timing only, results wrong): 1 TRSM MFMA, 2 RHS, 4 zero-L,
-                   // 8 deferred RBF, 16 bulk trailing update, 32 TRSM L stores, 64 diagonal sweep
-#endif
-#ifndef GPK_DIAG_DPP
-#define GPK_DIAG_DPP 1   // diagonal sweep as DPP-broadcast FMAs (gpk_diag_dpp.inc); 0 = readlane form
-#endif
+#include "gpk_exact_dev.h"
 
 namespace {
 
@@ -181,16 +156,6 @@ GPK_DEVICE void barrier_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-#ifndef GPK_TMO_DEBUG
-#define GPK_TMO_DEBUG 0   // 1 (debug builds): a timed-out window's info = flag index | target << 8
-#endif
-#ifndef GPK_EXACT_COL
-#define GPK_EXACT_COL 1   // 1: column-ownership worker plan for N = 256 at 8 waves (worker_step_col)
-#endif
-#ifndef GPK_LST_AUX
-#define GPK_LST_AUX 17   // L stores: -1 plain global stores; >= 0 buffer stores with this cache-policy aux
-                         // (17 = sc0 sc1: write-through, the lines leave L2 -- 64.5 -> 59.2 us per B=512 launch)
-#endif
 // One 16-byte store into a window's L (base = the window's L, wave-uniform).
 GPK_DEVICE void lstore(float* base, int off, const f32x4 v) {
   if constexpr (GPK_LST_AUX < 0) {
@@ -349,7 +314,6 @@ enum : int {
 // carries on, so a logic error can never leave waves spinning on the GPU
 // (the window then reports info = kInfoTimeout).
 constexpr int kInfoTimeout = 1 << 20;
-constexpr int kStampStride = 32 + 16 * 8 * 8;  // phase clocks + per-step timeline (STAMPS)
 GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
   int n = 0;
   while (flags[idx] < target) {
@@ -510,7 +474,7 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
     __builtin_amdgcn_sched_barrier(0);
   }
 #if GPK_DIAG_DPP
-  if (!(GPK_KO & 64)) diag_sweep_dpp(v);
+  if (!kKoDiagSweep) diag_sweep_dpp(v);
 #else
   diag_sweep<0>(v);
 #endif
@@ -531,7 +495,7 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
 #pragma unroll
   for (int i = 1; i < 16; ++i) dg = (c == i) ? v[i] : dg;
   const bool okd = (dg > 0.f) && (dg < __builtin_huge_valf());
-  const unsigned long long badm = (GPK_KO != 0) ? 0ull : __ballot(lane < 16 && !okd);
+  const unsigned long long badm = kKoAny ? 0ull : __ballot(lane < 16 && !okd);
   // provisional (the exact column follows): 16 k + 1 -- the failing STEP is readable from
   // either value as (word - 1) >> 4, so a worker that is still at an earlier step does not
   // leave the attempt before the others (they all leave at step k)
@@ -687,17 +651,6 @@ struct WorkerCtx {
   unsigned long long* tl;  // STAMPS builds only: per-step timeline [(k * 8 + wave) * 8 + event]
 };
 
-// Diagnostic phase clock inside the worker steps (STAMPS builds only).
-#define GPK_WSTAMP(slot, ev)                                      \
-  if constexpr (ST) {                                             \
-    __builtin_amdgcn_sched_barrier(0);                            \
-    const unsigned long long _n = __builtin_amdgcn_s_memtime();   \
-    x.st[slot] += _n - x.st[8];                                   \
-    x.st[8] = _n;                                                 \
-    if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8 + (ev)] = _n;        \
-    __builtin_amdgcn_sched_barrier(0);                            \
-  }
-
 // Barrier among the WK worker waves only (the diagonal wave runs ahead of them
 // and never joins): monotone LDS counter, one ds_add per wave.
 // Split into arrive (publish this wave's LDS writes, count in) and wait, so
@@ -787,7 +740,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     auto upd = [&](f32x4& d, auto I) {
       constexpr int s = decltype(I)::value;
       const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(wv + WK * s);
-      if constexpr (GPK_KO & 128) {   // knockout: one LDS operand per tile update
+      if constexpr (kKoOneOperand) {   // knockout: one LDS operand per tile update
         const pan_op_t q = pan_load(pprev + (p & 255) * 256, lane);
         d = pan_mma_op(q, q, d);
       } else {
@@ -802,7 +755,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if constexpr (s == TD / WK) sk = sk || (wv == TD % WK);
       if constexpr (!LAST && s == TA / WK) sk = sk || (wv == TA % WK);
       if constexpr (!LAST && s == TB / WK) sk = sk || (wv == TB % WK);
-      if (!sk && !(GPK_KO & 16)) upd(acc[s], I);
+      if (!sk && !kKoBulkUpdate) upd(acc[s], I);
     };
     if constexpr (NALL < SLOTS && (Pkm1 % WK) != 0) {
       if (wv < Pkm1 % WK) bulk(IC<NALL>{});
@@ -814,12 +767,12 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // zero-L + right-hand side lead into the TRSM
 #endif
   // zero L's strictly-upper part of block row K (streams out behind the MFMAs)
-  if (!(GPK_KO & 4) && x.Lb != nullptr) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, K, wv, WK, lane);
+  if (!kKoZeroL && x.Lb != nullptr) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, K, wv, WK, lane);
   // right-hand side, block rows i >= K owned by this wave: rw_i += R_{K-1,i}^T z_{K-1}
   // (rw holds -(y - c); only column 0 of the tile is live, so it round-trips
   // through LDS on the c == 0 lanes)
   const int rfirst = K + (((wv - K) % WK) + WK) % WK;
-  if constexpr (K > 0 && !(GPK_KO & 2)) {
+  if constexpr (K > 0 && !kKoRhs) {
     for (int i = rfirst; i < NB; i += WK) {
       f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -847,7 +800,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     q = load_w_v(wbk, c, grp);
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
-  if (GPK_KO == 0 && fail != 0 && ((fail - 1) >> 4) <= K) {   // the attempt failed at step <= K
+  if (!kKoAny && fail != 0 && ((fail - 1) >> 4) <= K) {   // the attempt failed at step <= K
     __builtin_amdgcn_s_setprio(0);   // the jitter-ladder retry starts at the base priority
     return 1;
   }
@@ -863,9 +816,9 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
         const int t = wv + WK * s;
         if (t >= TLO && t <= THI) {
           const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
-          const f32x4 rkj = pan_store(pcur + j * 256, lane, (GPK_KO & 1) ? acc[s] : trsm_tile(wq, acc[s]));
+          const f32x4 rkj = pan_store(pcur + j * 256, lane, kKoTrsmMfma ? acc[s] : trsm_tile(wq, acc[s]));
           // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
-          if (!(GPK_KO & 32) && x.Lb != nullptr)
+          if (!kKoTrsmLStores && x.Lb != nullptr)
             store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
         }
       });
@@ -892,7 +845,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   worker_arrive(x);
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
   // deferred RBF of block row K+2 (its diagonal tile is handed over at step K+1)
-  if constexpr (K + 2 < NB && !(GPK_KO & 8)) {
+  if constexpr (K + 2 < NB && !kKoDeferredRbf) {
     constexpr int RLO = plan_P<NB>(K + 2), RHI = plan_P<NB>(K + 1) - 1;
     constexpr int SLO = RLO / WK;
     constexpr int SHI = (RHI / WK) < SLOTS - 1 ? (RHI / WK) : SLOTS - 1;
@@ -1059,7 +1012,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     q = load_w_v(wbk, c, grp);
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
-  if (GPK_KO == 0 && fail != 0 && ((fail - 1) >> 4) <= K) return 1;
+  if (!kKoAny && fail != 0 && ((fail - 1) >> 4) <= K) return 1;
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);
   // panel buffer K & 1 held panel K-2 (read in step K-1): every wave must be past step K-1's
   // panel reads (one kFlagBulk add per wave per step)
@@ -1220,14 +1173,6 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
   constexpr int T = 64 * W;
   // Diagnostic-only phase clocks (STAMPS build): wave 0 lane 0 of each workgroup.
   unsigned long long st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0, st_t0 = 0, st_rt0 = 0;
-#define GPK_STAMP(slot)                                         \
-  if constexpr (STAMPS) {                                       \
-    __builtin_amdgcn_sched_barrier(0);                          \
-    const unsigned long long _n = __builtin_amdgcn_s_memtime(); \
-    st_acc[slot] += _n - st_last;                               \
-    st_last = _n;                                               \
-    __builtin_amdgcn_sched_barrier(0);                          \
-  }
   if constexpr (STAMPS) {
     st_rt0 = __builtin_amdgcn_s_memrealtime();
     st_t0 = __builtin_amdgcn_s_memtime();

@@ -65,8 +65,17 @@ GPK_DEVICE double readlane_d(double v, int lane) {
 #ifndef GPK_KZZ_STAMPS
 #define GPK_KZZ_STAMPS 0   // debug: per-step phase clocks into info[1..] (results still valid)
 #endif
+#ifndef GPK_KZZ_ISOLATE
+#define GPK_KZZ_ISOLATE 0  // 1: the diagonal wave's SIMD (waves w & 3 == 3) holds no worker tiles
+#endif
 constexpr int KW = GPK_KZZ_WAVES;
 constexpr int KT = 64 * KW;
+// tile-holding workers and the worker rank of a wave (-1: no tiles)
+constexpr int kKzzWorkers = GPK_KZZ_ISOLATE ? (KW - 1) - (KW - 1) / 4 : KW - 1;
+GPK_DEVICE int kzz_worker_rank(int wave) {
+  if (GPK_KZZ_ISOLATE) return (wave & 3) == 3 ? -1 : wave - (wave >> 2);
+  return wave;
+}
 __host__ __device__ inline int kzz_zstride(int D) { return ((D + 15) & ~15) + 4; }
 constexpr int kLinvStride = 17;   // L_kk^{-1} rows in LDS (odd: conflict-free column reads)
 
@@ -383,11 +392,12 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
     int its[NS], jts[NS];
     {
       const int ntile = T * (T + 1) / 2;
+      const int wr = kzz_worker_rank(wave);
 #pragma unroll
       for (int q = 0; q < NS; ++q) {
-        const int t = wave + NWK * q;
+        const int t = wr + kKzzWorkers * q;
         int it = T, jt = T;   // no tile: coordinates past the end (skipped everywhere)
-        if (t < ntile) tile_of(t, T, it, jt);
+        if (wr >= 0 && t < ntile) tile_of(t, T, it, jt);
         its[q] = __builtin_amdgcn_readfirstlane(it);
         jts[q] = __builtin_amdgcn_readfirstlane(jt);
       }
@@ -498,6 +508,9 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
 // is the B operand of k-step kk straight from register kk. S tiles dealt over 16 waves
 // (u = wave mod 16: one tile per wave up to M = 256, so a step costs one 4-MFMA chain per
 // wave, not four); the L tiles of the next step are prefetched from L2 during this one.
+#ifndef GPK_KZZ_INV_DEPTH2
+#define GPK_KZZ_INV_DEPTH2 0
+#endif
 constexpr int KIT = 1024, KIW = KIT / 64, KIS = 2;   // KIS slots: up to 32 block rows
 __global__ void __launch_bounds__(KIT)
 gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ info,
@@ -511,6 +524,11 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (info[0] > 0) return;           // no factor (the op raises NotPSDError)
+#if GPK_KZZ_STAMPS
+  // block column 0's clock: start, after the prologue, after each step's barrier
+  int* ist = (jb == 0 && tid == 0) ? const_cast<int*>(info) + 1 + 6 * T16 : nullptr;
+  if (ist) ist[0] = (int)__builtin_amdgcn_s_memtime();
+#endif
   auto Lat = [&](int i, int j) -> double {   // L with identity padding beyond M
     if (i < M && j < M) return L[(size_t)i * M + j];
     return i == j ? 1.0 : 0.0;
@@ -533,6 +551,9 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
     if (i < M && j < M) Linv[(size_t)i * M + j] = Tv[e];
   }
   lds_barrier();
+#if GPK_KZZ_STAMPS
+  if (ist) ist[1] = (int)__builtin_amdgcn_s_memtime();
+#endif
   f64x4 S[KIS];
 #pragma unroll
   for (int t = 0; t < KIS; ++t) S[t] = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -548,13 +569,25 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
     }
   };
   load_a(0, an);
+#if GPK_KZZ_INV_DEPTH2
+  double ann[KIS][4];   // step k + 2's operands, two HBM latencies ahead
+  if (nb > 2) load_a(1, ann);
+#endif
   for (int k = 0; k + 1 < nb; ++k) {
     double a[KIS][4];
 #pragma unroll
     for (int t = 0; t < KIS; ++t)
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) a[t][kk] = an[t][kk];
+#if GPK_KZZ_INV_DEPTH2
+#pragma unroll
+    for (int t = 0; t < KIS; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) an[t][kk] = ann[t][kk];
+    if (k + 3 < nb) load_a(k + 2, ann);
+#else
     if (k + 2 < nb) load_a(k + 1, an);
+#endif
     double xb[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) xb[kk] = Xs[k * 256 + (g + 4 * kk) * 16 + c];
@@ -583,6 +616,9 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
       }
     }
     lds_barrier();
+#if GPK_KZZ_STAMPS
+    if (ist) ist[2 + k] = (int)__builtin_amdgcn_s_memtime();
+#endif
   }
 }
 
@@ -617,11 +653,12 @@ int launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
 
 int gpk_launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
   const int T = (a.M + 15) >> 4;
-  const int ns = (T * (T + 1) / 2 + KW - 2) / (KW - 1);   // tiles per worker (round-robin)
+  const int ns = (T * (T + 1) / 2 + kKzzWorkers - 1) / kKzzWorkers;   // tiles per worker (round-robin)
   if (ns <= 2) return launch_kzz16<2>(a, stream);
   if (ns <= 4) return launch_kzz16<4>(a, stream);
   if (ns <= 7) return launch_kzz16<7>(a, stream);
   if (ns <= 10) return launch_kzz16<10>(a, stream);
+  if (ns <= 12) return launch_kzz16<12>(a, stream);
   if (ns <= 17) return launch_kzz16<17>(a, stream);
   if (ns <= 21) return launch_kzz16<21>(a, stream);
   return -3;

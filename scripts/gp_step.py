@@ -165,7 +165,8 @@ def run(cfg, steps, modes=("eager", "graph", "eager_anomaly"), gps=(True, False)
 if __name__ == "__main__":
     cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg3"
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    if len(sys.argv) > 3 and sys.argv[3] in ("graph-gp", "graph-nogp"):   # profiling: one graphed step kind
-        print(json.dumps(run(cfg, steps, modes=("graph",), gps=(sys.argv[3] == "graph-gp",))), flush=True)
+    if len(sys.argv) > 3 and sys.argv[3] in ("graph-gp", "graph-nogp", "eager-gp", "eager-nogp"):
+        mode, gp = sys.argv[3].split("-")                 # profiling / A/B: one step kind
+        print(json.dumps(run(cfg, steps, modes=(mode,), gps=(gp == "gp",))), flush=True)
     else:
         print(json.dumps(run(cfg, steps)), flush=True)

@@ -21,7 +21,7 @@ h = torch.cat([torch.tensor([LN2]), torch.full((D,), LN2)]).to(dev)
 T = (M + 15) // 16
 L = torch.empty(M, M, dtype=torch.float64, device=dev)
 Li = torch.empty(M, M, dtype=torch.float64, device=dev)
-info = torch.zeros(8 + 6 * T, dtype=torch.int32, device=dev)
+info = torch.zeros(8 + 8 * T, dtype=torch.int32, device=dev)
 lib = _native.lib()
 for _ in range(3):
     rc = lib.gpk_kzz_chol_f64(Z.data_ptr(), h.data_ptr(), M, D, 1e-4, 1e-8, 3, L.data_ptr(), Li.data_ptr(),
@@ -50,3 +50,6 @@ for k in range(1, T):
     sw = (ds[k][2] - ds[k][1]) & 0xffffffff
     ho = (ds[k][0] - st[k - 1][2]) & 0xffffffff
     print(f"k={k:2d} load {ld:6d} sweep {sw:6d}  handover-after-trsm {ho:6d}")
+iv = v[1 + 6 * T: 1 + 6 * T + T + 1]
+print("inverse kernel, block column 0 (ticks): prologue", (iv[1] - iv[0]) & 0xffffffff, " steps",
+      [(iv[2 + k] - iv[1 + k]) & 0xffffffff for k in range(T - 1)], " total", (iv[T] - iv[0]) & 0xffffffff)

@@ -192,3 +192,4 @@ def test_graphed_step_learning_rate_rules(cuda_device):
     lr.fill_(1e-2)
     step(X, y)
     assert (model.raw.detach() - before).abs().max() > 1e-4                  # the new lr is used
+
