@@ -14,9 +14,10 @@
 // R = L^T in 16-column steps:
 //   diag   the diagonal wave factors T'_kk in ONE sweep of the augmented [T_kk | I] (lanes
 //          0-15: columns of T_kk -> rows of L_kk, lanes 16-31: identity columns -> columns of
-//          L_kk^{-1}), broadcasts by 64-bit DPP (diag_col64) -- LOOK-AHEAD: the owner of
-//          (k+1, k+1) updates and hands it over (LDS + flag) first in step k's update, so the
-//          sweep overlaps the workers' trailing update;
+//          L_kk^{-1}), broadcasts by 64-bit DPP (diag_col64) -- LOOK-AHEAD: the owners of
+//          (k+1, k+1) and (k, k+1) update and hand them over first in step k-1's update; the
+//          diagonal wave forms R_{k,k+1} and T''_{k+1,k+1} itself beside step k's TRSM, so
+//          the sweep of (k+1, k+1) overlaps the workers' trailing update of step k;
 //   TRSM   owners of block row k: R_kj = L_kk^{-1} T'_kj (4 f64 MFMAs, the register tile is
 //          the B operand) -> LDS panel + L's block (j, k);
 //   update every tile (i, j), k < i <= j: T'_ij -= R_ki^T R_kj (4 f64 MFMAs, both operands
@@ -65,29 +66,47 @@ GPK_DEVICE double readlane_d(double v, int lane) {
 #ifndef GPK_KZZ_STAMPS
 #define GPK_KZZ_STAMPS 0   // debug: per-step phase clocks into info[1..] (results still valid)
 #endif
-#ifndef GPK_KZZ_ISOLATE
-#define GPK_KZZ_ISOLATE 0  // 1: the diagonal wave's SIMD (waves w & 3 == 3) holds no worker tiles
-#endif
 constexpr int KW = GPK_KZZ_WAVES;
 constexpr int KT = 64 * KW;
-// tile-holding workers and the worker rank of a wave (-1: no tiles)
-constexpr int kKzzWorkers = GPK_KZZ_ISOLATE ? (KW - 1) - (KW - 1) / 4 : KW - 1;
-GPK_DEVICE int kzz_worker_rank(int wave) {
-  if (GPK_KZZ_ISOLATE) return (wave & 3) == 3 ? -1 : wave - (wave >> 2);
-  return wave;
-}
+// (Measured and dropped, scripts/r05/gpu_kzz_ab.sh: keeping the diagonal wave's SIMD free of
+// worker tiles: the sweep then runs at its 4.7 K-cycle floor instead of 8-11 K in the early
+// steps, but 3 SIMDs make those steps update-bound (121 -> 123 us per factor + inverse), and
+// with 12 tiles per worker the kernel spills (118 -> 191 us); prefetching the inverse's L
+// operands two steps ahead: no change.)
+constexpr int kKzzWorkers = KW - 1;
 __host__ __device__ inline int kzz_zstride(int D) { return ((D + 15) & ~15) + 4; }
 constexpr int kLinvStride = 17;   // L_kk^{-1} rows in LDS (odd: conflict-free column reads)
 
+#ifndef GPK_KZZ_FUSED_DPP
+#define GPK_KZZ_FUSED_DPP 1   // 1: the sweep's broadcast FMAs as single v_fmac_f64_dpp (inline asm)
+#endif
 #ifndef GPK_KZZ_DPP
 #define GPK_KZZ_DPP 1   // 1: the diagonal sweep broadcasts by 64-bit DPP (row_newbcast); 0: readlanes
 #endif
 
-// x of lane 16 r' + i for every lane of row r' (64-bit row_newbcast:i)
+// x of lane 16 r' + i for every lane of row r' (64-bit row_newbcast:i; bound_ctrl: every lane
+// has a source, and the destination needs no zero-initialisation)
 template <int I>
 GPK_DEVICE double nbc(double x) {
-  return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + I, 0xf, 0xf, false);
+  return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + I, 0xf, 0xf, true);
 }
+// acc += (nr of lane i of the row) * vq as ONE v_fmac_f64_dpp (the compiler emits a separate
+// v_mov_b64_dpp + v_fmac_f64). NOP: the 2 wait states a DPP read of nr needs after the VALU
+// write of nr (the hazard recognizer does not look inside asm); the first use per column.
+#define GPK_FMAC_BC(I)                                                                       \
+  template <bool NOP>                                                                        \
+  GPK_DEVICE void fmac_bc##I(double& acc, double nr, double vq) {                            \
+    if constexpr (NOP)                                                                       \
+      asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:" #I                    \
+                   " row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(nr), "v"(vq));            \
+    else                                                                                     \
+      asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #I " row_mask:0xf bank_mask:0xf" \
+                   : "+v"(acc) : "v"(nr), "v"(vq));                                         \
+  }
+GPK_FMAC_BC(1) GPK_FMAC_BC(2) GPK_FMAC_BC(3) GPK_FMAC_BC(4) GPK_FMAC_BC(5)
+GPK_FMAC_BC(6) GPK_FMAC_BC(7) GPK_FMAC_BC(8) GPK_FMAC_BC(9) GPK_FMAC_BC(10)
+GPK_FMAC_BC(11) GPK_FMAC_BC(12) GPK_FMAC_BC(13) GPK_FMAC_BC(14) GPK_FMAC_BC(15)
+#undef GPK_FMAC_BC
 // row 0's value in rows 0 and 1 (and row 2's in rows 2 and 3): permlane16_swap per half
 GPK_DEVICE double row_even_both(double x) {
   const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
@@ -111,6 +130,18 @@ GPK_DEVICE void diag_col64(double (&v)[16]) {
   if constexpr (Q < 15) {
 #pragma unroll
     for (int i = Q + 1; i < 16; ++i) {
+#if GPK_KZZ_FUSED_DPP
+      const bool first = i == Q + 1;
+      switch (i) {   // (compile-time after unrolling)
+#define GPK_FMAC_CASE(I) \
+        case I: if (first) fmac_bc##I<true>(v[i], nr, v[Q]); else fmac_bc##I<false>(v[i], nr, v[Q]); break;
+        GPK_FMAC_CASE(1) GPK_FMAC_CASE(2) GPK_FMAC_CASE(3) GPK_FMAC_CASE(4) GPK_FMAC_CASE(5)
+        GPK_FMAC_CASE(6) GPK_FMAC_CASE(7) GPK_FMAC_CASE(8) GPK_FMAC_CASE(9) GPK_FMAC_CASE(10)
+        GPK_FMAC_CASE(11) GPK_FMAC_CASE(12) GPK_FMAC_CASE(13) GPK_FMAC_CASE(14)
+        default: if (first) fmac_bc15<true>(v[i], nr, v[Q]); else fmac_bc15<false>(v[i], nr, v[Q]); break;
+#undef GPK_FMAC_CASE
+      }
+#else
       double b;
       switch (i) {   // (compile-time after unrolling)
         case 1: b = nbc<1>(nr); break;   case 2: b = nbc<2>(nr); break;
@@ -123,29 +154,55 @@ GPK_DEVICE void diag_col64(double (&v)[16]) {
         default: b = nbc<15>(nr); break;
       }
       v[i] = __builtin_fma(b, v[Q], v[i]);
+#endif
     }
     diag_col64<Q + 1>(v);
   }
+}
+
+// x of the odd row (1 -> 0, 3 -> 2) in the even rows' lanes (permlane16_swap, new src0)
+GPK_DEVICE double from_odd_row(double x) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const unsigned nl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false)[1];
+  const unsigned nh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false)[1];
+  return __builtin_bit_cast(double, ((unsigned long long)nh << 32) | nl);
+}
+// x of rows 2, 3 in rows 0, 1 (permlane32_swap, new src0)
+GPK_DEVICE double from_upper_half(double x) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const unsigned nl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false)[1];
+  const unsigned nh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false)[1];
+  return __builtin_bit_cast(double, ((unsigned long long)nh << 32) | nl);
+}
+// The sweep's operand from an acc-layout tile in registers: lanes 0-15 get column c
+// (v[g' + 4r] = reg r of lane c + 16 g'), lanes 16-31 the identity column c - 16.
+GPK_DEVICE void acc_to_sweep(const f64x4 t, double (&v)[16]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const double up = from_upper_half(t[r]);
+    v[4 * r] = t[r];
+    v[4 * r + 1] = from_odd_row(t[r]);
+    v[4 * r + 2] = up;
+    v[4 * r + 3] = from_odd_row(up);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = lane < 16 ? v[i] : ((lane - 16 == i) ? 1.0 : 0.0);
 }
 
 // The diagonal wave factors the (updated, handed-over) diagonal tile t = T'_kk:
 // one broadcast sweep (diag_col64) of the augmented [T_kk | I] (lanes 0-15: columns of T_kk
 // -> rows of L_kk, lanes 16-31: identity columns -> columns of L_kk^{-1}). Results: lkk
 // (16 x 17, row-major L_kk), linv (16 x 17, L_kk^{-1}) in LDS; status = failed column + 1.
-GPK_DEVICE void factor_diag(int k, const double* dbuf, double* lkk, double* linv, int* status,
-                            int* stamp) {
+GPK_DEVICE void sweep_diag(int k, double (&v)[16], double* lkk, double* linv, int* status, int* stamp) {
   const int lane = threadIdx.x & 63, c = lane & 15;
-  double v[16];
   const bool left = lane < 16;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const double x = dbuf[i * 16 + c];   // unconditional read, then select
-    v[i] = left ? x : ((lane - 16 == i) ? 1.0 : 0.0);
-  }
   int bad = 0;
 #if GPK_KZZ_STAMPS
   if (stamp != nullptr) {
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the tile is in registers
+    asm volatile("" ::"v"(v[15]));   // the operand is in registers
     if (lane == 0) stamp[1] = (int)__builtin_amdgcn_s_memtime();
   }
 #endif
@@ -188,10 +245,34 @@ GPK_DEVICE void factor_diag(int k, const double* dbuf, double* lkk, double* linv
 #endif
 }
 
+// Tile (0, 0), handed over raw in acc layout through LDS (dbuf).
+GPK_DEVICE void factor_diag0(const double* dbuf, double* lkk, double* linv, int* status, int* stamp) {
+  const int lane = threadIdx.x & 63;
+  f64x4 t;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t[r] = dbuf[r * 64 + lane];
+  double v[16];
+  acc_to_sweep(t, v);
+  sweep_diag(0, v, lkk, linv, status, stamp);
+}
+
 // LDS flag words of the factor kernel (volatile, LDS address space: ds_read / ds_write only)
-// kKfTile + (t & 1): epoch of the last diagonal tile t handed over into dbuf[t & 1]
-enum KzzFlag { kKfTile = 0, kKfTmo = 1, kKfStatus = 2, kKfTile1 = 3 };
+// kKfTile: epoch of the raw (0, 0) hand-over of the tile formation (every later hand-over is
+// ordered by the step barriers)
+// kKfSync: the workers' step barrier [B] (monotone count: one add per worker wave per step)
+enum KzzFlag { kKfTile = 0, kKfTmo = 1, kKfStatus = 2, kKfSync = 3, kKfWords = 8 };
 constexpr int kKzzTimeout = 1 << 20;   // info code of an expired spin-wait (never NotPSD)
+
+GPK_DEVICE void kzz_spin_ge(lds_vint* f, int word, int target) {
+  int n = 0;
+  while (f[word] < target) {
+    if (++n > (1 << 20)) {
+      f[kKfTmo] = 1;
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 GPK_DEVICE void kzz_spin_until(lds_vint* f, int word, int target) {
   int n = 0;
@@ -254,12 +335,15 @@ GPK_DEVICE double ladder_of(int attempt, double jitter_chol) {   // GPyTorch: cu
 
 // Waves 0 .. KW-2 are WORKERS holding the upper triangle's tiles (dealt round-robin in
 // column-major order); wave KW-1 is the DIAGONAL wave and holds no tile. Per step k:
-//   [A] barrier: L_kk, L_kk^{-1} (LDS) and the step's status are out;
-//   [B] workers: TRSM of block row k -> LDS panel + L; diagonal wave: the diagonal blocks of
-//       L and L^{-1} to HBM; barrier;
-//   [C] the owner of column k+1 updates T'_{k+1,k+1} FIRST and hands it over (LDS + flag),
-//       then its other tiles; the diagonal wave factors it meanwhile (look-ahead), so the
-//       sequential 16-column sweeps overlap the trailing updates.
+//   [A] workgroup barrier: L_kk, L_kk^{-1} (LDS, parity k & 1) and the step's status are out;
+//   [B] workers: TRSM of block row k -> LDS panel + L, then a WORKER-ONLY barrier (LDS
+//       counter, kKfSync); the diagonal wave does not join it: it forms R_{k,k+1} =
+//       L_kk^{-1} T'_{k,k+1} and T''_{k+1,k+1} = T'_{k+1,k+1} - R^T R from the two hand-over
+//       tiles itself (the same MFMAs as the owners'), writes the diagonal blocks of L and
+//       L^{-1} to HBM and starts the sweep of (k+1, k+1) at once;
+//   [C] the owners of (k+2, k+2) and (k+1, k+2) update them FIRST and hand them over (LDS,
+//       read by the diagonal wave after the next [A]), then their other tiles, while the
+//       diagonal wave sweeps: the 16-column sweeps are the only sequential chain.
 // The diagonal wave's registers are disjoint from the workers' (separate loops), so the
 // tiles (NS per worker) and the sweep do not compete for the 256-VGPR budget.
 template <int NS>
@@ -270,12 +354,13 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
   extern __shared__ __attribute__((aligned(16))) double dsm[];
   const int T = (M + 15) >> 4;
   double* panel = dsm;                 // (T - 1) tiles x 256, [slot][reg][lane]
-  double* dbuf = panel + (size_t)(T > 1 ? T - 1 : 1) * 256;   // 2 x 256: hand-over tiles (parity)
-  double* linv = dbuf + 512;           // 16 x 17: L_kk^{-1}
-  double* lkk = linv + 16 * kLinvStride;                      // 16 x 17: L_kk
-  int* flagw = (int*)(lkk + 16 * kLinvStride);                // KzzFlag words
+  double* dbuf = panel + (size_t)(T > 1 ? T - 1 : 1) * 256;   // 2 x 256: hand-over tiles (t, t)
+  double* obuf = dbuf + 512;           // 2 x 256: hand-over tiles (t - 1, t), parity t & 1
+  double* linvb = obuf + 512;          // 2 x 16 x 17: L_kk^{-1}, parity k & 1
+  double* lkkb = linvb + 2 * 16 * kLinvStride;                // 2 x 16 x 17: L_kk, parity k & 1
+  int* flagw = (int*)(lkkb + 2 * 16 * kLinvStride);           // KzzFlag words
   lds_vint* fl = as_lds_flags(flagw);
-  float* zt = (float*)(flagw + 4);     // M x ZS  Z / l, centred (zero padded)
+  float* zt = (float*)(flagw + kKfWords);   // M x ZS  Z / l, centred (zero padded)
   const int ZS = kzz_zstride(D);
   const int D16 = (D + 15) & ~15;
   float* zn = zt + M * ZS;             // M
@@ -300,7 +385,7 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
       if (e < M * ZS) zt[e] = d < D ? v[u] / l[u] : 0.f;
     }
   }
-  if (tid < 4) flagw[tid] = (tid == kKfTile || tid == kKfTile1) ? -1 : 0;
+  if (tid < kKfWords) flagw[tid] = tid == kKfTile ? -1 : 0;
   lds_barrier();
   for (int d = wave; d < D; d += KT / 64) {   // column means: one wave per column
     float sm = 0.f;
@@ -331,48 +416,73 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
     __builtin_amdgcn_s_setprio(3);
     for (int attempt = 0; attempt <= max_tries; ++attempt) {
       int failed = 0;
-      for (int k = -1; k < T; ++k) {
-        if (k >= 0) {
-          lds_barrier();   // [A]
-          failed = fl[kKfStatus];
-          if (fl[kKfTmo]) failed = kKzzTimeout;
-          if (failed) break;
-          // [B] diagonal blocks of L and L^{-1}
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int e = lane + 64 * u, which = e >> 8, r = (e >> 4) & 15, cc = e & 15;
-            const int row = 16 * k + r, col = 16 * k + cc;
-            if (row < M && col < M) {
-              if (which == 0) L[(size_t)row * M + col] = lkk[r * kLinvStride + cc];
-              else Linv[(size_t)row * M + col] = linv[r * kLinvStride + cc];
-            }
-          }
-          lds_barrier();
-        }
-        if (k + 1 < T) {
-          // [C] look-ahead: tile k+1 was handed over through panel k-1 one step earlier; the
-          // diagonal wave applies panel k's R_{k,k+1} (slot 0) itself and factors it
-          const int tk = k + 1;
-          double* db = dbuf + (tk & 1) * 256;
-          kzz_spin_until(fl, kKfTile + 3 * (tk & 1), attempt * (T + 1) + tk);
-          int* stamp = nullptr;
+      // tile (0, 0): handed over raw by the tile formation
+      kzz_spin_until(fl, kKfTile, attempt * (T + 1));
 #if GPK_KZZ_STAMPS
-          if (attempt == 0) {
-            stamp = info + 1 + 3 * T + 3 * tk;
-            if (lane == 0) stamp[0] = (int)__builtin_amdgcn_s_memtime();
+      if (attempt == 0 && lane == 0) info[1 + 3 * T] = (int)__builtin_amdgcn_s_memtime();
+#endif
+      factor_diag0(dbuf, lkkb, linvb, flagw + kKfStatus, attempt == 0 ? info + 1 + 3 * T : nullptr);
+      for (int k = 0; k < T; ++k) {
+        const int tk = k + 1;
+        int* stamp = nullptr;
+#if GPK_KZZ_STAMPS
+        if (attempt == 0 && tk < T) stamp = info + 1 + 3 * T + 3 * tk;
+#endif
+        // L_kk^{-1} (this wave's own sweep output): A operands of R_{k,k+1}, read before [A]
+        double la[4];
+        wave_lds_sync();
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) la[kk] = linvb[(k & 1) * 16 * kLinvStride + c * kLinvStride + g + 4 * kk];
+        lds_barrier();   // [A]
+        failed = fl[kKfStatus];
+        if (fl[kKfTmo]) failed = kKzzTimeout;
+        if (failed) break;
+        if (tk < T) {
+          // LOOK-AHEAD beside the workers' TRSM of block row k: R_{k,k+1} = L_kk^{-1} T'_{k,k+1}
+          // and T''_{k+1,k+1} = T'_{k+1,k+1} - R^T R from the two tiles handed over in step
+          // k-1's [C] (panels < k applied) -- the same MFMAs as the owners' TRSM and update --
+          // then straight into the sweep of (k+1, k+1), operands moved by permlanes
+#if GPK_KZZ_STAMPS
+          if (stamp != nullptr && lane == 0) stamp[0] = (int)__builtin_amdgcn_s_memtime();
+#endif
+          const double* ob = obuf + (tk & 1) * 256;
+          const double* db = dbuf + (tk & 1) * 256;
+          f64x4 o, t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            o[r] = ob[r * 64 + lane];
+            t[r] = db[r * 64 + lane];
+          }
+#if GPK_KZZ_STAMPS
+          int* s2p = stamp != nullptr ? info + 1 + 8 * T + 4 * tk : nullptr;
+          if (s2p != nullptr) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (lane == 0) s2p[0] = (int)__builtin_amdgcn_s_memtime();
           }
 #endif
-          f64x4 t;
+          f64x4 x = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) t[r] = db[r * 64 + lane];
-          if (k >= 0) {
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) t = mfma64(-panel[kk * 64 + lane], panel[kk * 64 + lane], t);
+          for (int kk = 0; kk < 4; ++kk) x = mfma64(la[kk], o[kk], x);
+#if GPK_KZZ_STAMPS
+          if (s2p != nullptr) {
+            asm volatile("" ::"v"(x[3]));   // the MFMA chain's result is in
+            if (lane == 0) s2p[1] = (int)__builtin_amdgcn_s_memtime();
           }
+#endif
 #pragma unroll
-          for (int r = 0; r < 4; ++r) db[(g + 4 * r) * 16 + c] = t[r];   // row-major for the sweep
-          wave_lds_sync();
-          factor_diag(tk, db, lkk, linv, flagw + kKfStatus, stamp);
+          for (int kk = 0; kk < 4; ++kk) t = mfma64(-x[kk], x[kk], t);
+#if GPK_KZZ_STAMPS
+          if (s2p != nullptr) {
+            asm volatile("" ::"v"(t[3]));
+            if (lane == 0) s2p[2] = s2p[3] = (int)__builtin_amdgcn_s_memtime();
+          }
+#endif
+          // [C] the sweep of (k+1, k+1) overlaps the workers' trailing update of step k; it
+          // writes the other parity of L_kk / L_kk^{-1} (the workers read parity k & 1)
+          double v[16];
+          acc_to_sweep(t, v);
+          sweep_diag(tk, v, lkkb + (tk & 1) * 16 * kLinvStride, linvb + (tk & 1) * 16 * kLinvStride,
+                     flagw + kKfStatus, stamp);
         }
       }
       if (!failed) {
@@ -392,29 +502,32 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
     int its[NS], jts[NS];
     {
       const int ntile = T * (T + 1) / 2;
-      const int wr = kzz_worker_rank(wave);
 #pragma unroll
       for (int q = 0; q < NS; ++q) {
-        const int t = wr + kKzzWorkers * q;
+        const int t = wave + kKzzWorkers * q;
         int it = T, jt = T;   // no tile: coordinates past the end (skipped everywhere)
-        if (wr >= 0 && t < ntile) tile_of(t, T, it, jt);
+        if (t < ntile) tile_of(t, T, it, jt);
         its[q] = __builtin_amdgcn_readfirstlane(it);
         jts[q] = __builtin_amdgcn_readfirstlane(jt);
       }
     }
     f64x4 acc[NS];
+    int nsync = 0;   // worker barriers passed
     for (int attempt = 0; attempt <= max_tries; ++attempt) {
       const double ladder = ladder_of(attempt, jitter_chol);
 #pragma unroll
       for (int q = 0; q < NS; ++q) {
         asm volatile("" : "+s"(its[q]), "+s"(jts[q]));
         if (its[q] < T) acc[q] = kzz_tile(zt, zn, ZS, D16, M, T, its[q], jts[q], s2, jitter_var, ladder);
-        if (its[q] == jts[q] && its[q] < 2 && its[q] < T) {   // hand tiles (0,0), (1,1) over raw
-          const int tk = its[q];
+        if (its[q] == 0 && jts[q] == 0) {   // hand (0, 0) over raw: the sweep starts at once
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dbuf[tk * 256 + r * 64 + lane] = acc[q][r];
+          for (int r = 0; r < 4; ++r) dbuf[r * 64 + lane] = acc[q][r];
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-          if (lane == 0) fl[kKfTile + 3 * tk] = attempt * (T + 1) + tk;
+          if (lane == 0) fl[kKfTile] = attempt * (T + 1);
+        }
+        if (jts[q] == 1 && T > 1) {   // (0, 1), (1, 1) raw: read after barrier [A] of step 0
+#pragma unroll
+          for (int r = 0; r < 4; ++r) (its[q] == 1 ? dbuf : obuf)[256 + r * 64 + lane] = acc[q][r];
         }
       }
       int failed = 0;
@@ -434,7 +547,7 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
         // [B] TRSM of block row k: R_kj = L_kk^{-1} T'_kj -> registers, LDS panel, L
         double la[4];
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) la[kk] = linv[c * kLinvStride + g + 4 * kk];
+        for (int kk = 0; kk < 4; ++kk) la[kk] = linvb[(k & 1) * 16 * kLinvStride + c * kLinvStride + g + 4 * kk];
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
           if (its[q] == k && jts[q] > k && jts[q] < T) {
@@ -452,34 +565,54 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
             }
           }
         }
-        lds_barrier();
+        // worker-only barrier (LDS counter; the diagonal wave is sweeping tile k+1 meanwhile):
+        // panel k is complete. Every worker leaves a failed attempt at the same [A], so the
+        // counts stay in step across attempts.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        ++nsync;
+        if (lane == 0)
+          (void)__atomic_fetch_add((__attribute__((address_space(3))) int*)&flagw[kKfSync], 1, __ATOMIC_RELAXED);
+        kzz_spin_ge(fl, kKfSync, kKzzWorkers * nsync);
 #if GPK_KZZ_STAMPS
         if (tid == 0 && attempt == 0) info[3 + 3 * k] = (int)__builtin_amdgcn_s_memtime();
 #endif
-        // [C] hand over (k+2, k+2) through panel k first (the diagonal wave applies panel
-        // k+1 to it itself); (k+1, k+1) is the diagonal wave's from here on
+        // [C] hand over (k+2, k+2) and (k+1, k+2) through panel k first (the diagonal wave
+        // applies panel k+1 to them itself in step k+1's [B']; it reads them after barrier
+        // [A] of step k+1); (k+1, k+1) is the diagonal wave's from here on
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
-          if (its[q] == k + 2 && jts[q] == k + 2 && k + 2 < T) {
+          if (jts[q] == k + 2 && its[q] >= k + 1 && k + 2 < T) {
             const int tk = k + 2;
+            const double* pa = panel + (size_t)(its[q] - k - 1) * 256;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk)
-              acc[q] = mfma64(-panel[256 + kk * 64 + lane], panel[256 + kk * 64 + lane], acc[q]);
+              acc[q] = mfma64(-pa[kk * 64 + lane], panel[256 + kk * 64 + lane], acc[q]);
+            double* hb = (its[q] == tk ? dbuf : obuf) + (tk & 1) * 256;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dbuf[(tk & 1) * 256 + r * 64 + lane] = acc[q][r];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            if (lane == 0) fl[kKfTile + 3 * (tk & 1)] = attempt * (T + 1) + tk;
+            for (int r = 0; r < 4; ++r) hb[r * 64 + lane] = acc[q][r];
           }
         }
         // (a program-order software pipeline of the operand reads -- tile q+1's requested
         // before tile q's MFMAs -- measured slower: 155 vs 148 us at M = 256)
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
-          if (its[q] > k && its[q] < T && !(its[q] == jts[q] && its[q] <= k + 2)) {
+          if (its[q] > k && its[q] < T && !(its[q] == jts[q] && its[q] <= k + 2) &&
+              !(its[q] == k + 1 && jts[q] == k + 2)) {
             const double* pa = panel + (size_t)(its[q] - k - 1) * 256;
             const double* pb = panel + (size_t)(jts[q] - k - 1) * 256;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) acc[q] = mfma64(-pa[kk * 64 + lane], pb[kk * 64 + lane], acc[q]);
+          }
+        }
+        // the diagonal blocks of L and L^{-1} of step k (LDS parity k & 1, overwritten by the
+        // sweep of tile k+2 only after the next [A]): one 64-element slice per wave 0..7
+        if (wave < 8) {
+          const int e = lane + 64 * wave, r = (e >> 4) & 15, cc = e & 15;
+          const int row = 16 * k + r, col = 16 * k + cc;
+          const int o = (k & 1) * 16 * kLinvStride + r * kLinvStride + cc;
+          if (row < M && col < M) {
+            if (e < 256) L[(size_t)row * M + col] = lkkb[o];
+            else Linv[(size_t)row * M + col] = linvb[o];
           }
         }
       }
@@ -508,9 +641,6 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
 // is the B operand of k-step kk straight from register kk. S tiles dealt over 16 waves
 // (u = wave mod 16: one tile per wave up to M = 256, so a step costs one 4-MFMA chain per
 // wave, not four); the L tiles of the next step are prefetched from L2 during this one.
-#ifndef GPK_KZZ_INV_DEPTH2
-#define GPK_KZZ_INV_DEPTH2 0
-#endif
 constexpr int KIT = 1024, KIW = KIT / 64, KIS = 2;   // KIS slots: up to 32 block rows
 __global__ void __launch_bounds__(KIT)
 gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ info,
@@ -569,25 +699,13 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
     }
   };
   load_a(0, an);
-#if GPK_KZZ_INV_DEPTH2
-  double ann[KIS][4];   // step k + 2's operands, two HBM latencies ahead
-  if (nb > 2) load_a(1, ann);
-#endif
   for (int k = 0; k + 1 < nb; ++k) {
     double a[KIS][4];
 #pragma unroll
     for (int t = 0; t < KIS; ++t)
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) a[t][kk] = an[t][kk];
-#if GPK_KZZ_INV_DEPTH2
-#pragma unroll
-    for (int t = 0; t < KIS; ++t)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) an[t][kk] = ann[t][kk];
-    if (k + 3 < nb) load_a(k + 2, ann);
-#else
     if (k + 2 < nb) load_a(k + 1, an);
-#endif
     double xb[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) xb[kk] = Xs[k * 256 + (g + 4 * kk) * 16 + c];
@@ -634,8 +752,8 @@ void set_lds_once() {
 template <int NS>
 int launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
   const int T = (a.M + 15) >> 4;
-  const size_t lds = (size_t)((T > 1 ? T - 1 : 1) * 256 + 512 + 2 * 16 * kLinvStride) * sizeof(double) +
-                     4 * sizeof(int) + (size_t)(a.M * kzz_zstride(a.D) + a.M + a.D) * sizeof(float);
+  const size_t lds = (size_t)((T > 1 ? T - 1 : 1) * 256 + 1024 + 4 * 16 * kLinvStride) * sizeof(double) +
+                     kKfWords * sizeof(int) + (size_t)(a.M * kzz_zstride(a.D) + a.M + a.D) * sizeof(float);
   if (lds > 160 * 1024) return -4;
   set_lds_once<gpk_kzz16_kernel<NS>>();
   hipLaunchKernelGGL((gpk_kzz16_kernel<NS>), dim3(1), dim3(KT), lds, stream, a.Z, a.hyp, a.M, a.D,
@@ -658,7 +776,6 @@ int gpk_launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
   if (ns <= 4) return launch_kzz16<4>(a, stream);
   if (ns <= 7) return launch_kzz16<7>(a, stream);
   if (ns <= 10) return launch_kzz16<10>(a, stream);
-  if (ns <= 12) return launch_kzz16<12>(a, stream);
   if (ns <= 17) return launch_kzz16<17>(a, stream);
   if (ns <= 21) return launch_kzz16<21>(a, stream);
   return -3;

@@ -21,7 +21,7 @@ h = torch.cat([torch.tensor([LN2]), torch.full((D,), LN2)]).to(dev)
 T = (M + 15) // 16
 L = torch.empty(M, M, dtype=torch.float64, device=dev)
 Li = torch.empty(M, M, dtype=torch.float64, device=dev)
-info = torch.zeros(8 + 8 * T, dtype=torch.int32, device=dev)
+info = torch.zeros(8 + 16 * T, dtype=torch.int32, device=dev)
 lib = _native.lib()
 for _ in range(3):
     rc = lib.gpk_kzz_chol_f64(Z.data_ptr(), h.data_ptr(), M, D, 1e-4, 1e-8, 3, L.data_ptr(), Li.data_ptr(),
@@ -43,13 +43,19 @@ for k, (a, b, c) in enumerate(rows):
 tot = [sum(r[i] for r in rows) for i in range(3)]
 print("sum", tot, "total", sum(tot))
 ds = [v[1 + 3 * T + 3 * k: 4 + 3 * T + 3 * k] for k in range(T)]
-print("diagonal wave, factor of (k,k) (ticks): hand-over seen -> tile loaded / sweep + LDS writes; "
-      "hand-over seen relative to the previous step's TRSM barrier")
+print("diagonal wave, factor of (k,k) (ticks): look-ahead start -> sweep start / sweep + LDS writes; "
+      "look-ahead start relative to the previous step's TRSM barrier")
 for k in range(1, T):
     ld = (ds[k][1] - ds[k][0]) & 0xffffffff
     sw = (ds[k][2] - ds[k][1]) & 0xffffffff
     ho = (ds[k][0] - st[k - 1][2]) & 0xffffffff
-    print(f"k={k:2d} load {ld:6d} sweep {sw:6d}  handover-after-trsm {ho:6d}")
+    print(f"k={k:2d} look-ahead {ld:6d} sweep {sw:6d}  start-after-trsm {ho:6d}")
 iv = v[1 + 6 * T: 1 + 6 * T + T + 1]
 print("inverse kernel, block column 0 (ticks): prologue", (iv[1] - iv[0]) & 0xffffffff, " steps",
       [(iv[2 + k] - iv[1 + k]) & 0xffffffff for k in range(T - 1)], " total", (iv[T] - iv[0]) & 0xffffffff)
+print("look-ahead detail (ticks): operands in -> R done / -> T'' + row-major write done / -> diag blocks stored / -> sweep start")
+for k in range(1, T):
+    a = v[1 + 8 * T + 4 * k: 5 + 8 * T + 4 * k]
+    sw = ds[k][1]
+    print(f"k={k:2d} load {(a[0] - ds[k][0]) & 0xffffffff:6d} R {(a[1] - a[0]) & 0xffffffff:6d} T'' {(a[2] - a[1]) & 0xffffffff:6d} "
+          f"stores {(a[3] - a[2]) & 0xffffffff:6d} to-sweep {(sw - a[3]) & 0xffffffff:6d}")
