@@ -276,13 +276,14 @@ int gpk_variational_adjoint_f32(const float* X, const float* Z, const double* Li
  *   gpk_variational_saved_bytes(B, N, M, D): bytes of that state; 0 when the shape is served
  *     by the recompute adjoint only (M <= 64, or the saved path's LDS plan does not fit).
  *   gpk_variational_train_f32: gpk_variational_f32 + `saved` (device, saved_bytes bytes; may be
- *     NULL only when saved_bytes is 0): A (fp32, as the reference casts it) and the variance
- *     clamp mask of every point.
+ *     NULL only when saved_bytes is 0, else -16): A (fp32, as the reference casts it) and the
+ *     variance clamp mask of every point.
  *   gpk_variational_adjoint_saved_f32: gpk_variational_adjoint_f32 from that state (same
- *     outputs, same argument meaning; -12 when saved_bytes is 0 for the shape), workspace of
- *     gpk_variational_adjoint_saved_workspace_bytes(B, N, M, D) bytes. dLinv is formed as
- *     m u^T + 2 diag(s^2 - 1) Linv G with u = K_ZX gmean, G = K_ZX diag(gvar) K_ZX^T
- *     (= sum_i dA_i K_i^T with the fp64 A; the recompute path uses the fp32-cast A).
+ *     outputs, same argument meaning; saved = argument 9, -12 when saved_bytes is 0 for the
+ *     shape), workspace of gpk_variational_adjoint_saved_workspace_bytes(B, N, M, D) bytes.
+ *     dLinv = sum_i dA_i K_i^T is formed as m u^T + 2 diag(s^2 - 1) G' with u = K_ZX gmean and
+ *     G' = A diag(gvar) K_ZX^T on the saved fp32 A (products exact on f32 MFMA), i.e. the
+ *     reference's own fp32 dA, without a dA / K_ZX workspace.
  * Replaces (reference): the same forward / autograd backward as the two functions above.
  */
 size_t gpk_variational_saved_bytes(int B, int N, int M, int D);
