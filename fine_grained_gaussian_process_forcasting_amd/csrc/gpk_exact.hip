@@ -875,16 +875,17 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
 // read from LDS once per step instead of once per tile. Per step the workers synchronise
 // through per-column panel flags (kFlagPan + j), the z flag and two monotone counters
 // (TRSM phases done / panel reads done) instead of a workgroup-wide step barrier:
-//   1. hand-over HO_K: (K, K+1) and (K+1, K+1) through panel K-1, by the owner of column
-//      K+1, as soon as R_{K-1,K} is out;
 //   2. the other tiles of block row K through panel K-1 (this step's TRSM inputs);
 //   3. right-hand side row K (owner of column K);
 //   4. TRSM of row K with R_KK^{-T} (+ z_K): panel K, flags; the panel buffer is reused
 //      only once every wave has finished reading panel K-2 (kFlagBulk);
+//   4b. the NEXT step's hand-over HO_{K+1} = (K+1, K+2), (K+2, K+2), by their owners: panel
+//      K-1, (K+2, K+2)'s deferred RBF, then panel K as soon as R_{K,K+1}, R_{K,K+2} are out
+//      (round 5; before, HO_K opened step K, i.e. it waited for the owners' whole step K-1);
 //   5. the rest of the trailing update through panel K-1 once panel K-1 is complete
 //      (kFlagTrsm), one P load per column;
 //   6. right-hand side rows > K of the owned columns; count the panel reads done;
-//   7. deferred RBF of block row K+2, zero-L.
+//   7. deferred RBF of block row K+2 (less (K+2, K+2): 4b), zero-L.
 // ---------------------------------------------------------------------------
 constexpr int kColSlots = 20;
 
@@ -929,7 +930,6 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   const int jA = 15 - wv, jB = wv + 1;
   const float* pprev = x.panel + ((K + 1) & 1) * (NB + 1) * 256;   // panel K-1
   float* pcur = x.panel + (K & 1) * (NB + 1) * 256;                // panel K
-  float* hA = x.hbuf + (K & 1) * 512;
   constexpr int OWN_K = ColOwners<K>::col_owner(K);                 // RHS row K, column K
   if constexpr (ST) {
     if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8] = __builtin_amdgcn_s_memtime();
@@ -937,29 +937,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   auto upd = [&](f32x4& d, const float* qt, const pan_op_t p_hl, const pan_op_t p_lh) {
     d = pan_mma2(pan_load(qt, lane), p_hl, p_lh, d);
   };
-  // ---- 1. hand-over HO_K = (K, K+1), (K+1, K+1) through panel K-1
-  if constexpr (K > 0 && K + 1 < NB) {
-    constexpr int HAW = K <= 6 ? K : (K == 7 ? 0 : 14 - K);   // owner of (K, K+1)
-    constexpr int HBW = K <= 6 ? K : (K == 7 ? 1 : 14 - K);   // owner of (K+1, K+1)
-    constexpr int SA = K <= 6 ? 17 - K : (K == 7 ? 19 : K);
-    constexpr int SB = K <= 6 ? 16 - K : (K == 7 ? 19 : K + 1);
-    if (wv == HAW || wv == HBW) {
-      if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);
-      GPK_WAITF(kFlagPan + K + 1, e0 + K - 1)
-      const pan_op_t p = pan_load(pprev + (K + 1) * 256, lane);
-      const pan_op_t pl = pan_swap(p);
-      if (wv == HAW) {
-        GPK_WAITF(kFlagPan + K, e0 + K - 1)
-        upd(acc[SA], pprev + K * 256, p, pl);
-        publish_tile(hA, lane, acc[SA], x.vflag, kFlagHA + (K & 1), e0 + K);
-      }
-      if (wv == HBW) {
-        acc[SB] = pan_mma2(p, p, pl, acc[SB]);
-        publish_tile(hA + 256, lane, acc[SB], x.vflag, kFlagHB + (K & 1), e0 + K);
-      }
-      if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
-    }
-  }
+  // ---- 1. (the hand-over HO_K = (K, K+1), (K+1, K+1) was produced in step K-1: see 4b)
   // ---- 2. the other tiles of row K (K, j), j >= K+2, through panel K-1
   if constexpr (K > 0) {
     const bool a_row = (K + 2 <= jA);                 // (K, A), A >= K+2
@@ -999,7 +977,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if (c == 0) *(f32x4*)&x.rw[16 * K + 4 * grp] = d;
     }
   }
-  GPK_WSTAMP(6, 2)  // hand-over + row K + RHS row K
+  GPK_WSTAMP(6, 2)  // row K + RHS row K
   // ---- 4. TRSM of row K with R_KK^{-T} (panel K) and z_K
   const float* wbk = x.wbuf + (K % 3) * kWBuf;
   const int flag_now = x.vflag[kFlagFact];
@@ -1064,8 +1042,50 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     }
     count_in(x, kFlagTrsm);
   }
+  // ---- 4b. hand-over HO_{K+1} = (K+1, K+2), (K+2, K+2) through panels K-1 AND K, right
+  // after this step's TRSM instead of at the start of step K+1 (behind this step's bulk
+  // update): the owners apply panel K-1, then (K+2, K+2)'s deferred RBF, then panel K as soon
+  // as its two tiles are out -- the same updates in the same order as before, so the same
+  // values -- and the diagonal wave's look-ahead stops waiting for the bulk update.
+  if constexpr (K + 2 < NB) {
+    constexpr int K1 = K + 1;
+    constexpr int HAW = K1 <= 6 ? K1 : (K1 == 7 ? 0 : 14 - K1);   // owner of (K1, K1+1)
+    constexpr int HBW = K1 <= 6 ? K1 : (K1 == 7 ? 1 : 14 - K1);   // owner of (K1+1, K1+1)
+    constexpr int SA = K1 <= 6 ? 17 - K1 : (K1 == 7 ? 19 : K1);
+    constexpr int SB = K1 <= 6 ? 16 - K1 : (K1 == 7 ? 19 : K1 + 1);
+    if (wv == HAW || wv == HBW) {
+      float* hN = x.hbuf + (K1 & 1) * 512;
+      if constexpr (K > 0) {   // panel K-1
+        GPK_WAITF(kFlagPan + K1 + 1, e0 + K - 1)
+        const pan_op_t p = pan_load(pprev + (K1 + 1) * 256, lane);
+        const pan_op_t pl = pan_swap(p);
+        if (wv == HAW) {
+          GPK_WAITF(kFlagPan + K1, e0 + K - 1)
+          upd(acc[SA], pprev + K1 * 256, p, pl);
+        }
+        if (wv == HBW) acc[SB] = pan_mma2(p, p, pl, acc[SB]);
+      }
+      if (wv == HBW) {   // (K+2, K+2)'s deferred RBF (phase 7 skips it)
+        const RbfK rk = read_rbfk(x.smem + x.rbfc);
+        acc[SB] += rbf_tile<NB, FULL>(x.smem, rk, K1 + 1, K1 + 1, lane, x.N);
+      }
+      // panel K (this step's TRSM)
+      GPK_WAITF(kFlagPan + K1 + 1, e0 + K)
+      const pan_op_t p = pan_load(pcur + (K1 + 1) * 256, lane);
+      const pan_op_t pl = pan_swap(p);
+      if (wv == HAW) {
+        GPK_WAITF(kFlagPan + K1, e0 + K)
+        upd(acc[SA], pcur + K1 * 256, p, pl);
+        publish_tile(hN, lane, acc[SA], x.vflag, kFlagHA + (K1 & 1), e0 + K1);
+      }
+      if (wv == HBW) {
+        acc[SB] = pan_mma2(p, p, pl, acc[SB]);
+        publish_tile(hN + 256, lane, acc[SB], x.vflag, kFlagHB + (K1 & 1), e0 + K1);
+      }
+    }
+  }
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
-  GPK_WSTAMP(4, 5)  // TRSM
+  GPK_WSTAMP(4, 5)  // TRSM + hand-over
   if constexpr (K + 1 == NB) return 0;
   // ---- 5. the rest of the trailing update through panel K-1: rows K+1 .. of the owned columns
   if constexpr (K > 0) {
@@ -1076,7 +1096,9 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       const pan_op_t pl = pan_swap(p);
       static_for_range<K + 1, 15>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        if (i <= jA && !(i == K + 1 && jA == K + 1)) upd(acc[i], pprev + i * 256, p, pl);
+        constexpr bool ho = K + 2 < NB && (i == K + 1 || i == K + 2);   // HO_{K+1}: done in 4b
+        if (i <= jA && !(i == K + 1 && jA == K + 1) && !(ho && jA == K + 2))
+          upd(acc[i], pprev + i * 256, p, pl);
       });
     }
     // column B (rows K+1 .. jB <= 7)
@@ -1086,14 +1108,17 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
         const pan_op_t pl = pan_swap(p);
         static_for_range<K + 1, 7>([&](auto I) {
           constexpr int i = decltype(I)::value;
-          if (i <= jB && !(i == K + 1 && jB == K + 1)) upd(acc[17 - i], pprev + i * 256, p, pl);
+          constexpr bool ho = K + 2 < NB && (i == K + 1 || i == K + 2);
+          if (i <= jB && !(i == K + 1 && jB == K + 1) && !(ho && jB == K + 2))
+            upd(acc[17 - i], pprev + i * 256, p, pl);
         });
       }
     }
     // column 8: (w, 8) slot 18 and (w + 7, 8) slot 19
     if constexpr (K + 1 <= 8) {
       const bool s18 = (wv >= K + 1);                             // row w <= 6 < 8
-      const bool s19 = (wv <= 1) && (wv + 7 >= K + 1) && !(wv + 7 == 8 && K + 1 == 8);
+      const bool s19 = (wv <= 1) && (wv + 7 >= K + 1) && !(wv + 7 == 8 && K + 1 == 8) &&
+                       !(K + 2 == 8 && (wv + 7 == K + 1 || wv + 7 == K + 2));   // HO_7: 4b
       if (s18 || s19) {
         const pan_op_t p = pan_load(pprev + 8 * 256, lane);
         const pan_op_t pl = pan_swap(p);
@@ -1122,15 +1147,16 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   if constexpr (K + 2 < NB) {
     constexpr int R = K + 2;
     const RbfK rk = read_rbfk(x.smem + x.rbfc);
-    if (R <= jA) acc[R] += rbf_tile<NB, FULL>(x.smem, rk, R, jA, lane, x.N);
+    // ((R, R) is HO_{K+1}'s tile: its RBF went in with the hand-over, 4b)
+    if (R < jA) acc[R] += rbf_tile<NB, FULL>(x.smem, rk, R, jA, lane, x.N);
     if constexpr (17 - R >= 0 && R <= 7) {
-      if (R <= jB) acc[17 - R] += rbf_tile<NB, FULL>(x.smem, rk, R, jB, lane, x.N);
+      if (R < jB) acc[17 - R] += rbf_tile<NB, FULL>(x.smem, rk, R, jB, lane, x.N);
     }
     if constexpr (R <= 6) {
       if (wv == R) acc[18] += rbf_tile<NB, FULL>(x.smem, rk, R, 8, lane, x.N);
     }
-    if constexpr (R == 7 || R == 8) {
-      if (wv == R - 7) acc[19] += rbf_tile<NB, FULL>(x.smem, rk, R, 8, lane, x.N);
+    if constexpr (R == 7) {
+      if (wv == 0) acc[19] += rbf_tile<NB, FULL>(x.smem, rk, R, 8, lane, x.N);
     }
   }
   if (x.Lb != nullptr) zero_l_block<FULL>(x.Lb, FULL ? 16 * NB : x.N, K, wv, WK, lane);

@@ -639,9 +639,18 @@ gpk_kzz16_kernel(const float* __restrict__ Z, const float* __restrict__ hyp, int
 //   X_jb = T_jb;  for k = jb ..: S_u += -L_uk X_k (u > k), X_{k+1} = T_{k+1} S_{k+1}.
 // k-order of every MFMA: q = g + 4 kk, so a tile held in acc layout (reg r <-> row g + 4r)
 // is the B operand of k-step kk straight from register kk. S tiles dealt over 16 waves
-// (u = wave mod 16: one tile per wave up to M = 256, so a step costs one 4-MFMA chain per
-// wave, not four); the L tiles of the next step are prefetched from L2 during this one.
-constexpr int KIT = 1024, KIW = KIT / 64, KIS = 2;   // KIS slots: up to 32 block rows
+// (u = wave: one tile per wave, M <= 256). Each step's L block column is STAGED in LDS by
+// the whole workgroup from loads along the rows of L, issued two steps ahead (register sets
+// by step parity) and stored into a double-buffered LDS block after the MFMAs of the step
+// before its use: the round-4 per-lane operand gather (16 rows per load instruction) waited
+// for every load right where it was issued (a load under a branch merged into a value makes
+// the compiler wait at the join), ~3-5 K cycles per step against ~1 K of MFMA chain.
+constexpr int KIT = 1024, KIW = KIT / 64;
+constexpr int kInvLS = 17;                 // row stride (doubles) of a staged L tile: conflict-free
+constexpr int kInvTile = 16 * kInvLS;
+__host__ __device__ inline size_t kzz_inv_lds_bytes(int T16) {
+  return ((size_t)T16 * kInvTile + (size_t)T16 * 256 + (size_t)2 * 16 * kInvTile) * sizeof(double);
+}
 __global__ void __launch_bounds__(KIT)
 gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ info,
                    double* __restrict__ Linv) {
@@ -649,8 +658,9 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
   const int Mp = (M + 15) & ~15, T16 = Mp >> 4;
   const int jb = blockIdx.x;
   const int nb = T16 - jb;            // block rows jb .. T16-1 of this block column
-  double* Tv = dsm;                   // nb x 256: T_{jb+u}, row-major [row][col]
-  double* Xs = Tv + nb * 256;         // nb x 256: X_{jb+u}, row-major
+  double* Tv = dsm;                   // nb tiles: T_{jb+u}, row-major [row][col], row stride 17
+  double* Xs = Tv + T16 * kInvTile;   // nb x 256: X_{jb+u}, row-major
+  double* Lb = Xs + T16 * 256;        // 2 x 16 tiles: L_{jb+u, jb+k} of step k, parity k & 1
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (info[0] > 0) return;           // no factor (the op raises NotPSDError)
@@ -659,84 +669,126 @@ gpk_kzz_inv_kernel(const double* __restrict__ L, int M, const int* __restrict__ 
   int* ist = (jb == 0 && tid == 0) ? const_cast<int*>(info) + 1 + 6 * T16 : nullptr;
   if (ist) ist[0] = (int)__builtin_amdgcn_s_memtime();
 #endif
-  auto Lat = [&](int i, int j) -> double {   // L with identity padding beyond M
-    if (i < M && j < M) return L[(size_t)i * M + j];
-    return i == j ? 1.0 : 0.0;
-  };
   for (int e = tid; e < 16 * jb * 16; e += KIT) {   // block rows above the diagonal: zero
     const int i = e >> 4, j = 16 * jb + (e & 15);
     if (i < M && j < M) Linv[(size_t)i * M + j] = 0.0;
   }
+  // staging of step s's L tiles u = s+1 .. nb-1 (block column jb + s): piece p = 2 doubles of
+  // one tile row, two pieces per thread (15 tiles x 128 pieces <= 2 x 1024). Two register sets
+  // (step parity): step s+2's loads are issued in step s and land in LDS at the end of step
+  // s+1, two steps of compute behind the load latency.
+  double st[2][2][2];
+  auto stage_load = [&](int s, double (&st)[2][2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = tid + KIT * h, tt = p >> 7, row = (p >> 3) & 15, pc = p & 7;
+      const int i = 16 * (jb + s + 1 + tt) + row, j = 16 * (jb + s) + 2 * pc;
+      const int ic = i < M ? i : M - 1;      // unconditional loads (clamped): no wait at a join
+      const size_t o = (size_t)ic * M;
+      st[h][0] = L[o + (j < M ? j : M - 1)];
+      st[h][1] = L[o + (j + 1 < M ? j + 1 : M - 1)];
+    }
+  };
+  auto stage_store = [&](int s, const double (&st)[2][2]) {
+    double* dst = Lb + (s & 1) * 16 * kInvTile;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = tid + KIT * h, tt = p >> 7, row = (p >> 3) & 15, pc = p & 7;
+      if (s + 1 + tt < nb) {
+        const int i = 16 * (jb + s + 1 + tt) + row, j = 16 * (jb + s) + 2 * pc;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          dst[tt * kInvTile + row * kInvLS + 2 * pc + q] =
+              (i < M && j + q < M) ? st[h][q] : (i == j + q ? 1.0 : 0.0);
+      }
+    }
+  };
+  stage_load(0, st[0]);
+  stage_load(1, st[1]);
   // diagonal-block inverses T_u = L_uu^{-1}: the factor kernel stored them as the diagonal
   // blocks of Linv (identity padding beyond M)
   for (int e = tid; e < nb * 256; e += KIT) {
     const int u = e >> 8, r = (e >> 4) & 15, q = e & 15;
     const int i = 16 * (jb + u) + r, j = 16 * (jb + u) + q;
-    Tv[e] = (i < M && j < M) ? Linv[(size_t)i * M + j] : (i == j ? 1.0 : 0.0);
+    Tv[u * kInvTile + r * kInvLS + q] = (i < M && j < M) ? Linv[(size_t)i * M + j] : (i == j ? 1.0 : 0.0);
   }
+  if (nb > 1) stage_store(0, st[0]);
   lds_barrier();
   for (int e = tid; e < 256; e += KIT) {      // X_jb = T_jb
-    Xs[e] = Tv[e];
+    const double tv = Tv[(e >> 4) * kInvLS + (e & 15)];
+    Xs[e] = tv;
     const int i = 16 * jb + (e >> 4), j = 16 * jb + (e & 15);
-    if (i < M && j < M) Linv[(size_t)i * M + j] = Tv[e];
+    if (i < M && j < M) Linv[(size_t)i * M + j] = tv;
   }
   lds_barrier();
 #if GPK_KZZ_STAMPS
   if (ist) ist[1] = (int)__builtin_amdgcn_s_memtime();
 #endif
-  f64x4 S[KIS];
+  f64x4 S = {0.0, 0.0, 0.0, 0.0};
+  const int u = wave;                          // this wave's S tile (block row jb + u)
+  // step k: loads of step k+2 into `ld` (unconditional, clamped: no wait at a branch join),
+  // the MFMAs, then step k+1's staged tiles (`sv`, loaded in step k-1) into LDS
+  auto step = [&](int k, double (&ld)[2][2], const double (&sv)[2][2]) {
+    stage_load(k + 2, ld);
+    // the next owner's chain (S_{k+1} -> X_{k+1}) is the step's critical path: it wins the
+    // MFMA issue arbitration against the 14 other waves' S updates on its SIMD
+    const bool owner = wave == k + 1;
+    if (owner) __builtin_amdgcn_s_setprio(3);
+    double tq[4];                              // the owner's T_{k+1} operands, read up front
 #pragma unroll
-  for (int t = 0; t < KIS; ++t) S[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-  // A operands of step k: -L_{jb+u, jb+k}[c][g + 4kk] for the wave's tiles u = wave + KIW t
-  double an[KIS][4];
-  auto load_a = [&](int k, double (&dst)[KIS][4]) {
+    for (int kk = 0; kk < 4; ++kk) tq[kk] = Tv[(owner ? k + 1 : 0) * kInvTile + c * kInvLS + g + 4 * kk];
+    const bool act = u > k && u < nb;
+    const double* lt = Lb + (k & 1) * 16 * kInvTile + (act ? u - k - 1 : 0) * kInvTile;
+    double a[4], xb[4];
 #pragma unroll
-    for (int t = 0; t < KIS; ++t) {
-      const int u = wave + KIW * t;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        dst[t][kk] = (u > k && u < nb) ? -Lat(16 * (jb + u) + c, 16 * (jb + k) + g + 4 * kk) : 0.0;
+    for (int kk = 0; kk < 4; ++kk) {
+      a[kk] = act ? -lt[c * kInvLS + g + 4 * kk] : 0.0;
+      xb[kk] = Xs[k * 256 + (g + 4 * kk) * 16 + c];
     }
-  };
-  load_a(0, an);
-  for (int k = 0; k + 1 < nb; ++k) {
-    double a[KIS][4];
+    if (act) {
 #pragma unroll
-    for (int t = 0; t < KIS; ++t)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) a[t][kk] = an[t][kk];
-    if (k + 2 < nb) load_a(k + 1, an);
-    double xb[4];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) xb[kk] = Xs[k * 256 + (g + 4 * kk) * 16 + c];
-    const int tn = (k + 1) / KIW;         // slot of S_{k+1} in its owner wave
-    const bool own = wave == ((k + 1) % KIW);
-#pragma unroll
-    for (int t = 0; t < KIS; ++t) {
-      const int u = wave + KIW * t;
-      if (u > k && u < nb) {
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) S[t] = mfma64(a[t][kk], xb[kk], S[t]);
-      }
+      for (int kk = 0; kk < 4; ++kk) S = mfma64(a[kk], xb[kk], S);
     }
-    if (own) {                            // X_{k+1} = T_{k+1} S_{k+1}
-      f64x4 sv = S[0];
-#pragma unroll
-      for (int t = 1; t < KIS; ++t) sv = (t == tn) ? S[t] : sv;
+#if GPK_KZZ_STAMPS
+    int* ost = (jb == 0 && owner && lane == 0) ? const_cast<int*>(info) + 1 + 12 * T16 + 4 * k : nullptr;
+    if (ost) {
+      asm volatile("" ::"v"(S[3]));
+      ost[0] = (int)__builtin_amdgcn_s_memtime();
+    }
+#endif
+    if (owner) {                               // X_{k+1} = T_{k+1} S_{k+1}
       f64x4 xv = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) xv = mfma64(Tv[(k + 1) * 256 + c * 16 + g + 4 * kk], sv[kk], xv);
+      for (int kk = 0; kk < 4; ++kk) xv = mfma64(tq[kk], S[kk], xv);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         Xs[(k + 1) * 256 + (g + 4 * r) * 16 + c] = xv[r];
         const int i = 16 * (jb + k + 1) + g + 4 * r, j = 16 * jb + c;
         if (i < M && j < M) Linv[(size_t)i * M + j] = xv[r];
       }
+      __builtin_amdgcn_s_setprio(0);
     }
+#if GPK_KZZ_STAMPS
+    if (ost) ost[1] = (int)__builtin_amdgcn_s_memtime();
+#endif
+    if (k + 2 < nb) stage_store(k + 1, sv);
+#if GPK_KZZ_STAMPS
+    if (ost) {
+      __builtin_amdgcn_s_waitcnt(0);
+      ost[2] = (int)__builtin_amdgcn_s_memtime();
+    }
+#endif
     lds_barrier();
+#if GPK_KZZ_STAMPS
+    if (ost) ost[3] = (int)__builtin_amdgcn_s_memtime();
+#endif
 #if GPK_KZZ_STAMPS
     if (ist) ist[2 + k] = (int)__builtin_amdgcn_s_memtime();
 #endif
+  };
+  for (int k = 0; k + 1 < nb; k += 2) {        // unrolled by two: static register sets
+    step(k, st[0], st[1]);
+    if (k + 2 < nb) step(k + 1, st[1], st[0]);
   }
 }
 
@@ -761,8 +813,8 @@ int launch_kzz16(const GpkKzzArgs& a, hipStream_t stream) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   set_lds_once<gpk_kzz_inv_kernel>();
-  hipLaunchKernelGGL(gpk_kzz_inv_kernel, dim3(T), dim3(KIT), (size_t)2 * T * 256 * sizeof(double),
-                     stream, a.L, a.M, a.info, a.Linv);
+  hipLaunchKernelGGL(gpk_kzz_inv_kernel, dim3(T), dim3(KIT), kzz_inv_lds_bytes(T), stream, a.L, a.M,
+                     a.info, a.Linv);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }

@@ -17,8 +17,9 @@
 // Kernels: gpk_kzzg_gemm_kernel<MODE> (one workgroup per 16 x 16 output tile, its k-blocks
 // split over the 4 waves, all operands requested up front from L2, fp64 MFMA; triangular
 // k-ranges), gpk_kzzg_rbf_kernel (one wave per 16 x 16 tile of W: partial w1 / Wz per row
-// and column block), gpk_kzzg_sum_kernel + gpk_kzzg_fin_kernel (fixed-order sums -> dZ,
-// ds2, dl: deterministic).
+// and column block), gpk_kzzg_rows_kernel (per 16-row block: fixed-order totals -> dZ and
+// the block's dl / ds2 partials) + gpk_kzzg_fin_kernel (fixed-order sum of the T block
+// partials -> ds2, dl): deterministic.
 #include "gpk_common.h"
 #include "gpk_internal.h"
 
@@ -184,61 +185,63 @@ gpk_kzzg_rbf_kernel(const double* __restrict__ S, const float* __restrict__ Z,
   }
 }
 
-// Fixed-order sums over the column blocks: tot[i][0] = w1_i, tot[i][1 + d] = Wz_id
-// (one thread per output, many workgroups).
+// One workgroup per 16-row block ib (16 rows x 16 threads): w1_i and Wz_id summed over the
+// column blocks in a fixed order, dZ of those rows, and the block's fixed-order partials
+// rpart[ib] = {sum_i w1_i, sum_i (w1_i z_id^2 - Wz_id z_id) for each d} (rows in order).
+// (Round 4 ran the row totals and ONE 256-thread workgroup over all M rows: 5 + 19 us.)
 __global__ void __launch_bounds__(256)
-gpk_kzzg_sum_kernel(const double* __restrict__ part, int M, int D, double* __restrict__ tot) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= M * (D + 1)) return;
+gpk_kzzg_rows_kernel(const double* __restrict__ part, const float* __restrict__ Z,
+                     const float* __restrict__ hyp, int M, int D, float* __restrict__ dZ,
+                     double* __restrict__ rpart) {
+  __shared__ double cs[16][kRbfMaxD + 1];
+  __shared__ double w1s[16];
   const int T = (M + 15) >> 4;
-  double v[16];
-#pragma unroll
-  for (int jb = 0; jb < 16; ++jb) v[jb] = jb < T ? part[(size_t)jb * M * (D + 1) + e] : 0.0;
-  double s = 0.0;
-#pragma unroll
-  for (int jb = 0; jb < 16; ++jb) s += v[jb];
-  tot[e] = s;
-}
-
-// dZ (M, D) float, dhyp = {ds2, dl[D]} float from the row totals; the sums over rows in a
-// fixed order (8 row groups per dimension, then the 8 group sums). One workgroup.
-__global__ void __launch_bounds__(256)
-gpk_kzzg_fin_kernel(const double* __restrict__ tot, const float* __restrict__ Z,
-                    const float* __restrict__ hyp, int M, int D, float* __restrict__ dZ,
-                    float* __restrict__ dhyp) {
-  __shared__ double red[256];
-  __shared__ double w1r[4];
-  const int tid = threadIdx.x;
-  for (int e = tid; e < M * D; e += 256) {
-    const int i = e / D, d = e - i * D;
-    const double l = (double)hyp[1 + d];
-    const double z = (double)Z[e] / l;
-    dZ[e] = (float)(2.0 * (tot[(size_t)i * (D + 1) + 1 + d] - z * tot[(size_t)i * (D + 1)]) / l);
+  const int ib = blockIdx.x, tid = threadIdx.x, r = tid >> 4, q = tid & 15;
+  const int i = 16 * ib + r;
+  const bool iok = i < M;
+  double w1 = 0.0;
+  if (iok) {
+    for (int jb = 0; jb < T; ++jb) w1 += part[((size_t)jb * M + i) * (D + 1)];
   }
-  // dl_d = 2/l_d sum_i (w1_i z_id^2 - Wz_id z_id): thread (d, part) with part = tid / D
-  const int nparts = 256 / D;
-  double acc = 0.0;
-  if (tid < nparts * D) {
-    const int d = tid % D, pp = tid / D;
-    const double l = (double)hyp[1 + d];
-    for (int i = pp; i < M; i += nparts) {
+  if (q == 0) w1s[r] = w1;
+  for (int d = q; d < D; d += 16) {
+    double c = 0.0;
+    if (iok) {
+      double wz = 0.0;
+      for (int jb = 0; jb < T; ++jb) wz += part[((size_t)jb * M + i) * (D + 1) + 1 + d];
+      const double l = (double)hyp[1 + d];
       const double z = (double)Z[(size_t)i * D + d] / l;
-      acc += tot[(size_t)i * (D + 1)] * z * z - tot[(size_t)i * (D + 1) + 1 + d] * z;
+      dZ[(size_t)i * D + d] = (float)(2.0 * (wz - z * w1) / l);
+      c = w1 * z * z - wz * z;
     }
+    cs[r][d] = c;
   }
-  red[tid] = acc;
-  // ds2 = sum_i w1_i / s2: one wave per quarter of the rows
-  double w = 0.0;
-  for (int i = tid; i < M; i += 256) w += tot[(size_t)i * (D + 1)];
-  w = wave_sum_d(w);
-  if ((tid & 63) == 0) w1r[tid >> 6] = w;
   __syncthreads();
+  double* out = rpart + (size_t)ib * (D + 1);
   if (tid < D) {
     double s = 0.0;
-    for (int pp = 0; pp < nparts; ++pp) s += red[pp * D + tid];
-    dhyp[1 + tid] = (float)(2.0 * s / (double)hyp[1 + tid]);
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) s += cs[rr][tid];
+    out[1 + tid] = s;
+  } else if (tid == D) {
+    double s = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) s += w1s[rr];
+    out[0] = s;
   }
-  if (tid == 0) dhyp[0] = (float)((((w1r[0] + w1r[1]) + w1r[2]) + w1r[3]) / (double)hyp[0]);
+}
+
+// dhyp = {ds2 = sum w1 / s2, dl_d = 2 / l_d sum_i (...)} from the row-block partials, summed
+// over the blocks in a fixed order. One wave per output group.
+__global__ void __launch_bounds__(128)
+gpk_kzzg_fin_kernel(const double* __restrict__ rpart, const float* __restrict__ hyp, int M, int D,
+                    float* __restrict__ dhyp) {
+  const int e = threadIdx.x;
+  if (e > D) return;
+  const int T = (M + 15) >> 4;
+  double s = 0.0;
+  for (int ib = 0; ib < T; ++ib) s += rpart[(size_t)ib * (D + 1) + e];
+  dhyp[e] = e == 0 ? (float)(s / (double)hyp[0]) : (float)(2.0 * s / (double)hyp[e]);
 }
 
 template <int MODE>
@@ -270,12 +273,11 @@ int gpk_launch_kzz_grad(const GpkKzzGradArgs& a, hipStream_t stream) {
   const int T = (M + 15) >> 4;
   hipLaunchKernelGGL(gpk_kzzg_rbf_kernel, dim3(T * T), dim3(64), 0, stream, b0, a.Z, a.hyp, M, D, part);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  double* tot = part + (size_t)T * M * (D + 1);
-  hipLaunchKernelGGL(gpk_kzzg_sum_kernel, dim3((M * (D + 1) + 255) / 256), dim3(256), 0, stream, part, M,
-                     D, tot);
+  double* rpart = part + (size_t)T * M * (D + 1);
+  hipLaunchKernelGGL(gpk_kzzg_rows_kernel, dim3(T), dim3(256), 0, stream, part, a.Z, a.hyp, M, D, a.dZ,
+                     rpart);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(gpk_kzzg_fin_kernel, dim3(1), dim3(256), 0, stream, tot, a.Z, a.hyp, M, D, a.dZ,
-                     a.dhyp);
+  hipLaunchKernelGGL(gpk_kzzg_fin_kernel, dim3(1), dim3(128), 0, stream, rpart, a.hyp, M, D, a.dhyp);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }

@@ -59,3 +59,9 @@ for k in range(1, T):
     sw = ds[k][1]
     print(f"k={k:2d} load {(a[0] - ds[k][0]) & 0xffffffff:6d} R {(a[1] - a[0]) & 0xffffffff:6d} T'' {(a[2] - a[1]) & 0xffffffff:6d} "
           f"stores {(a[3] - a[2]) & 0xffffffff:6d} to-sweep {(sw - a[3]) & 0xffffffff:6d}")
+print("inverse, owner wave of each step (block column 0; ticks from the previous barrier): S done / X done / staging stored / barrier")
+for k in range(1, T - 1):
+    o = v[1 + 12 * T + 4 * k: 5 + 12 * T + 4 * k]
+    prev = iv[1 + k]
+    print(f"k={k:2d} S {(o[0] - prev) & 0xffffffff:6d} X {(o[1] - o[0]) & 0xffffffff:6d} store {(o[2] - o[1]) & 0xffffffff:6d} "
+          f"barrier {(o[3] - o[2]) & 0xffffffff:6d}")

@@ -1,7 +1,8 @@
 """Per-step timeline of the exact kernel's column-ownership plan (STAMPS build, N=256 D=32).
 
-Worker events per (step k, wave w): 0 start, 2 hand-over + row k + RHS k, 4 R_kk^-T arrived,
-5 TRSM done, 1 trailing update done, 6 RHS rows + bulk count, 3 RBF + zero-L (step end),
+Worker events per (step k, wave w): 0 start, 2 row k + RHS k, 4 R_kk^-T arrived,
+5 TRSM + the next step's hand-over (HO_{k+1}) done, 1 trailing update done, 6 RHS rows + bulk
+count, 3 RBF + zero-L (step end),
 7 cumulative cycles spent in flag waits (panel / z / counters; not the R_kk^-T wait).
 Diagonal wave (w = 7): 0 factor start, 1 factor done (R_kk^-T published), 2 look-ahead
 tiles arrived, 3 look-ahead done.
@@ -52,8 +53,8 @@ wcum = tl[:, :, :7, 7].astype(np.float64)        # cumulative waits (B, 16, 7)
 wstep = np.diff(np.concatenate([np.zeros((B, 1, 7)), wcum], axis=1), axis=1)
 wstep[:, 15] = np.nan
 ws = np.nanmean(wstep, axis=0)                   # (16, 7)
-print(" k | diag fac0   fac1   LAin LAdone (LA wait) | wrk start  end  (dur) | mean per wave: HO+rowK  "
-      "Wwait  TRSM  trail  rhs+cnt  rbf+zl | flag-wait | slowest wave end")
+print(" k | diag fac0   fac1   LAin LAdone (LA wait) | wrk start  end  (dur) | mean per wave:  rowK  "
+      "Wwait TRSM+HO trail  rhs+cnt  rbf+zl | flag-wait | slowest wave end")
 for k in range(16):
     d = m[k, 7]
     w = m[k, :7]                                   # (7, 8)
