@@ -739,11 +739,17 @@ __global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : GPK_GRAM_WPE) gpk_grad
   }
   lds_barrier();
   for (int n = tid; n < NP; n += 64 * kGW) {
+    // |xs_n|^2 from the planes, 16-byte reads (the same dims in the same order as 2-byte reads)
     float t = 0.f;
 #pragma unroll
-    for (int d = 0; d < DW; ++d) {
-      const float x = (float)xh[n * RS + d] + (float)xl[n * RS + d];
-      t = __builtin_fmaf(x, x, t);
+    for (int d0 = 0; d0 < DW; d0 += 8) {
+      const half8_t h8 = *(const half8_t*)&xh[n * RS + d0];
+      const half8_t l8 = *(const half8_t*)&xl[n * RS + d0];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float x = (float)h8[q] + (float)l8[q];
+        t = __builtin_fmaf(x, x, t);
+      }
     }
     nrm[n] = t;
   }

@@ -2026,9 +2026,13 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 // 8 g + j). Partials gpart[wg] = G' tiles (acc layout) | u, summed in a fixed order afterwards
 // (gpk_var_red_kernel), then gpk_var_gdl_l_kernel forms dL^{-1} elementwise.
 // ---------------------------------------------------------------------------
-template <int MB, int DQ>
+#ifndef GPK_KGRAM_SPL
+#define GPK_KGRAM_SPL 2   // waves per G' tile-row pair (1: 8 waves x 17 tiles, 209 VGPRs, 2 waves/SIMD)
+#endif
+template <int MB, int DQ, int SPL = GPK_KGRAM_SPL>
 struct LGramGeo {
-  static constexpr int NWV = (MB + 1) / 2, NT = 64 * NWV, MP = 16 * MB, DS = DQ + 2;
+  static constexpr int NWV = SPL * ((MB + 1) / 2), NT = 64 * NWV, MP = 16 * MB, DS = DQ + 2;
+  static constexpr int HS = (MB + 1 + SPL - 1) / SPL;      // G' slots per wave (of the pair's MB + 1)
   static constexpr int NPASS = (LTW * 16 + NT - 1) / NT, DV = DQ / 16;
   static constexpr int KS = LTW + 4;                       // row stride of the A / K blocks (floats)
   static constexpr int NTILE = MB * (MB + 1) / 2;
@@ -2048,7 +2052,7 @@ struct LGramGeo {
 };
 
 template <int MB, int DQ>
-__global__ void __launch_bounds__(64 * ((MB + 1) / 2), 2)
+__global__ void __launch_bounds__(64 * GPK_KGRAM_SPL * ((MB + 1) / 2), GPK_KGRAM_SPL == 1 ? 2 : 4)
 gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
                        const float* __restrict__ vmean, const float* __restrict__ vstd,
                        const float* __restrict__ hyp, const float* __restrict__ gmean,
@@ -2057,13 +2061,18 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   using G = LGramGeo<MB, DQ>;
   using SV = LSaved<MB>;
   constexpr int NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV, KS = G::KS;
+  constexpr int SPL = GPK_KGRAM_SPL, HS = G::HS;
   constexpr int NU = SV::tiles / 4;                 // f32x4 units of A per chunk
   static_assert(NU % NT == 0, "A block: whole passes");
   extern __shared__ __attribute__((aligned(16))) float vsm[];
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4, sub = tid & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int IA = wave, IB = MB - 1 - wave;
+  // the tile-row pair (IA, IB) of this wave and its share of the pair's slots
+  // (slot s <= IA: tile (IA, s); slot IA + 1 + s': tile (IB, s')), [s0, s0 + HS)
+  const int pr = wave / SPL, hf = wave - pr * SPL;
+  const int IA = pr, IB = MB - 1 - pr;
   const bool two = IB != IA;
+  const int nslot = two ? MB + 1 : IA + 1, s0 = hf * HS;
   const float s2 = hyp[0];
   const float* ls = hyp + 4 + D;
   const int nch = (N + LTW - 1) / LTW;
@@ -2078,10 +2087,9 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   float cmr[DV];
 #pragma unroll
   for (int v = 0; v < DV; ++v) cmr[v] = vsm[G::oCm + sub + 16 * v];
-  // accumulators: slot s <= IA: tile (IA, s); slot IA + 1 + s': tile (IB, s')
-  f32x4 gacc[MB + 1];
+  f32x4 gacc[HS];
 #pragma unroll
-  for (int s = 0; s <= MB; ++s) gacc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < HS; ++s) gacc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 uacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   // the chunk's A units (4 rows of one point each): loaded one chunk ahead (registers)
   f32x4 au[NU / NT];
@@ -2128,10 +2136,11 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       load_a(t + gridDim.x);   // (au was consumed by the LDS stores above)
     }
     lds_barrier();
-    // K_ZX of the wave's rows -> Kr[row][point]; u partials
+    // K_ZX of the wave's rows -> Kr[row][point]; u partials (SPL = 2: half 0 row IA, half 1 IB)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (h == 1 && !two) break;
+      if (SPL == 2 && h != hf) continue;
       const int rt = h == 0 ? IA : IB;
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
@@ -2172,14 +2181,15 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         aB[q] *= gv0[q]; aB[4 + q] *= gv1[q];
       }
 #pragma unroll
-      for (int s = 0; s <= MB; ++s) {
+      for (int ls = 0; ls < HS; ++ls) {
+        const int s = s0 + ls;
+        if (s >= nslot) break;
         const bool isA = s <= IA;
         const int J = isA ? s : s - IA - 1;
-        if (!isA && !two) break;
         float bo[8];
         rowop(Kr, J, bo);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) gacc[s] = mfma32(isA ? aA[q] : aB[q], bo[q], gacc[s]);
+        for (int q = 0; q < 8; ++q) gacc[ls] = mfma32(isA ? aA[q] : aB[q], bo[q], gacc[ls]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -2187,15 +2197,17 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   // partials: tile (I, J) at (I (I + 1) / 2 + J) * 256 + lane * 4 + r (acc layout) | u
   float* po = gpart + (size_t)blockIdx.x * G::PG;
 #pragma unroll
-  for (int s = 0; s <= MB; ++s) {
+  for (int ls = 0; ls < HS; ++ls) {
+    const int s = s0 + ls;
+    if (s >= nslot) break;
     const bool isA = s <= IA;
-    if (!isA && !two) break;
     const int I = isA ? IA : IB, J = isA ? s : s - IA - 1;
-    *(f32x4*)(po + (I * (I + 1) / 2 + J) * 256 + lane * 4) = gacc[s];
+    *(f32x4*)(po + (I * (I + 1) / 2 + J) * 256 + lane * 4) = gacc[ls];
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (h == 1 && !two) break;
+    if (SPL == 2 && h != hf) continue;
     const int rt = h == 0 ? IA : IB;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
