@@ -199,16 +199,24 @@ gpk_kzzg_rows_kernel(const double* __restrict__ part, const float* __restrict__ 
   const int ib = blockIdx.x, tid = threadIdx.x, r = tid >> 4, q = tid & 15;
   const int i = 16 * ib + r;
   const bool iok = i < M;
-  double w1 = 0.0;
-  if (iok) {
-    for (int jb = 0; jb < T; ++jb) w1 += part[((size_t)jb * M + i) * (D + 1)];
-  }
+  const int ic = iok ? i : 0;
+  // the T <= 16 column-block partials of a row: all loads issued together (clamped, fixed
+  // count), then the fixed-order sum -- a runtime-bounded load + add loop waited per load
+  auto colsum = [&](int o) {
+    double v[16];
+#pragma unroll
+    for (int jb = 0; jb < 16; ++jb) v[jb] = part[((size_t)(jb < T ? jb : 0) * M + ic) * (D + 1) + o];
+    double t = 0.0;
+#pragma unroll
+    for (int jb = 0; jb < 16; ++jb) t += jb < T ? v[jb] : 0.0;
+    return t;
+  };
+  const double w1 = iok ? colsum(0) : 0.0;
   if (q == 0) w1s[r] = w1;
   for (int d = q; d < D; d += 16) {
     double c = 0.0;
     if (iok) {
-      double wz = 0.0;
-      for (int jb = 0; jb < T; ++jb) wz += part[((size_t)jb * M + i) * (D + 1) + 1 + d];
+      const double wz = colsum(1 + d);
       const double l = (double)hyp[1 + d];
       const double z = (double)Z[(size_t)i * D + d] / l;
       dZ[(size_t)i * D + d] = (float)(2.0 * (wz - z * w1) / l);
@@ -239,8 +247,12 @@ gpk_kzzg_fin_kernel(const double* __restrict__ rpart, const float* __restrict__ 
   const int e = threadIdx.x;
   if (e > D) return;
   const int T = (M + 15) >> 4;
+  double v[16];
+#pragma unroll
+  for (int ib = 0; ib < 16; ++ib) v[ib] = rpart[(size_t)(ib < T ? ib : 0) * (D + 1) + e];
   double s = 0.0;
-  for (int ib = 0; ib < T; ++ib) s += rpart[(size_t)ib * (D + 1) + e];
+#pragma unroll
+  for (int ib = 0; ib < 16; ++ib) s += ib < T ? v[ib] : 0.0;
   dhyp[e] = e == 0 ? (float)(s / (double)hyp[0]) : (float)(2.0 * s / (double)hyp[e]);
 }
 

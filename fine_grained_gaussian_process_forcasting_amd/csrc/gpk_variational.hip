@@ -2490,8 +2490,13 @@ gpk_var_fin2_kernel(const float* __restrict__ vstd, const float* __restrict__ hy
   const double* gx = rx2 + D + 2;
   const double sumgm = gx[D];
   if (tid < D) {
+    // the <= 16 block partials: loads issued together (clamped, fixed count), fixed-order sum
+    double pv[256 / kFinRows];
+#pragma unroll
+    for (int k = 0; k < 256 / kFinRows; ++k) pv[k] = dlp[(size_t)(k < nblk ? k : 0) * D + tid];
     double v = rx2[tid];
-    for (int k = 0; k < nblk; ++k) v += dlp[(size_t)k * D + tid];
+#pragma unroll
+    for (int k = 0; k < 256 / kFinRows; ++k) v += k < nblk ? pv[k] : 0.0;
     dpar[2 * M + 1 + tid] = (float)(v / (double)ls[tid]);
     dpar[2 * M + 1 + D + tid] = (float)((double)ls[tid] * (gx[tid] + (double)cmf[tid] * sumgm));
   }
