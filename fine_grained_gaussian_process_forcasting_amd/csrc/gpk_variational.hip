@@ -1694,7 +1694,7 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
                       const float* __restrict__ vstd, const float* __restrict__ hyp,
                       const float* __restrict__ gmean, const float* __restrict__ gvar,
                       const float* __restrict__ saved, int N, int M, int D, int nchunks,
-                      float* __restrict__ wspart, float* __restrict__ dX) {
+                      float* __restrict__ wspart, float* __restrict__ dX, float* __restrict__ cm_out) {
   using G = LAdjGeo<MB, DQ>;
   using SV = LSaved<MB>;
   constexpr int NWV = G::NWV, NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV, NDT = G::NDT;
@@ -1757,6 +1757,7 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   };
   copy_a(blockIdx.x, vsm + G::kdA);
   lds_barrier();
+  if (blockIdx.x == 0 && tid < D) cm_out[tid] = vsm[G::kCm + tid];   // the finisher's centre
   float cmr[DV];
 #pragma unroll
   for (int v = 0; v < DV; ++v) cmr[v] = vsm[G::kCm + sub + 16 * v];
@@ -2394,13 +2395,24 @@ constexpr size_t kFinWsBytes = (256 / kFinRows) * 64 * sizeof(double) + 64 * siz
 __global__ void __launch_bounds__(256)
 gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ hyp,
                    const double* __restrict__ tot, int M, int D, float* __restrict__ dZ,
-                   double* __restrict__ dlp, float* __restrict__ cm_out) {
+                   double* __restrict__ dlp, float* __restrict__ cm_out, const float* __restrict__ cm_in) {
   extern __shared__ __attribute__((aligned(16))) float fzs[];   // M x D zs (centred Z / l)
   __shared__ double red[256];
   __shared__ float cmf[64];
   __shared__ float cms[kCmParts * 64];
   const int tid = threadIdx.x;
   const float* ls = hyp + 4 + D;
+  const int p0 = blockIdx.x * kFinRows;
+  const int np = M - p0 < kFinRows ? M - p0 : kFinRows;
+  if (cm_in != nullptr) {
+    // the centre from the adjoint kernel (its stage_inducing: the same fixed-order sums), so
+    // only this block's rows of Z are staged
+    if (tid < D) cmf[tid] = cm_in[tid];
+    for (int e = tid; e < np * D; e += 256) {
+      const int d = e % D;
+      fzs[p0 * D + e] = Z[(size_t)p0 * D + e] / ls[d] - cm_in[d];
+    }
+  } else {
   for (int base = 0; base < M * D; base += 32 * 256) {
     float zv[32], lv[32];
 #pragma unroll
@@ -2417,11 +2429,10 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ hyp,
   }
   lds_barrier();
   col_means(fzs, M, D, D, D, cms, cmf);   // the same fp32 sums as stage_inducing: the identical centre
-  const int p0 = blockIdx.x * kFinRows;
-  const int np = M - p0 < kFinRows ? M - p0 : kFinRows;
-  if (blockIdx.x == 0 && tid < D) cm_out[tid] = cmf[tid];
   for (int e = tid; e < np * D; e += 256) fzs[p0 * D + e] -= cmf[e % D];
+  }
   lds_barrier();
+  if (blockIdx.x == 0 && tid < D) cm_out[tid] = cmf[tid];
   const double* QX = tot;
   const double* q = tot + (size_t)M * D;
   {
@@ -2512,7 +2523,7 @@ gpk_var_fin2_kernel(const float* __restrict__ vstd, const float* __restrict__ hy
 
 // the two output launches (ws: nblk x D doubles of dl partials, then D floats of the centre)
 int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const double* tot, int M, int D,
-                   float* dZ, float* dpar, void* ws, hipStream_t stream);
+                   float* dZ, float* dpar, void* ws, hipStream_t stream, const float* cm_in = nullptr);
 
 // ---------------------------------------------------------------------------
 // Register-resident variants for M <= 64, D <= 32 (BASELINE cfg 5: M = 64, D = 32).
@@ -3556,13 +3567,13 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
 }
 
 int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const double* tot, int M, int D,
-                   float* dZ, float* dpar, void* ws, hipStream_t stream) {
+                   float* dZ, float* dpar, void* ws, hipStream_t stream, const float* cm_in) {
   const int nblk = (M + kFinRows - 1) / kFinRows;
   double* dlp = (double*)ws;
   float* cm = (float*)(dlp + (size_t)nblk * D);
   set_lds_once<gpk_var_fin_kernel, 64 * 1024>();   // + ~3.3 KB static
   hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(nblk), dim3(256), (size_t)M * D * sizeof(float), stream, Z, hyp,
-                     tot, M, D, dZ, dlp, cm);
+                     tot, M, D, dZ, dlp, cm, cm_in);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(gpk_var_fin2_kernel, dim3(1), dim3(256), 0, stream, vstd, hyp, tot, M, D, nblk, dlp, cm,
@@ -3596,7 +3607,7 @@ int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t st
 struct AdjSavedPlan {
   int nchunks, nwg, nwg_g, P, PG;
   long long BN;
-  size_t off_gpart, off_part, off_tot, off_gtot, off_fin, total, fin_lds;
+  size_t off_gpart, off_part, off_tot, off_gtot, off_fin, off_cm, total, fin_lds;
 };
 
 template <int MB, int DQ>
@@ -3618,6 +3629,7 @@ AdjSavedPlan adj_saved_plan(int B, int N, int M, int D) {
   p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
   p.off_gtot = o; o = al(o + (size_t)p.PG * sizeof(double));
   p.off_fin = o; o = al(o + kFinWsBytes);
+  p.off_cm = o; o = al(o + 64 * sizeof(float));
   p.total = o;
   return p;
 }
@@ -3636,7 +3648,7 @@ int launch_var_adj_saved(const GpkVarAdjArgs& a, hipStream_t stream) {
     set_lds_once<gpk_var_adjs_l_kernel<MB, DQ>>();
     hipLaunchKernelGGL((gpk_var_adjs_l_kernel<MB, DQ>), dim3(p.nwg), dim3(LA::NT), (size_t)LA::k_total * sizeof(float),
                        stream, a.X, a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.saved, a.N, a.M,
-                       a.D, p.nchunks, wspart, a.dX);
+                       a.D, p.nchunks, wspart, a.dX, (float*)(ws + p.off_cm));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     set_lds_once<gpk_var_kgram_l_kernel<MB, DQ>>();
@@ -3653,7 +3665,8 @@ int launch_var_adj_saved(const GpkVarAdjArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(gpk_var_gdl_l_kernel, dim3((unsigned)(((long long)a.M * a.M + 255) / 256)), dim3(256), 0,
                        stream, gtot, a.vmean, a.vstd, a.M, MB, a.dLinv);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream);
+    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream,
+                          (const float*)(ws + p.off_cm));
   } else {
     return -13;
   }
