@@ -2392,15 +2392,35 @@ gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __r
 // dpar = [dvmean (M) | dvstd (M) | ds2 | dl (D) | dw (D) | db0]  (cm: written by block 0)
 constexpr int kFinRows = 16;
 constexpr size_t kFinWsBytes = (256 / kFinRows) * 64 * sizeof(double) + 64 * sizeof(float);
+GPK_DEVICE void var_gdl_block(const double* __restrict__ gtot, const double* __restrict__ Linv,
+                              const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
+                              double* __restrict__ dLinv, double (*Gs)[65], double* us);
+
+// gd != nullptr (register path, M <= 64): one extra workgroup forms dL^{-1} from the K-Gram
+// totals (var_gdl_block) beside the output blocks instead of in a launch of its own
+struct VarGdlArgs {
+  const double* gtot;
+  const double* Linv;
+  const float* vmean;
+  const float* vstd;
+  double* dLinv;
+};
+
 __global__ void __launch_bounds__(256)
 gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ hyp,
                    const double* __restrict__ tot, int M, int D, float* __restrict__ dZ,
-                   double* __restrict__ dlp, float* __restrict__ cm_out, const float* __restrict__ cm_in) {
+                   double* __restrict__ dlp, float* __restrict__ cm_out, const float* __restrict__ cm_in,
+                   VarGdlArgs gd) {
   extern __shared__ __attribute__((aligned(16))) float fzs[];   // M x D zs (centred Z / l)
   __shared__ double red[256];
   __shared__ float cmf[64];
   __shared__ float cms[kCmParts * 64];
   const int tid = threadIdx.x;
+  if (gd.gtot != nullptr && blockIdx.x == gridDim.x - 1) {
+    double* gl = (double*)fzs;
+    var_gdl_block(gd.gtot, gd.Linv, gd.vmean, gd.vstd, M, gd.dLinv, (double(*)[65])gl, gl + 64 * 65);
+    return;
+  }
   const float* ls = hyp + 4 + D;
   const int p0 = blockIdx.x * kFinRows;
   const int np = M - p0 < kFinRows ? M - p0 : kFinRows;
@@ -2523,7 +2543,8 @@ gpk_var_fin2_kernel(const float* __restrict__ vstd, const float* __restrict__ hy
 
 // the two output launches (ws: nblk x D doubles of dl partials, then D floats of the centre)
 int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const double* tot, int M, int D,
-                   float* dZ, float* dpar, void* ws, hipStream_t stream, const float* cm_in = nullptr);
+                   float* dZ, float* dpar, void* ws, hipStream_t stream, const float* cm_in = nullptr,
+                   const VarGdlArgs* gd = nullptr);
 
 // ---------------------------------------------------------------------------
 // Register-resident variants for M <= 64, D <= 32 (BASELINE cfg 5: M = 64, D = 32).
@@ -2542,8 +2563,12 @@ int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const do
                          // prefetch measured slower at 3 (spills) and at 2 waves/SIMD)
 #endif
 constexpr int RLS = 66;        // L^{-1} row stride (doubles)
+constexpr int kGTiles = 10;                  // lower 16 x 16 tiles of a 64 x 64 G
+constexpr int kGPart = kGTiles * 256 + 64;   // floats per workgroup K-Gram partial
 
-template <int DQ>
+// NW waves per workgroup; FG: the adjoint also accumulates the K-Gram G / u per wave
+// (gpk_var_adj_r_kernel with the K-Gram folded in, 8 waves: 154 KB at DQ = 32)
+template <int DQ, int NW = 4, bool FG = false>
 struct RegLds {
   static constexpr int ZS = DQ + 1;
   static constexpr int zs = 0;                      // 64 x ZS
@@ -2554,11 +2579,12 @@ struct RegLds {
   static constexpr int li = ((cm + DQ + 3) / 4) * 4;          // 64 x RLS doubles (16-B aligned)
   static constexpr int fwd_total = li + 2 * 64 * RLS;
   // adjoint only: per-wave transpose scratch, per-wave row accumulators, reductions
-  static constexpr int scr = fwd_total;             // 4 x 320
-  static constexpr int rows = scr + 4 * 320;        // 4 waves x 3 x 64 (dvm, dsm, q)
-  static constexpr int qxr = rows + 4 * 3 * 64;     // 64 x DQ  (workgroup QX)
-  static constexpr int misc = qxr + 64 * DQ;        // 4 x (2 DQ + 3)
-  static constexpr int adj_total = misc + 4 * (2 * DQ + 3);
+  static constexpr int scr = fwd_total;             // NW x 320
+  static constexpr int rows = scr + NW * 320;       // NW waves x 4 x 64 (dvm, dsm, q, u)
+  static constexpr int qxr = rows + NW * 4 * 64;    // 64 x DQ  (workgroup QX)
+  static constexpr int misc = qxr + 64 * DQ;        // NW x (2 DQ + 3)
+  static constexpr int gacc = ((misc + NW * (2 * DQ + 3) + 3) / 4) * 4;   // NW x 10 G tiles
+  static constexpr int adj_total = gacc + (FG ? NW * kGTiles * 256 : 0);
 };
 
 // stage zs, norms, q(u) moments (stage_inducing) and L^{-1} (zero padded to 64 x 64)
@@ -2765,15 +2791,35 @@ gpk_var_fwd_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     (void)__hip_atomic_fetch_or(flags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int DQ>
-__global__ void __launch_bounds__(256, 2)
+// FG (the K-Gram folded in, NW = 8): the same pass also accumulates the K-Gram partials of
+// gpk_var_kgram_r_kernel -- G = K_ZX diag(gvar) K_ZX^T (10 lower tiles, per-wave fp32 in LDS)
+// and u = sum gmean K_ZX -- from the K_ZX tiles it already holds, so X is read once per
+// adjoint instead of twice and the clamp-masked gvar never goes to HBM. The K-Gram partial
+// follows the adjoint partial in the workgroup's row (one reduction launch for both), and
+// block 0 writes the centre cm for gpk_var_fin_kernel.
+// Order of the per-wave scratch transposes: one wave's LDS operations execute in issue order,
+// so a code-motion barrier is enough between a tile's writes, its reads and the next tile's
+// writes (GPK_ADJ_LDS_WAIT=1: the waitcnt-draining wave_lds_sync instead, for A/B builds)
+#ifndef GPK_ADJ_LDS_WAIT
+#define GPK_ADJ_LDS_WAIT 0
+#endif
+GPK_DEVICE void adj_lds_order() {
+#if GPK_ADJ_LDS_WAIT
+  wave_lds_sync();
+#else
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+
+template <int DQ, int NW, bool FG>
+__global__ void __launch_bounds__(64 * NW, 8 / NW)
 gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
                      const double* __restrict__ Linv, const float* __restrict__ vmean,
                      const float* __restrict__ vstd, const float* __restrict__ hyp,
                      const float* __restrict__ gmean, const float* __restrict__ gvar, int B, int N,
                      int M, int D, long long BN, float* __restrict__ wsgv,
-                     float* __restrict__ wspart, float* __restrict__ dX) {
-  using L = RegLds<DQ>;
+                     float* __restrict__ wspart, float* __restrict__ cm_out, float* __restrict__ dX) {
+  using L = RegLds<DQ, NW, FG>;
   constexpr int NDT = DQ / 16;
   extern __shared__ __attribute__((aligned(16))) float vsm[];
   const float s2 = hyp[0], jit = hyp[2];
@@ -2782,9 +2828,12 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int wave = tid >> 6;
   stage_reg<DQ>(Z, ls, vmean, vstd, Linv, M, D, vsm);
-  float* rows = vsm + L::rows + wave * 3 * 64;    // this wave's dvm | dsm | q accumulators
-  for (int e = lane; e < 3 * 64; e += 64) rows[e] = 0.f;
+  float* rows = vsm + L::rows + wave * 4 * 64;    // this wave's dvm | dsm | q | u accumulators
+  for (int e = lane; e < 4 * 64; e += 64) rows[e] = 0.f;
   float* scr = vsm + L::scr + wave * 320;
+  float* ga = vsm + L::gacc + wave * (kGTiles * 256);   // FG: this wave's G tiles (acc order)
+  if constexpr (FG)
+    for (int e = lane; e < kGTiles * 64; e += 64) *(f32x4*)(ga + 4 * e) = f32x4{0.f, 0.f, 0.f, 0.f};
   float il[DQ / 4], cmv[DQ / 4], wv[DQ / 4];
   dim_consts<DQ>(vsm, ls, nullptr, D, il, cmv, wv);
   // constants of the dims 16 dt + c (QX / dX operands)
@@ -2807,7 +2856,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 
   const int nch = (N + 31) / 32;
   const long long total = (long long)B * nch;
-  for (long long t = (long long)blockIdx.x * 4 + wave; t < total; t += (long long)gridDim.x * 4) {
+  for (long long t = (long long)blockIdx.x * NW + wave; t < total; t += (long long)gridDim.x * NW) {
     const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
     const size_t col0 = (size_t)b * N;
     const float* sm = fresh_lds(vsm);
@@ -2863,18 +2912,56 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         }
         pm = row16_sum_f(pm);
         ps = row16_sum_f(ps);
+        float pu = 0.f;
+        if constexpr (FG) pu = row16_sum_f(__builtin_fmaf(gmq[1], K[rt][1][r], gmq[0] * K[rt][0][r]));
         if (c == 0) {
           rows[p] += pm;
           rows[64 + p] += ps;
+          if constexpr (FG) rows[192 + p] += pu;
         }
       }
-    // the clamp-masked gvar -> workspace: dL^{-1} = vm u^T + 2 (s^2 - 1) o L^{-1} G with
-    // u = sum gmean K_ZX, G = K_ZX diag(gvar) K_ZX^T (gpk_var_kgram_r_kernel), so neither
-    // dA nor K_ZX makes an HBM round trip
+    // dL^{-1} = vm u^T + 2 (s^2 - 1) o L^{-1} G with u = sum gmean K_ZX and
+    // G = K_ZX diag(gvar) K_ZX^T, so neither dA nor K_ZX makes an HBM round trip
+    if constexpr (FG) {
+      // G(rt, rp) += sum_points K_rt diag(gv) K_rp^T: each K tile transposed through the
+      // wave's scratch (points -> k), then sum_s mfma(K^T.reg[s], (gv K)^T.reg[s]) as in
+      // gpk_var_kgram_r_kernel (same acc layout); the tiles live in LDS between chunks
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int i = i0 + 16 * q + c;
-      if (i < N && g == 0) wsgv[col0 + i] = gvq[q];
+      for (int q = 0; q < 2; ++q) {
+        float aK[4][4], aW[4][4];
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = K[rt][q][r];
+          adj_lds_order();
+#pragma unroll
+          for (int s = 0; s < 4; ++s) aK[rt][s] = scr[((c & 3) * 16 + 4 * s + g) * 5 + (c >> 2)];
+          adj_lds_order();
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float gvp = __shfl(gvq[q], 4 * s + g, 64);   // gvar of point 16 q + 4 s + g
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt) aW[rt][s] = aK[rt][s] * gvp;
+        }
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int rp = 0; rp <= rt; ++rp) {
+            f32x4* gp = (f32x4*)(ga + 4 * ((rt * (rt + 1) / 2 + rp) * 64 + lane));
+            f32x4 acc = *gp;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) acc = mfma32(aK[rt][s], aW[rp][s], acc);
+            *gp = acc;
+          }
+      }
+    } else {
+      // the clamp-masked gvar -> workspace for gpk_var_kgram_r_kernel
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = i0 + 16 * q + c;
+        if (i < N && g == 0) wsgv[col0 + i] = gvq[q];
+      }
     }
     // dK = L^{-T} dA (fp64; L^{-T} upper: kb >= rt), then Q = dK o K_ZX (in K's registers)
 #pragma unroll
@@ -2950,11 +3037,11 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       for (int rt = 0; rt < 4; ++rt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = K[rt][q][r];
-        wave_lds_sync();
+        adj_lds_order();
         float aq[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) aq[s] = scr[((c & 3) * 16 + 4 * s + g) * 5 + (c >> 2)];
-        wave_lds_sync();   // the next tile overwrites scr
+        adj_lds_order();   // the next tile overwrites scr
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -3020,7 +3107,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     misc[2 * DQ + 1] = sumgv;
     misc[2 * DQ + 2] = sumgm;
   }
-  for (int wv2 = 0; wv2 < 4; ++wv2) {
+  for (int wv2 = 0; wv2 < NW; ++wv2) {
     lds_barrier();
     if (wave == wv2) {
 #pragma unroll
@@ -3036,7 +3123,8 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   }
   lds_barrier();
   const int P = M * D + 3 * M + 2 * D + 3;
-  float* po = wspart + (size_t)blockIdx.x * P;
+  float* po = wspart + (size_t)blockIdx.x * (P + (FG ? kGPart : 0));
+  if (FG && blockIdx.x == 0 && tid < D) cm_out[tid] = vsm[L::cm + tid];
   for (int e = tid; e < M * D; e += blockDim.x) {
     const int p = e / D, d = e - p * D;
     po[e] = qxr[p * DQ + d];
@@ -3044,10 +3132,10 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   const float* rw = vsm + L::rows;
   for (int m = tid; m < M; m += blockDim.x) {
     float a = 0.f, s = 0.f, qq = 0.f;
-    for (int u = 0; u < 4; ++u) {
-      a += rw[u * 192 + m];
-      s += rw[u * 192 + 64 + m];
-      qq += rw[u * 192 + 128 + m];
+    for (int u = 0; u < NW; ++u) {
+      a += rw[u * 256 + m];
+      s += rw[u * 256 + 64 + m];
+      qq += rw[u * 256 + 128 + m];
     }
     po[M * D + m] = qq;
     po[M * D + M + m] = a;
@@ -3056,7 +3144,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   const float* ms = vsm + L::misc;
   for (int d = tid; d < D; d += blockDim.x) {
     float v = 0.f, u = 0.f;
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NW; ++k) {
       v += ms[k * (2 * DQ + 3) + d];
       u += ms[k * (2 * DQ + 3) + DQ + d];
     }
@@ -3065,7 +3153,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   }
   if (tid == 0) {
     float a = 0.f, v = 0.f, u = 0.f;
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NW; ++k) {
       a += ms[k * (2 * DQ + 3) + 2 * DQ];
       v += ms[k * (2 * DQ + 3) + 2 * DQ + 1];
       u += ms[k * (2 * DQ + 3) + 2 * DQ + 2];
@@ -3073,6 +3161,24 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     po[M * D + 3 * M + D] = a;
     po[M * D + 3 * M + D + 1] = v;
     po[M * D + 3 * M + 2 * D + 2] = u;
+  }
+  if constexpr (FG) {
+    // K-Gram partial [G lower tiles (10 x 256, acc order) | u (64)], waves in a fixed order
+    const float* gw = vsm + L::gacc;
+    float* pg = po + P;
+    for (int e = tid; e < kGTiles * 256; e += blockDim.x) {
+      const int t2 = e >> 8, r = (e >> 6) & 3, ln = e & 63;
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) v += gw[k * (kGTiles * 256) + 4 * (t2 * 64 + ln) + r];
+      pg[e] = v;
+    }
+    for (int m = tid; m < 64; m += blockDim.x) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) v += rw[k * 256 + 192 + m];
+      pg[kGTiles * 256 + m] = v;
+    }
   }
 }
 
@@ -3087,9 +3193,6 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 // wave, fp64 across waves / workgroups). Partials per workgroup:
 //   [G lower tiles (10 x 256, acc order) | u (64)].
 // ---------------------------------------------------------------------------
-constexpr int kGTiles = 10;                  // lower 16 x 16 tiles of a 64 x 64 G
-constexpr int kGPart = kGTiles * 256 + 64;   // floats per workgroup partial
-
 template <int DQ>
 __global__ void __launch_bounds__(256, 2)
 gpk_var_kgram_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
@@ -3238,25 +3341,28 @@ gpk_var_kgram_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 // reduced totals (fp64). One workgroup: G (symmetric, from its lower tiles) in LDS, wave w
 // forms the 16-row block w of L^{-1} G on fp64 MFMA with its L^{-1} operands requested up
 // front (the triangular k-range: jb <= w).
-__global__ void __launch_bounds__(256)
-gpk_var_gdl_kernel(const double* __restrict__ gtot, const double* __restrict__ Linv,
-                   const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
-                   double* __restrict__ dLinv) {
-  __shared__ double Gs[64][65];
-  __shared__ double us[64];
+// (256 threads; Gs: 64 x 65 doubles, us: 64 doubles of LDS)
+GPK_DEVICE void var_gdl_block(const double* __restrict__ gtot, const double* __restrict__ Linv,
+                              const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
+                              double* __restrict__ dLinv, double (*Gs)[65], double* us) {
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = tid >> 6;
-  for (int e = tid; e < kGTiles * 256; e += 256) {   // acc order: tile, reg r, lane (c, g)
-    const int t2 = e >> 8, r = (e >> 6) & 3, ln = e & 63;
-    int rt = 0;
-    while ((rt + 1) * (rt + 2) / 2 <= t2) ++rt;
-    const int rp = t2 - rt * (rt + 1) / 2;
+  // the 10 tile elements of this thread requested together (acc order: tile, reg r, lane)
+  double gv[kGTiles];
+#pragma unroll
+  for (int t2 = 0; t2 < kGTiles; ++t2) gv[t2] = gtot[t2 * 256 + tid];
+  const double uv = gtot[kGTiles * 256 + (tid & 63)];
+#pragma unroll
+  for (int t2 = 0; t2 < kGTiles; ++t2) {
+    constexpr int kRt[kGTiles] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3};
+    const int rt = kRt[t2], rp = t2 - rt * (rt + 1) / 2;
+    const int r = tid >> 6, ln = tid & 63;
     const int row = 16 * rt + 4 * (ln >> 4) + r, col = 16 * rp + (ln & 15);   // f32 acc: row 4g + r
     if (rt == rp && row < col) continue;   // one writer per element: deterministic
-    Gs[row][col] = gtot[e];
-    Gs[col][row] = gtot[e];
+    Gs[row][col] = gv[t2];
+    Gs[col][row] = gv[t2];
   }
-  for (int e = tid; e < 64; e += 256) us[e] = gtot[kGTiles * 256 + e];
+  if (tid < 64) us[tid] = uv;
   // A operands L^{-1}[16 w + c][16 jb + 4 s + g] for jb <= w, requested before the barrier
   double la[4][4];
 #pragma unroll
@@ -3285,6 +3391,15 @@ gpk_var_gdl_kernel(const double* __restrict__ gtot, const double* __restrict__ L
       }
     }
   }
+}
+
+__global__ void __launch_bounds__(256)
+gpk_var_gdl_kernel(const double* __restrict__ gtot, const double* __restrict__ Linv,
+                   const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
+                   double* __restrict__ dLinv) {
+  __shared__ double Gs[64][65];
+  __shared__ double us[64];
+  var_gdl_block(gtot, Linv, vmean, vstd, M, dLinv, Gs, us);
 }
 
 // ---------------------------------------------------------------------------
@@ -3400,6 +3515,10 @@ struct AdjPlan {
 #define GPK_VAR_REG 1   // 0: A/B builds without the register-resident path
 #endif
 GPK_HOST_DEVICE_INLINE bool var_reg_path(int M, int D) { return GPK_VAR_REG && M <= 64 && D <= 32; }
+#ifndef GPK_VAR_FUSEG
+#define GPK_VAR_FUSEG 1   // 0: A/B builds with the separate gpk_var_kgram_r_kernel (4-wave adjoint)
+#endif
+constexpr int kAdjRWaves = GPK_VAR_FUSEG ? 8 : 4;   // waves per register-path adjoint workgroup
 
 AdjPlan adj_plan_common(AdjPlan p, int B, int N, int M, int D);
 
@@ -3425,18 +3544,23 @@ AdjPlan adj_plan(int B, int N, int M, int D) {
     }
   }
   if (var_reg_path(M, D)) {
-    // workspace: masked gvar (BN) | K-Gram partials (nwg x kGPart) | their fp64 totals
+    // workspace: masked gvar (BN) | K-Gram partials (nwg x kGPart) | adjoint partials | their
+    // fp64 totals | K-Gram totals. With the K-Gram folded in (GPK_VAR_FUSEG): the centre (64) |
+    // - | rows of [adjoint | K-Gram] partials | their fp64 totals (the K-Gram totals at + P) | -
     const long long nch = (long long)B * ((N + 31) / 32);
     p.nchunks = (int)nch;
-    p.nwg = (int)((nch + 3) / 4 < 512 ? (nch + 3) / 4 : 512);
+    // one workgroup per CU (8 waves, K-Gram folded in) or two (4 waves)
+    const long long nwg_max = 2048 / kAdjRWaves;
+    p.nwg = (int)((nch + kAdjRWaves - 1) / kAdjRWaves < nwg_max ? (nch + kAdjRWaves - 1) / kAdjRWaves : nwg_max);
     p = adj_plan_common(p, B, N, M, D);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o = 0;
-    p.off_dA = o; o = al(o + (size_t)p.BN * sizeof(float));
-    p.off_K = o; o = al(o + (size_t)p.nwg * kGPart * sizeof(float));
-    p.off_part = o; o = al(o + (size_t)p.nwg * p.P * sizeof(float));
-    p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
-    p.off_dl = o; o = al(o + (size_t)kGPart * sizeof(double));
+    constexpr bool fg = GPK_VAR_FUSEG != 0;
+    p.off_dA = o; o = al(o + (fg ? 64 : (size_t)p.BN) * sizeof(float));
+    p.off_K = o; o = al(o + (fg ? 0 : (size_t)p.nwg * kGPart) * sizeof(float));
+    p.off_part = o; o = al(o + (size_t)p.nwg * (p.P + (fg ? kGPart : 0)) * sizeof(float));
+    p.off_tot = o; o = al(o + (size_t)(p.P + (fg ? kGPart : 0)) * sizeof(double));
+    p.off_dl = o; o = al(o + (fg ? 0 : (size_t)kGPart) * sizeof(double));
     p.off_fin = o; o = al(o + kFinWsBytes);
     p.total = o;
     return p;
@@ -3507,22 +3631,35 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
   float* wspart = (float*)(ws + p.off_part);
   if (var_reg_path(a.M, a.D)) {
     constexpr int RQ = DQ <= 16 ? 16 : 32;
-    float* wsgv = wsdA;
+    float* wsgv = wsdA;   // FG: the centre cm (D floats)
     float* gpart = wsK;
-    double* gtot = (double*)(ws + p.off_dl);
     double* tot = (double*)(ws + p.off_tot);
-    const size_t lds = (size_t)RegLds<RQ>::adj_total * sizeof(float);
-    set_lds_once<gpk_var_adj_r_kernel<RQ>>();
-    hipLaunchKernelGGL((gpk_var_adj_r_kernel<RQ>), dim3(p.nwg), dim3(256), lds, stream, a.X, a.Z,
-                       a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.B, a.N, a.M, a.D, p.BN,
-                       wsgv, wspart, a.dX);
+    constexpr int NW = kAdjRWaves;
+    constexpr bool FG = GPK_VAR_FUSEG != 0;
+    double* gtot = FG ? tot + p.P : (double*)(ws + p.off_dl);
+    static_assert(RegLds<RQ, NW, FG>::adj_total * sizeof(float) <= 160 * 1024, "LDS per workgroup");
+    const size_t lds = (size_t)RegLds<RQ, NW, FG>::adj_total * sizeof(float);
+    set_lds_once<gpk_var_adj_r_kernel<RQ, NW, FG>>();
+    hipLaunchKernelGGL((gpk_var_adj_r_kernel<RQ, NW, FG>), dim3(p.nwg), dim3(64 * NW), lds, stream, a.X,
+                       a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.B, a.N, a.M, a.D, p.BN,
+                       wsgv, wspart, wsgv, a.dX);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    set_lds_once<gpk_var_kgram_r_kernel<RQ>>();
-    hipLaunchKernelGGL((gpk_var_kgram_r_kernel<RQ>), dim3(p.nwg), dim3(256),
-                       (size_t)RegLds<RQ>::fwd_total * sizeof(float), stream, a.X, a.Z, a.vmean, a.vstd,
-                       a.hyp, a.gmean, wsgv, a.B, a.N, a.M, a.D, gpart);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    if constexpr (FG) {
+      // one fixed-order reduction of the [adjoint | K-Gram] rows; dL^{-1} in the output launch
+      const int PR = p.P + kGPart;
+      hipLaunchKernelGGL(gpk_var_red_kernel, dim3((PR + 31) / 32), dim3(256), 0, stream, wspart, p.nwg, PR,
+                         tot, nullptr, 0, 0, 0, nullptr);
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+      const VarGdlArgs gd{gtot, a.Linv, a.vmean, a.vstd, a.dLinv};
+      return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream, wsgv, &gd);
+    } else {
+      set_lds_once<gpk_var_kgram_r_kernel<RQ>>();
+      hipLaunchKernelGGL((gpk_var_kgram_r_kernel<RQ>), dim3(p.nwg), dim3(256),
+                         (size_t)RegLds<RQ>::fwd_total * sizeof(float), stream, a.X, a.Z, a.vmean, a.vstd,
+                         a.hyp, a.gmean, wsgv, a.B, a.N, a.M, a.D, gpart);
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    }
     // fixed-order sums: K-Gram partials -> gtot, adjoint partials -> tot (section (a) only)
     hipLaunchKernelGGL(gpk_var_red_kernel, dim3((kGPart + 31) / 32), dim3(256), 0, stream, gpart, p.nwg,
                        kGPart, gtot, nullptr, 0, 0, 0, nullptr);
@@ -3567,13 +3704,21 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
 }
 
 int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const double* tot, int M, int D,
-                   float* dZ, float* dpar, void* ws, hipStream_t stream, const float* cm_in) {
+                   float* dZ, float* dpar, void* ws, hipStream_t stream, const float* cm_in,
+                   const VarGdlArgs* gd) {
   const int nblk = (M + kFinRows - 1) / kFinRows;
   double* dlp = (double*)ws;
   float* cm = (float*)(dlp + (size_t)nblk * D);
   set_lds_once<gpk_var_fin_kernel, 64 * 1024>();   // + ~3.3 KB static
-  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(nblk), dim3(256), (size_t)M * D * sizeof(float), stream, Z, hyp,
-                     tot, M, D, dZ, dlp, cm, cm_in);
+  size_t lds = (size_t)M * D * sizeof(float);
+  VarGdlArgs g{};
+  if (gd != nullptr) {
+    g = *gd;
+    const size_t gl = (64 * 65 + 64) * sizeof(double);
+    if (lds < gl) lds = gl;
+  }
+  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(nblk + (gd != nullptr ? 1 : 0)), dim3(256), lds, stream, Z, hyp,
+                     tot, M, D, dZ, dlp, cm, cm_in, g);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(gpk_var_fin2_kernel, dim3(1), dim3(256), 0, stream, vstd, hyp, tot, M, D, nblk, dlp, cm,
