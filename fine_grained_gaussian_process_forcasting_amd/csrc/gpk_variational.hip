@@ -2379,25 +2379,25 @@ gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __r
   }
 }
 
-// Outputs from the reduced totals, in two launches:
-//   gpk_var_fin_kernel (ceil(M / 16) workgroups, 16 inducing points each; every workgroup stages
-//     all of Z / l for the column means -- col_means, the same fp32 sums as stage_inducing, so
-//     the identical centre -- with its global reads in flight together):
-//       dZ_p = (QX_p - zs_p q_p) / l
-//       dlp[blk][d] = sum_{p in blk} (q_p zs_pd^2 - 2 zs_pd QX_pd)      (fixed order)
-//   gpk_var_fin2_kernel (one workgroup):
-//       dl_d = (sum_blk dlp[blk][d] + sum_i r_i xs_id^2) / l_d
+// Outputs from the reduced totals, ONE launch (gpk_var_fin_kernel):
+//   blocks 0 .. nblk-1 (16 inducing points each):  dZ_p = (QX_p - zs_p q_p) / l
+//   block nblk (the totals block, all M rows):
+//       dl_d = (sum_p (q_p zs_pd^2 - 2 zs_pd QX_pd) + sum_i r_i xs_id^2) / l_d
 //       ds2 = sum Q / s2 + sum gvar;    dvmean = sum gmean A;   dvstd = 2 s sum gvar A^2
 //       dw_d = l_d (sum_i gmean_i xs_id + cm_d sum_i gmean_i);   db0 = sum_i gmean_i
-// dpar = [dvmean (M) | dvstd (M) | ds2 | dl (D) | dw (D) | db0]  (cm: written by block 0)
+//   block nblk + 1 (gd.gtot != nullptr, register path): dL^{-1} from the K-Gram totals
+// dpar = [dvmean (M) | dvstd (M) | ds2 | dl (D) | dw (D) | db0]. zs = Z / l - cm with the centre
+// cm from the adjoint kernel (cm_in: its stage_inducing) or, without it, recomputed by
+// col_means -- the same fixed-order fp32 sums, so the identical centre. No block depends on
+// another: the round-4 second launch (block partials of dl) is gone.
 constexpr int kFinRows = 16;
-constexpr size_t kFinWsBytes = (256 / kFinRows) * 64 * sizeof(double) + 64 * sizeof(float);
+
 GPK_DEVICE void var_gdl_block(const double* __restrict__ gtot, const double* __restrict__ Linv,
                               const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
                               double* __restrict__ dLinv, double (*Gs)[65], double* us);
 
-// gd != nullptr (register path, M <= 64): one extra workgroup forms dL^{-1} from the K-Gram
-// totals (var_gdl_block) beside the output blocks instead of in a launch of its own
+// gd.gtot != nullptr (register path, M <= 64): one extra workgroup forms dL^{-1} from the
+// K-Gram totals (var_gdl_block) beside the output blocks instead of in a launch of its own
 struct VarGdlArgs {
   const double* gtot;
   const double* Linv;
@@ -2407,55 +2407,66 @@ struct VarGdlArgs {
 };
 
 __global__ void __launch_bounds__(256)
-gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ hyp,
-                   const double* __restrict__ tot, int M, int D, float* __restrict__ dZ,
-                   double* __restrict__ dlp, float* __restrict__ cm_out, const float* __restrict__ cm_in,
+gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
+                   const float* __restrict__ hyp, const double* __restrict__ tot, int M, int D,
+                   float* __restrict__ dZ, float* __restrict__ dpar, const float* __restrict__ cm_in,
                    VarGdlArgs gd) {
   extern __shared__ __attribute__((aligned(16))) float fzs[];   // M x D zs (centred Z / l)
   __shared__ double red[256];
   __shared__ float cmf[64];
   __shared__ float cms[kCmParts * 64];
   const int tid = threadIdx.x;
-  if (gd.gtot != nullptr && blockIdx.x == gridDim.x - 1) {
+  const int nblk = (M + kFinRows - 1) / kFinRows;
+  if (gd.gtot != nullptr && (int)blockIdx.x == nblk + 1) {
     double* gl = (double*)fzs;
     var_gdl_block(gd.gtot, gd.Linv, gd.vmean, gd.vstd, M, gd.dLinv, (double(*)[65])gl, gl + 64 * 65);
     return;
   }
+  const bool totals = (int)blockIdx.x == nblk;
   const float* ls = hyp + 4 + D;
-  const int p0 = blockIdx.x * kFinRows;
-  const int np = M - p0 < kFinRows ? M - p0 : kFinRows;
+  const int p0 = totals ? 0 : blockIdx.x * kFinRows;
+  const int np = totals ? M : (M - p0 < kFinRows ? M - p0 : kFinRows);
   if (cm_in != nullptr) {
-    // the centre from the adjoint kernel (its stage_inducing: the same fixed-order sums), so
-    // only this block's rows of Z are staged
+    // the centre from the adjoint kernel, so only this block's rows of Z are staged
     if (tid < D) cmf[tid] = cm_in[tid];
-    for (int e = tid; e < np * D; e += 256) {
-      const int d = e % D;
-      fzs[p0 * D + e] = Z[(size_t)p0 * D + e] / ls[d] - cm_in[d];
+    for (int base = 0; base < np * D; base += 8 * 256) {
+      float zv[8], lv[8], cv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = base + 256 * u + tid, ec = e < np * D ? e : 0, d = ec % D;
+        zv[u] = Z[(size_t)p0 * D + ec];
+        lv[u] = ls[d];
+        cv[u] = cm_in[d];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = base + 256 * u + tid;
+        if (e < np * D) fzs[p0 * D + e] = zv[u] / lv[u] - cv[u];
+      }
     }
   } else {
-  for (int base = 0; base < M * D; base += 32 * 256) {
-    float zv[32], lv[32];
+    for (int base = 0; base < M * D; base += 32 * 256) {
+      float zv[32], lv[32];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      const int e = base + 256 * u + tid, ec = e < M * D ? e : 0;
-      zv[u] = Z[ec];
-      lv[u] = ls[ec % D];
-    }
+      for (int u = 0; u < 32; ++u) {
+        const int e = base + 256 * u + tid, ec = e < M * D ? e : 0;
+        zv[u] = Z[ec];
+        lv[u] = ls[ec % D];
+      }
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      const int e = base + 256 * u + tid;
-      if (e < M * D) fzs[e] = zv[u] / lv[u];
+      for (int u = 0; u < 32; ++u) {
+        const int e = base + 256 * u + tid;
+        if (e < M * D) fzs[e] = zv[u] / lv[u];
+      }
     }
+    lds_barrier();
+    col_means(fzs, M, D, D, D, cms, cmf);   // the same fp32 sums as stage_inducing: the identical centre
+    for (int e = tid; e < np * D; e += 256) fzs[p0 * D + e] -= cmf[e % D];
   }
   lds_barrier();
-  col_means(fzs, M, D, D, D, cms, cmf);   // the same fp32 sums as stage_inducing: the identical centre
-  for (int e = tid; e < np * D; e += 256) fzs[p0 * D + e] -= cmf[e % D];
-  }
-  lds_barrier();
-  if (blockIdx.x == 0 && tid < D) cm_out[tid] = cmf[tid];
   const double* QX = tot;
   const double* q = tot + (size_t)M * D;
-  {
+  if (!totals) {
     const int e = tid;   // np * D <= 16 * 64 = 1024: up to 4 per thread, loads together
     double xv[4], qv[4];
     float lv[4];
@@ -2476,58 +2487,43 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ hyp,
         dZ[(size_t)p * D + d] = (float)((xv[u] - zsv * qv[u]) / (double)lv[u]);
       }
     }
+    return;
   }
-  // per-d partial over this block's rows: threads (d, k), k = tid / D, rows p0 + k, p0 + k + nk..
+  // ---- the totals block: dl over all M rows, threads (d, k), k = tid / D, rows k, k + nk, ..
+  // (16 rows' loads in flight per thread, fixed order)
+  const double* dvm = tot + (size_t)M * D + M;
+  const double* dsm = dvm + M;
+  const double* rx2 = dsm + M;
+  const double* gx = rx2 + D + 2;
   const int nk = 256 / D;
   double acc = 0.0;
   if (tid < nk * D) {
     const int d = tid % D, k = tid / D;
-    double qv[kFinRows], xv[kFinRows];
+    for (int base = k; base < M; base += 16 * nk) {
+      double qv[16], xv[16];
 #pragma unroll
-    for (int u = 0; u < kFinRows; ++u) {
-      const int pl = k + nk * u, p = p0 + (pl < np ? pl : 0);
-      qv[u] = q[p];
-      xv[u] = QX[(size_t)p * D + d];
-    }
+      for (int u = 0; u < 16; ++u) {
+        const int pl = base + nk * u, pc = pl < M ? pl : 0;
+        qv[u] = q[pc];
+        xv[u] = QX[(size_t)pc * D + d];
+      }
 #pragma unroll
-    for (int u = 0; u < kFinRows; ++u) {
-      const int pl = k + nk * u;
-      if (pl < np) {
-        const double zsv = (double)fzs[(p0 + pl) * D + d];
-        acc += qv[u] * zsv * zsv - 2.0 * zsv * xv[u];
+      for (int u = 0; u < 16; ++u) {
+        const int pl = base + nk * u;
+        if (pl < M) {
+          const double zsv = (double)fzs[pl * D + d];
+          acc += qv[u] * zsv * zsv - 2.0 * zsv * xv[u];
+        }
       }
     }
   }
   red[tid] = acc;
   lds_barrier();
-  if (tid < D) {
-    double v = 0.0;
-    for (int k = 0; k < nk; ++k) v += red[k * D + tid];
-    dlp[(size_t)blockIdx.x * D + tid] = v;
-  }
-}
-
-__global__ void __launch_bounds__(256)
-gpk_var_fin2_kernel(const float* __restrict__ vstd, const float* __restrict__ hyp,
-                    const double* __restrict__ tot, int M, int D, int nblk,
-                    const double* __restrict__ dlp, const float* __restrict__ cmf, float* __restrict__ dpar) {
-  const int tid = threadIdx.x;
   const float s2 = hyp[0];
-  const float* ls = hyp + 4 + D;
-  const double* dvm = tot + (size_t)M * D + M;
-  const double* dsm = dvm + M;
-  const double* rx2 = dsm + M;
-  const double sumQ = rx2[D], sumgv = rx2[D + 1];
-  const double* gx = rx2 + D + 2;
-  const double sumgm = gx[D];
   if (tid < D) {
-    // the <= 16 block partials: loads issued together (clamped, fixed count), fixed-order sum
-    double pv[256 / kFinRows];
-#pragma unroll
-    for (int k = 0; k < 256 / kFinRows; ++k) pv[k] = dlp[(size_t)(k < nblk ? k : 0) * D + tid];
     double v = rx2[tid];
-#pragma unroll
-    for (int k = 0; k < 256 / kFinRows; ++k) v += k < nblk ? pv[k] : 0.0;
+    for (int k = 0; k < nk; ++k) v += red[k * D + tid];
+    const double sumgm = gx[D];
     dpar[2 * M + 1 + tid] = (float)(v / (double)ls[tid]);
     dpar[2 * M + 1 + D + tid] = (float)((double)ls[tid] * (gx[tid] + (double)cmf[tid] * sumgm));
   }
@@ -2536,6 +2532,7 @@ gpk_var_fin2_kernel(const float* __restrict__ vstd, const float* __restrict__ hy
     dpar[M + m] = (float)(2.0 * (double)vstd[m] * dsm[m]);
   }
   if (tid == 0) {
+    const double sumQ = rx2[D], sumgv = rx2[D + 1], sumgm = gx[D];
     dpar[2 * M] = (float)(sumQ / (double)s2 + sumgv);
     dpar[2 * M + 1 + 2 * D] = (float)sumgm;
   }
@@ -2543,7 +2540,7 @@ gpk_var_fin2_kernel(const float* __restrict__ vstd, const float* __restrict__ hy
 
 // the two output launches (ws: nblk x D doubles of dl partials, then D floats of the centre)
 int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const double* tot, int M, int D,
-                   float* dZ, float* dpar, void* ws, hipStream_t stream, const float* cm_in = nullptr,
+                   float* dZ, float* dpar, hipStream_t stream, const float* cm_in = nullptr,
                    const VarGdlArgs* gd = nullptr);
 
 // ---------------------------------------------------------------------------
@@ -3505,7 +3502,7 @@ int launch_var_fwd_l(const GpkVarArgs& a, int* flags, hipStream_t stream) {
 struct AdjPlan {
   int nchunks, nwg, P, ntiles, nsplit;
   long long BN, cols_per_split;
-  size_t off_dA, off_K, off_part, off_tot, off_dl, off_fin, total;  // byte offsets
+  size_t off_dA, off_K, off_part, off_tot, off_dl, total;  // byte offsets
   size_t fin_lds;
 };
 
@@ -3561,7 +3558,6 @@ AdjPlan adj_plan(int B, int N, int M, int D) {
     p.off_part = o; o = al(o + (size_t)p.nwg * (p.P + (fg ? kGPart : 0)) * sizeof(float));
     p.off_tot = o; o = al(o + (size_t)(p.P + (fg ? kGPart : 0)) * sizeof(double));
     p.off_dl = o; o = al(o + (fg ? 0 : (size_t)kGPart) * sizeof(double));
-    p.off_fin = o; o = al(o + kFinWsBytes);
     p.total = o;
     return p;
   }
@@ -3590,7 +3586,6 @@ AdjPlan adj_plan_common(AdjPlan p, int B, int N, int M, int D) {
   p.off_part = o; o = al(o + (size_t)p.nwg * p.P * sizeof(float));
   p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
   p.off_dl = o; o = al(o + (size_t)p.nsplit * p.ntiles * 4096 * sizeof(double));
-  p.off_fin = o; o = al(o + kFinWsBytes);
   p.total = o;
   return p;
 }
@@ -3652,7 +3647,7 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
                          tot, nullptr, 0, 0, 0, nullptr);
       if ((e = hipGetLastError()) != hipSuccess) return (int)e;
       const VarGdlArgs gd{gtot, a.Linv, a.vmean, a.vstd, a.dLinv};
-      return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream, wsgv, &gd);
+      return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream, wsgv, &gd);
     } else {
       set_lds_once<gpk_var_kgram_r_kernel<RQ>>();
       hipLaunchKernelGGL((gpk_var_kgram_r_kernel<RQ>), dim3(p.nwg), dim3(256),
@@ -3670,7 +3665,7 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(gpk_var_gdl_kernel, dim3(1), dim3(256), 0, stream, gtot, a.Linv, a.vmean, a.vstd,
                        a.M, a.dLinv);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream);
+    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream);
   }
   if constexpr (var_adj_lreg_fits<MB, DQ>()) {
     if (GPK_VAR_LREG && a.M > 64 && (long long)a.M * p.BN * 4 < (1LL << 31)) {
@@ -3704,11 +3699,9 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
 }
 
 int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const double* tot, int M, int D,
-                   float* dZ, float* dpar, void* ws, hipStream_t stream, const float* cm_in,
+                   float* dZ, float* dpar, hipStream_t stream, const float* cm_in,
                    const VarGdlArgs* gd) {
   const int nblk = (M + kFinRows - 1) / kFinRows;
-  double* dlp = (double*)ws;
-  float* cm = (float*)(dlp + (size_t)nblk * D);
   set_lds_once<gpk_var_fin_kernel, 64 * 1024>();   // + ~3.3 KB static
   size_t lds = (size_t)M * D * sizeof(float);
   VarGdlArgs g{};
@@ -3717,13 +3710,9 @@ int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const do
     const size_t gl = (64 * 65 + 64) * sizeof(double);
     if (lds < gl) lds = gl;
   }
-  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(nblk + (gd != nullptr ? 1 : 0)), dim3(256), lds, stream, Z, hyp,
-                     tot, M, D, dZ, dlp, cm, cm_in, g);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(gpk_var_fin2_kernel, dim3(1), dim3(256), 0, stream, vstd, hyp, tot, M, D, nblk, dlp, cm,
-                     dpar);
-  e = hipGetLastError();
+  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(nblk + 1 + (gd != nullptr ? 1 : 0)), dim3(256), lds, stream, Z,
+                     vstd, hyp, tot, M, D, dZ, dpar, cm_in, g);
+  const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
 
@@ -3744,7 +3733,7 @@ int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t st
                      wspart, p.nwg, p.P, tot, dl, p.nsplit, p.ntiles, a.M, a.dLinv);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream);
+  return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream);
 }
 
 // ---- the saved-state adjoint (M > 64): workspace G' partials | adjoint partials | their fp64 totals
@@ -3752,7 +3741,7 @@ int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t st
 struct AdjSavedPlan {
   int nchunks, nwg, nwg_g, P, PG;
   long long BN;
-  size_t off_gpart, off_part, off_tot, off_gtot, off_fin, off_cm, total, fin_lds;
+  size_t off_gpart, off_part, off_tot, off_gtot, off_cm, total, fin_lds;
 };
 
 template <int MB, int DQ>
@@ -3773,7 +3762,6 @@ AdjSavedPlan adj_saved_plan(int B, int N, int M, int D) {
   p.off_part = o; o = al(o + (size_t)p.nwg * p.P * sizeof(float));
   p.off_tot = o; o = al(o + (size_t)p.P * sizeof(double));
   p.off_gtot = o; o = al(o + (size_t)p.PG * sizeof(double));
-  p.off_fin = o; o = al(o + kFinWsBytes);
   p.off_cm = o; o = al(o + 64 * sizeof(float));
   p.total = o;
   return p;
@@ -3810,7 +3798,7 @@ int launch_var_adj_saved(const GpkVarAdjArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(gpk_var_gdl_l_kernel, dim3((unsigned)(((long long)a.M * a.M + 255) / 256)), dim3(256), 0,
                        stream, gtot, a.vmean, a.vstd, a.M, MB, a.dLinv);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, ws + p.off_fin, stream,
+    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream,
                           (const float*)(ws + p.off_cm));
   } else {
     return -13;
