@@ -57,6 +57,14 @@ GPK_DEVICE float row16_sum_f(float v) {
   return v;
 }
 
+// Add v into an LDS accumulator that only the calling wave updates, without a round trip: a
+// no-return LDS add (no wait, where `*p += v` costs a read, a full LDS-latency wait and a
+// write). One wave's LDS operations execute in issue order, so the adds land in program
+// order: the sums stay deterministic.
+GPK_DEVICE void lds_acc(float* p, float v) {
+  (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 // Per-chunk LDS base the compiler must treat as new on every iteration: the staged
 // operands (L^{-1}, zs, norms) and their per-lane addresses would otherwise be hoisted out of the chunk loop as
 // loop-invariant loads and pinned in (hundreds of) registers.
@@ -1841,8 +1849,8 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
           const float a = row16_sum_f(pm[r]), q = row16_sum_f(ps[r]);
           if (c == 0) {
             const int p = 16 * rt + g + 4 * r;
-            rows[p] += a;
-            rows[G::MP + p] += q;
+            lds_acc(rows + p, a);
+            lds_acc(rows + G::MP + p, q);
           }
         }
       }
@@ -1888,7 +1896,7 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = row16_sum_f(Qt[h][0][r] + Qt[h][1][r]);
-        if (c == 0) qrow[16 * rt + g + 4 * r] += v;
+        if (c == 0) lds_acc(qrow + 16 * rt + g + 4 * r, v);
       }
     }
 #pragma unroll
@@ -2883,8 +2891,9 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       vp += __shfl_xor(vp, 32, 64);
       const int i = i0 + 16 * q + c;
       const bool ok = i < N;
-      gmq[q] = ok ? gmean[col0 + i] : 0.f;
-      gvq[q] = ok ? gvar[col0 + i] : 0.f;
+      const float gml = gmean[col0 + (ok ? i : 0)], gvl = gvar[col0 + (ok ? i : 0)];   // clamped
+      gmq[q] = ok ? gml : 0.f;
+      gvq[q] = ok ? gvl : 0.f;
       if (s2 + jit + vp < 1e-6f) gvq[q] = 0.f;   // clamp_min(1e-6): gradient masked
       if (g == 0) {
         sumgv += gvq[q];
@@ -2912,9 +2921,9 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         float pu = 0.f;
         if constexpr (FG) pu = row16_sum_f(__builtin_fmaf(gmq[1], K[rt][1][r], gmq[0] * K[rt][0][r]));
         if (c == 0) {
-          rows[p] += pm;
-          rows[64 + p] += ps;
-          if constexpr (FG) rows[192 + p] += pu;
+          lds_acc(rows + p, pm);
+          lds_acc(rows + 64 + p, ps);
+          if constexpr (FG) lds_acc(rows + 192 + p, pu);
         }
       }
     // dL^{-1} = vm u^T + 2 (s^2 - 1) o L^{-1} G with u = sum gmean K_ZX and
@@ -2994,7 +3003,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = row16_sum_f(K[rt][0][r] + K[rt][1][r]);
-        if (c == 0) rows[128 + 16 * rt + g + 4 * r] += v;
+        if (c == 0) lds_acc(rows + 128 + 16 * rt + g + 4 * r, v);
       }
     // (Q^T zs)_i: f32 MFMA with k = p (rows g + 4r of each row tile)
     f32x4 xz[2][NDT];
@@ -3057,6 +3066,8 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
           const int i = i0 + 16 * q + 4 * g + r, d = 16 * dt + c;
           xo[q][r][dt] = X[(i < N && d < D) ? (col0 + i) * D + d : 0];
         }
+    // (branch-free but for the stores: a load whose only use sits under the point / dim
+    // guard is sunk into it by the compiler and waited for one point at a time)
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -3065,17 +3076,15 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         const float rr = __shfl(rq[q], pc, 64);
         const float gm = __shfl(gmq[q], pc, 64);
         const int i = i0 + 16 * q + pc;
-        if (i < N) {
 #pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) {
-            const int d = 16 * dt + c;
-            if (d < D) {
-              const float xv = xo[q][r][dt] * ilc[dt] - cmc[dt];
-              dX[(col0 + i) * D + d] = (xz[q][dt][r] - xv * rr) * ilc[dt] + gm * wc[dt];
-              rx2[dt] = __builtin_fmaf(rr * xv, xv, rx2[dt]);
-              gx[dt] = __builtin_fmaf(gm, xv, gx[dt]);
-            }
-          }
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int d = 16 * dt + c;
+          const bool ok = i < N && d < D;
+          const float xv = ok ? xo[q][r][dt] * ilc[dt] - cmc[dt] : 0.f;
+          const float dxv = (xz[q][dt][r] - xv * rr) * ilc[dt] + gm * wc[dt];
+          if (ok) dX[(col0 + i) * D + d] = dxv;
+          rx2[dt] = __builtin_fmaf(rr * xv, xv, rx2[dt]);
+          gx[dt] = __builtin_fmaf(gm, xv, gx[dt]);
         }
       }
   }
