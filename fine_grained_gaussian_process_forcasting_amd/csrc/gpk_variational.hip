@@ -2816,6 +2816,19 @@ GPK_DEVICE void adj_lds_order() {
 #endif
 }
 
+#ifndef GPK_ADJR_STAMPS
+#define GPK_ADJR_STAMPS 0   // dev builds: per-phase s_memtime cycle totals per wave (gpk_dev_adjr_stamps)
+#endif
+#if GPK_ADJR_STAMPS
+__device__ unsigned g_adjr_st[4096 * 16];
+extern "C" int gpk_dev_adjr_stamps(unsigned* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_adjr_st), (size_t)n * sizeof(unsigned), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
+#ifndef GPK_ADJR_SKIP
+#define GPK_ADJR_SKIP 0   // timing-only ablations (wrong results): 1 G, 2 dK, 4 Q^T zs, 8 QX, 16 dX, 64 A
+#endif
 template <int DQ, int NW, bool FG>
 __global__ void __launch_bounds__(64 * NW, 8 / NW)
 gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
@@ -2861,7 +2874,21 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 
   const int nch = (N + 31) / 32;
   const long long total = (long long)B * nch;
+#if GPK_ADJR_STAMPS
+  unsigned long long st_acc[10] = {}, st_last = __builtin_amdgcn_s_memtime();
+#define GPK_ADJR_ST(k)                                          \
+  {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += _n - st_last;                                  \
+    st_last = _n;                                               \
+    __builtin_amdgcn_sched_barrier(0);                          \
+  }
+#else
+#define GPK_ADJR_ST(k)
+#endif
   for (long long t = (long long)blockIdx.x * NW + wave; t < total; t += (long long)gridDim.x * NW) {
+    GPK_ADJR_ST(0)
     const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
     const size_t col0 = (size_t)b * N;
     const float* sm = fresh_lds(vsm);
@@ -2873,8 +2900,17 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     load_points<DQ, false>(X, N, D, b, i0, il, cmv, wv, P);
     f32x4 K[4][2];
     build_k_reg<DQ>(sm, P, M, N, i0, s2, K);
+    GPK_ADJR_ST(1)
     f32x4 A[4][2];
-    linv_times_k<DQ>(sm, K, A);
+    if (GPK_ADJR_SKIP & 64) {
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) A[rt][q] = K[rt][q];
+    } else {
+      linv_times_k<DQ>(sm, K, A);
+    }
+    GPK_ADJR_ST(2)
     // variance -> clamp mask; point gradients
     float gmq[2], gvq[2];
 #pragma unroll
@@ -2926,9 +2962,10 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
           if constexpr (FG) lds_acc(rows + 192 + p, pu);
         }
       }
+    GPK_ADJR_ST(3)
     // dL^{-1} = vm u^T + 2 (s^2 - 1) o L^{-1} G with u = sum gmean K_ZX and
     // G = K_ZX diag(gvar) K_ZX^T, so neither dA nor K_ZX makes an HBM round trip
-    if constexpr (FG) {
+    if constexpr (FG && !(GPK_ADJR_SKIP & 1)) {
       // G(rt, rp) += sum_points K_rt diag(gv) K_rp^T: each K tile transposed through the
       // wave's scratch (points -> k), then sum_s mfma(K^T.reg[s], (gv K)^T.reg[s]) as in
       // gpk_var_kgram_r_kernel (same acc layout); the tiles live in LDS between chunks
@@ -2961,7 +2998,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
             *gp = acc;
           }
       }
-    } else {
+    } else if constexpr (!FG) {
       // the clamp-masked gvar -> workspace for gpk_var_kgram_r_kernel
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -2969,9 +3006,10 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         if (i < N && g == 0) wsgv[col0 + i] = gvq[q];
       }
     }
+    GPK_ADJR_ST(4)
     // dK = L^{-T} dA (fp64; L^{-T} upper: kb >= rt), then Q = dK o K_ZX (in K's registers)
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt) {
+    for (int rt = 0; rt < 4 && !(GPK_ADJR_SKIP & 2); ++rt) {
       f64x4 acc[2] = {f64x4{0.0, 0.0, 0.0, 0.0}, f64x4{0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
       for (int kb = rt; kb < 4; ++kb)
@@ -2986,6 +3024,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 #pragma unroll
         for (int r = 0; r < 4; ++r) K[rt][q][r] = (float)acc[q][r] * K[rt][q][r];
     }
+    GPK_ADJR_ST(5)
     // r_i = sum_p Q_pi (every lane c of a column), q_p row partials, sum Q
     float rq[2];
 #pragma unroll
@@ -3005,6 +3044,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         const float v = row16_sum_f(K[rt][0][r] + K[rt][1][r]);
         if (c == 0) lds_acc(rows + 128 + 16 * rt + g + 4 * r, v);
       }
+    GPK_ADJR_ST(6)
     // (Q^T zs)_i: f32 MFMA with k = p (rows g + 4r of each row tile)
     f32x4 xz[2][NDT];
 #pragma unroll
@@ -3019,11 +3059,13 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         for (int dt = 0; dt < NDT; ++dt) {
           const float zb = zs[(16 * rt + g + 4 * r) * L::ZS + 16 * dt + c];
 #pragma unroll
-          for (int q = 0; q < 2; ++q) xz[q][dt] = mfma32(K[rt][q][r], zb, xz[q][dt]);
+          for (int q = 0; q < 2; ++q)
+            if (!(GPK_ADJR_SKIP & 4)) xz[q][dt] = mfma32(K[rt][q][r], zb, xz[q][dt]);
         }
+    GPK_ADJR_ST(7)
     // QX_p += sum_i Q_pi xs_i: Q tiles transposed through LDS (k = point 4s + g)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < 2 && !(GPK_ADJR_SKIP & 8); ++q) {
       float xb2[4][NDT];
 #pragma unroll
       for (int s = 0; s < 4; ++s)     // unconditional (clamped) loads: all in flight together
@@ -3054,6 +3096,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
           for (int s = 0; s < 4; ++s) qx[rt][dt] = mfma32(aq[s], xb2[s][dt], qx[rt][dt]);
       }
     }
+    GPK_ADJR_ST(8)
     // dX_i = ((Q^T zs)_i - xs_i r_i) / l + gmean_i w; sum_i r_i xs_i^2, sum_i gmean_i xs_i
     // (the point values are requested up front, unconditionally: clamped addresses)
     float xo[2][4][NDT];
@@ -3069,7 +3112,7 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
     // (branch-free but for the stores: a load whose only use sits under the point / dim
     // guard is sunk into it by the compiler and waited for one point at a time)
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2 && !(GPK_ADJR_SKIP & 16); ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int pc = 4 * g + r;                  // point (within the tile) of register r
@@ -3087,7 +3130,16 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
           gx[dt] = __builtin_fmaf(gm, xv, gx[dt]);
         }
       }
+    GPK_ADJR_ST(9)
   }
+#if GPK_ADJR_STAMPS
+  if (lane == 0) {
+#pragma unroll
+    for (int k2 = 0; k2 < 10; ++k2) g_adjr_st[(blockIdx.x * NW + wave) * 16 + k2] = (unsigned)st_acc[k2];
+  }
+#endif
+#undef GPK_ADJR_ST
+
 
   // ---- workgroup partials, summed over the waves in a fixed order:
   //   [QX (M x D) | q (M) | dvm (M) | dsm (M) | rx2 (D) | sumQ | sumgv | gx (D) | sumgm]
