@@ -65,6 +65,20 @@ GPK_DEVICE void lds_acc(float* p, float v) {
   (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// Order of the per-wave scratch transposes: one wave's LDS operations execute in issue order,
+// so a code-motion barrier is enough between a tile's writes, its reads and the next tile's
+// writes (GPK_ADJ_LDS_WAIT=1: the waitcnt-draining wave_lds_sync instead, for A/B builds)
+#ifndef GPK_ADJ_LDS_WAIT
+#define GPK_ADJ_LDS_WAIT 0
+#endif
+GPK_DEVICE void adj_lds_order() {
+#if GPK_ADJ_LDS_WAIT
+  wave_lds_sync();
+#else
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+
 // Per-chunk LDS base the compiler must treat as new on every iteration: the staged
 // operands (L^{-1}, zs, norms) and their per-lane addresses would otherwise be hoisted out of the chunk loop as
 // loop-invariant loads and pinned in (hundreds of) registers.
@@ -1612,11 +1626,11 @@ gpk_var_adjk_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       for (int ct = 0; ct < 2; ++ct) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = Qt[h][ct][r];
-        wave_lds_sync();
+        adj_lds_order();
         float aq[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) aq[s] = scr[((c & 3) * 16 + 4 * s + g) * 5 + (c >> 2)];
-        wave_lds_sync();   // the next tile overwrites scr
+        adj_lds_order();   // the next tile overwrites scr
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -1943,11 +1957,11 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       for (int ct = 0; ct < 2; ++ct) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = Qt[h][ct][r];
-        wave_lds_sync();
+        adj_lds_order();
         float aq[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) aq[s] = scr[((c & 3) * 16 + 4 * s + g) * 5 + (c >> 2)];
-        wave_lds_sync();
+        adj_lds_order();
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -2802,19 +2816,6 @@ gpk_var_fwd_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 // adjoint instead of twice and the clamp-masked gvar never goes to HBM. The K-Gram partial
 // follows the adjoint partial in the workgroup's row (one reduction launch for both), and
 // block 0 writes the centre cm for gpk_var_fin_kernel.
-// Order of the per-wave scratch transposes: one wave's LDS operations execute in issue order,
-// so a code-motion barrier is enough between a tile's writes, its reads and the next tile's
-// writes (GPK_ADJ_LDS_WAIT=1: the waitcnt-draining wave_lds_sync instead, for A/B builds)
-#ifndef GPK_ADJ_LDS_WAIT
-#define GPK_ADJ_LDS_WAIT 0
-#endif
-GPK_DEVICE void adj_lds_order() {
-#if GPK_ADJ_LDS_WAIT
-  wave_lds_sync();
-#else
-  __builtin_amdgcn_wave_barrier();
-#endif
-}
 
 #ifndef GPK_ADJR_STAMPS
 #define GPK_ADJR_STAMPS 0   // dev builds: per-phase s_memtime cycle totals per wave (gpk_dev_adjr_stamps)
