@@ -62,9 +62,9 @@ def table(fetch, write):
 
 
 VAR3_FWD = ("gpk_var_fwd_l_kernel",)
-# the saved-state adjoint (round 5): adjs -> kgram -> red (G') -> red (partials) -> gdl -> fin -> fin2
+# the saved-state adjoint (round 5): adjs -> kgram -> red (G') -> red (partials) -> gdl -> fin
 VAR3_ADJ = ("gpk_var_adjs_l_kernel", "gpk_var_kgram_l_kernel", "gpk_var_red_kernel", "gpk_var_gdl_l_kernel",
-            "gpk_var_fin_kernel", "gpk_var_fin2_kernel")
+            "gpk_var_fin_kernel")
 
 
 def main():
@@ -108,15 +108,16 @@ def main():
             summary["var_B1024_N256_M64_D32"] = {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
                                                  "fetch_raw_bytes": v["fetch_bytes_raw"],
                                                  "source": "profiles/r05_pmc.json bench " + k}
-    adj = [v for k, v in rows.items() if k.split(" grid")[0] in (
-        "gpk_var_adj_r_kernel<32>", "gpk_var_kgram_r_kernel<32>", "gpk_var_gdl_kernel", "gpk_var_fin_kernel")
-        or (k.startswith("gpk_var_red_kernel") and not k.endswith("grid=596736"))]
+    # cfg 5 (M = 64): the adjoint with the K-Gram folded in, ONE reduction of its
+    # [adjoint | K-Gram] rows (155 blocks) and the output launch (4 dZ blocks + totals + dL^-1)
+    adj = [v for k, v in rows.items() if k.startswith("gpk_var_adj_r_kernel<32")
+           or k == "gpk_var_red_kernel grid=39680" or k == "gpk_var_fin_kernel grid=1536"]
     if adj:
         summary["var_adjoint_B1024_N256_M64_D32"] = {
             "hbm_bytes_per_launch": sum(v["hbm_bytes_per_launch"] for v in adj),
             "hbm_bytes_per_launch_raw": sum(v["fetch_bytes_raw"] + v["write_bytes"] for v in adj),
             "algorithmic_bytes": 4 * (2 * 1024 * 256 * 32 + 2 * 1024 * 256),
-            "source": "profiles/r05_pmc.json bench gpk_var_adj_r / kgram_r / red / gdl / fin"}
+            "source": "profiles/r05_pmc.json bench gpk_var_adj_r<32, 8, true> / red / fin"}
     for n, r in var3.items():
         fwd = [v for k, v in r.items() if k.split("<")[0].split(" ")[0] in VAR3_FWD]
         ad = [v for k, v in r.items() if k.split("<")[0].split(" ")[0] in VAR3_ADJ]
@@ -130,7 +131,7 @@ def main():
                 "hbm_bytes_per_launch_raw": sum(v["fetch_bytes_raw"] + v["write_bytes"] for v in ad),
                 "algorithmic_bytes": 4 * (2 * 256 * n * 32 + 2 * 256 * n),
                 "note": "includes the forward's saved fp32 A read twice (adjs, kgram): 4 B N M per window",
-                "source": f"profiles/r05_pmc.json var3_N{n} adjs / kgram / red / gdl / fin / fin2"}
+                "source": f"profiles/r05_pmc.json var3_N{n} adjs / kgram / red / gdl / fin"}
     with open(p, "w") as fo:
         json.dump(summary, fo, indent=1)
     print(json.dumps(summary, indent=1))
