@@ -2047,7 +2047,8 @@ gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 // LDS rows, gvar masked by the saved clamp mask; each tile product is 8 mfma_f32_16x16x4_f32
 // with both operands read as two b128 per lane (the k index of step j on lane (c, g) is point
 // 8 g + j). Partials gpart[wg] = G' tiles (acc layout) | u, summed in a fixed order afterwards
-// (gpk_var_red_kernel), then gpk_var_gdl_l_kernel forms dL^{-1} elementwise.
+// (gpk_var_red_kernel), then var_gdl_elem (extra blocks of gpk_var_fin_kernel) forms dL^{-1}
+// elementwise.
 // ---------------------------------------------------------------------------
 #ifndef GPK_KGRAM_SPL
 #define GPK_KGRAM_SPL 2   // waves per G' tile-row pair (1: 8 waves x 17 tiles, 209 VGPRs, 2 waves/SIMD)
@@ -2242,10 +2243,8 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 
 // dL^{-1}[p][q] = m_p u_q + 2 (s_p^2 - 1) G'[p][q] for q <= p, 0 above (fp64), elementwise from
 // the fixed-order totals gtot (G' lower tiles in acc layout | u).
-__global__ void __launch_bounds__(256)
-gpk_var_gdl_l_kernel(const double* __restrict__ gtot, const float* __restrict__ vmean,
-                     const float* __restrict__ vstd, int M, int MB, double* __restrict__ dLinv) {
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+GPK_DEVICE void var_gdl_elem(long long e, const double* __restrict__ gtot, const float* __restrict__ vmean,
+                             const float* __restrict__ vstd, int M, int MB, double* __restrict__ dLinv) {
   if (e >= (long long)M * M) return;
   const int p = (int)(e / M), q = (int)(e - (long long)p * M);
   double v = 0.0;
@@ -2362,7 +2361,8 @@ gpk_dlinv_kernel(const float* __restrict__ dA, const float* __restrict__ Kz, int
 __global__ void __launch_bounds__(256)
 gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __restrict__ tot,
                    const double* __restrict__ dlpart, int nsplit, int ntiles, int M,
-                   double* __restrict__ dLinv) {
+                   double* __restrict__ dLinv, const float* __restrict__ wspart2, int P2,
+                   double* __restrict__ tot2) {
   __shared__ double red[8][33];
   const int tid = threadIdx.x, o = tid & 31, q0 = tid >> 5;
   const int nblk_a = (P + 31) / 32;
@@ -2373,6 +2373,13 @@ gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __r
     if (out < P) {
 #pragma unroll 4
       for (int q = q0; q < nwg; q += 8) s += (double)wspart[(size_t)q * P + out];
+    }
+  } else if (wspart2 != nullptr) {
+    // a second partial array with the same workgroup count (one launch for both sums)
+    out = (long long)(blockIdx.x - nblk_a) * 32 + o;
+    if (out < P2) {
+#pragma unroll 4
+      for (int q = q0; q < nwg; q += 8) s += (double)wspart2[(size_t)q * P2 + out];
     }
   } else {
     out = (long long)(blockIdx.x - nblk_a) * 32 + o;
@@ -2395,6 +2402,8 @@ gpk_var_red_kernel(const float* __restrict__ wspart, int nwg, int P, double* __r
     for (int q = 0; q < 8; ++q) t += red[q][o];
     if ((int)blockIdx.x < nblk_a) {
       if (out < P) tot[out] = t;
+    } else if (wspart2 != nullptr) {
+      if (out < P2) tot2[out] = t;
     } else if (out < (long long)M * M) {
       dLinv[out] = t;
     }
@@ -2418,15 +2427,20 @@ GPK_DEVICE void var_gdl_block(const double* __restrict__ gtot, const double* __r
                               const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
                               double* __restrict__ dLinv, double (*Gs)[65], double* us);
 
-// gd.gtot != nullptr (register path, M <= 64): one extra workgroup forms dL^{-1} from the
-// K-Gram totals (var_gdl_block) beside the output blocks instead of in a launch of its own
+// gd.gtot != nullptr: dL^{-1} from the K-Gram totals in extra workgroups of the output launch
+// instead of a launch of its own -- MB == 0 (register path, M <= 64): one workgroup
+// (var_gdl_block, L^{-1} G on fp64 MFMA); MB > 0 (saved-state path): M^2 / 256 workgroups of
+// the elementwise m u^T + 2 (s^2 - 1) G' (var_gdl_elem)
 struct VarGdlArgs {
   const double* gtot;
   const double* Linv;
   const float* vmean;
   const float* vstd;
   double* dLinv;
+  int MB;
 };
+GPK_DEVICE void var_gdl_elem(long long e, const double* __restrict__ gtot, const float* __restrict__ vmean,
+                             const float* __restrict__ vstd, int M, int MB, double* __restrict__ dLinv);
 
 __global__ void __launch_bounds__(256)
 gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
@@ -2439,9 +2453,14 @@ gpk_var_fin_kernel(const float* __restrict__ Z, const float* __restrict__ vstd,
   __shared__ float cms[kCmParts * 64];
   const int tid = threadIdx.x;
   const int nblk = (M + kFinRows - 1) / kFinRows;
-  if (gd.gtot != nullptr && (int)blockIdx.x == nblk + 1) {
-    double* gl = (double*)fzs;
-    var_gdl_block(gd.gtot, gd.Linv, gd.vmean, gd.vstd, M, gd.dLinv, (double(*)[65])gl, gl + 64 * 65);
+  if (gd.gtot != nullptr && (int)blockIdx.x > nblk) {
+    if (gd.MB == 0) {
+      double* gl = (double*)fzs;
+      var_gdl_block(gd.gtot, gd.Linv, gd.vmean, gd.vstd, M, gd.dLinv, (double(*)[65])gl, gl + 64 * 65);
+    } else {
+      var_gdl_elem((long long)(blockIdx.x - nblk - 1) * 256 + tid, gd.gtot, gd.vmean, gd.vstd, M, gd.MB,
+                   gd.dLinv);
+    }
     return;
   }
   const bool totals = (int)blockIdx.x == nblk;
@@ -3706,9 +3725,9 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
       // one fixed-order reduction of the [adjoint | K-Gram] rows; dL^{-1} in the output launch
       const int PR = p.P + kGPart;
       hipLaunchKernelGGL(gpk_var_red_kernel, dim3((PR + 31) / 32), dim3(256), 0, stream, wspart, p.nwg, PR,
-                         tot, nullptr, 0, 0, 0, nullptr);
+                         tot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
       if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-      const VarGdlArgs gd{gtot, a.Linv, a.vmean, a.vstd, a.dLinv};
+      const VarGdlArgs gd{gtot, a.Linv, a.vmean, a.vstd, a.dLinv, 0};
       return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream, wsgv, &gd);
     } else {
       set_lds_once<gpk_var_kgram_r_kernel<RQ>>();
@@ -3719,10 +3738,10 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
     }
     // fixed-order sums: K-Gram partials -> gtot, adjoint partials -> tot (section (a) only)
     hipLaunchKernelGGL(gpk_var_red_kernel, dim3((kGPart + 31) / 32), dim3(256), 0, stream, gpart, p.nwg,
-                       kGPart, gtot, nullptr, 0, 0, 0, nullptr);
+                       kGPart, gtot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.P + 31) / 32), dim3(256), 0, stream, wspart, p.nwg,
-                       p.P, tot, nullptr, 0, 0, 0, nullptr);
+                       p.P, tot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(gpk_var_gdl_kernel, dim3(1), dim3(256), 0, stream, gtot, a.Linv, a.vmean, a.vstd,
                        a.M, a.dLinv);
@@ -3767,12 +3786,18 @@ int launch_var_fin(const float* Z, const float* vstd, const float* hyp, const do
   set_lds_once<gpk_var_fin_kernel, 64 * 1024>();   // + ~3.3 KB static
   size_t lds = (size_t)M * D * sizeof(float);
   VarGdlArgs g{};
+  int ngd = 0;
   if (gd != nullptr) {
     g = *gd;
-    const size_t gl = (64 * 65 + 64) * sizeof(double);
-    if (lds < gl) lds = gl;
+    if (g.MB == 0) {
+      ngd = 1;
+      const size_t gl = (64 * 65 + 64) * sizeof(double);
+      if (lds < gl) lds = gl;
+    } else {
+      ngd = (int)(((long long)M * M + 255) / 256);
+    }
   }
-  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(nblk + 1 + (gd != nullptr ? 1 : 0)), dim3(256), lds, stream, Z,
+  hipLaunchKernelGGL(gpk_var_fin_kernel, dim3(nblk + 1 + ngd), dim3(256), lds, stream, Z,
                      vstd, hyp, tot, M, D, dZ, dpar, cm_in, g);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
@@ -3792,7 +3817,7 @@ int launch_var_adj_tail(const GpkVarAdjArgs& a, const AdjPlan& p, hipStream_t st
   if (e != hipSuccess) return (int)e;
   const long long nred = (p.P + 31) / 32 + ((long long)a.M * a.M + 31) / 32;
   hipLaunchKernelGGL(gpk_var_red_kernel, dim3((unsigned)nred), dim3(256), 0, stream,
-                     wspart, p.nwg, p.P, tot, dl, p.nsplit, p.ntiles, a.M, a.dLinv);
+                     wspart, p.nwg, p.P, tot, dl, p.nsplit, p.ntiles, a.M, a.dLinv, nullptr, 0, nullptr);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream);
@@ -3851,17 +3876,23 @@ int launch_var_adj_saved(const GpkVarAdjArgs& a, hipStream_t stream) {
                        stream, a.X, a.Z, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.saved, a.N, a.M, a.D,
                        p.nchunks, gpart);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.PG + 31) / 32), dim3(256), 0, stream, gpart, p.nwg_g, p.PG,
-                       gtot, nullptr, 0, 0, 0, nullptr);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.P + 31) / 32), dim3(256), 0, stream, wspart, p.nwg, p.P, tot,
-                       nullptr, 0, 0, 0, nullptr);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(gpk_var_gdl_l_kernel, dim3((unsigned)(((long long)a.M * a.M + 255) / 256)), dim3(256), 0,
-                       stream, gtot, a.vmean, a.vstd, a.M, MB, a.dLinv);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    // one fixed-order reduction launch for both partial arrays (same workgroup count), then
+    // the output launch with dL^{-1} in extra workgroups
+    if (p.nwg == p.nwg_g) {
+      hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.P + 31) / 32 + (p.PG + 31) / 32), dim3(256), 0, stream,
+                         wspart, p.nwg, p.P, tot, nullptr, 0, 0, 0, nullptr, gpart, p.PG, gtot);
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    } else {
+      hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.PG + 31) / 32), dim3(256), 0, stream, gpart, p.nwg_g,
+                         p.PG, gtot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+      hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.P + 31) / 32), dim3(256), 0, stream, wspart, p.nwg, p.P,
+                         tot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    }
+    const VarGdlArgs gd{gtot, a.Linv, a.vmean, a.vstd, a.dLinv, MB};
     return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream,
-                          (const float*)(ws + p.off_cm));
+                          (const float*)(ws + p.off_cm), &gd);
   } else {
     return -13;
   }

@@ -62,9 +62,8 @@ def table(fetch, write):
 
 
 VAR3_FWD = ("gpk_var_fwd_l_kernel",)
-# the saved-state adjoint (round 5): adjs -> kgram -> red (G') -> red (partials) -> gdl -> fin
-VAR3_ADJ = ("gpk_var_adjs_l_kernel", "gpk_var_kgram_l_kernel", "gpk_var_red_kernel", "gpk_var_gdl_l_kernel",
-            "gpk_var_fin_kernel")
+# the saved-state adjoint (round 5): adjs -> kgram -> red (partials | G') -> fin (+ dL^-1 blocks)
+VAR3_ADJ = ("gpk_var_adjs_l_kernel", "gpk_var_kgram_l_kernel", "gpk_var_red_kernel", "gpk_var_fin_kernel")
 
 
 def main():
@@ -131,7 +130,7 @@ def main():
                 "hbm_bytes_per_launch_raw": sum(v["fetch_bytes_raw"] + v["write_bytes"] for v in ad),
                 "algorithmic_bytes": 4 * (2 * 256 * n * 32 + 2 * 256 * n),
                 "note": "includes the forward's saved fp32 A read twice (adjs, kgram): 4 B N M per window",
-                "source": f"profiles/r05_pmc.json var3_N{n} adjs / kgram / red / gdl / fin"}
+                "source": f"profiles/r05_pmc.json var3_N{n} adjs / kgram / red / fin"}
     with open(p, "w") as fo:
         json.dump(summary, fo, indent=1)
     print(json.dumps(summary, indent=1))
