@@ -72,10 +72,22 @@ def var_flops_per_window(N, M, D):  # SURVEY.md §8d cfg 5: (fp32, fp64)
 
 
 def var_adj_flops_per_window(N, M, D):
-    """Adjoint of the same window: fp32 = K_ZX recompute (3DMN + 5MN),
-    Q^T zs and Q X (2 x 2MND), elementwise dA / Q / dX (~10MN + 6DN); fp64 = A = L^-1 K_ZX,
-    dK = L^-T dA and the window's share of dL^-1 = sum dA K^T (3 x M^2 N, triangular)."""
-    return 3 * D * M * N + 5 * M * N + 4 * M * N * D + 10 * M * N + 6 * D * N, 3 * M * M * N
+    """The REFERENCE's backward of one window (what autograd runs through GPyTorch's
+    VariationalStrategy, DeepGP.py:14-73): it keeps A = L^-1 K_ZX and K_ZX from the forward,
+    so nothing is recomputed. fp64: the triangular-solve adjoint dK = L^-T dA (M^2 N) and the
+    window's share of dL^-1 = -tril(dK A^T) (M^2 N) = 2 M^2 N; fp32: the RBF adjoint's
+    Q^T zs and Q X contractions (2 x 2MND) plus the elementwise dA / Q / dX work (~10MN + 6DN).
+    DESIGN.md §4.5; what the kernels actually execute is var_adj_impl_flops_per_window."""
+    return 4 * M * N * D + 10 * M * N + 6 * D * N, 2 * M * M * N
+
+
+def var_adj_impl_flops_per_window(N, M, D, saved):
+    """What the adjoint kernels execute per window, recomputation included: the f32 K_ZX Gram
+    (3DMN + 5MN) is always recomputed; without a saved forward state (M <= 64, the register
+    path) A = L^-1 K_ZX is recomputed too (+M^2 N fp64). Reported beside the reference count,
+    never used for the roofline fraction."""
+    f32, f64 = var_adj_flops_per_window(N, M, D)
+    return f32 + 3 * D * M * N + 5 * M * N, f64 + (0 if saved else M * M * N)
 
 
 def cpu_model():
@@ -311,6 +323,9 @@ def variational_leg(dev, B, N, M, D, steps, warmup, world, seed, label="BASELINE
                               "peak": sum(var_adj_flops_per_window(N, M, D)) / adj_roof_s / 1e12,
                               "unit": "TFLOP/s", "frac": adj_roof_s * B / (ms["bwd"] * 1e-3),
                               "flops_per_window": dict(zip(("fp32", "fp64"), var_adj_flops_per_window(N, M, D))),
+                              "flops_basis": "the reference's backward (A and K_ZX kept by autograd; no recompute)",
+                              "implementation_flops_per_window": dict(zip(("fp32", "fp64"), var_adj_impl_flops_per_window(
+                                  N, M, D, saved is not None))),
                               "traffic": load_traffic(f"var_adjoint_B{B}_N{N}_M{M}_D{D}"),
                               "algorithmic_bytes": 4 * (2 * B * N * D + 2 * B * N)},
         "mean_ell": float(out.ell.double().mean()),
@@ -622,6 +637,17 @@ def main():
                 "gpu_over_cpu": value / best,
                 "mll_rel_err_vs_fp64_oracle": mll_rel_err(X, y, out.mll),
             }
+            if v_procs:
+                # the whole host: the measured per-process rate times every affinity core. An
+                # extrapolation, not a run -- the GPU pool caps a job's worker processes at its
+                # CPU share (OMP_NUM_THREADS), so `cores` single-thread processes is the most it runs.
+                whole = v_procs / cores * affinity
+                line["cpu_baseline"]["all_affinity_cores"] = {
+                    "value": whole, "cores": affinity, "measured": False,
+                    "basis": f"{v_procs / cores:.0f} windows/s per single-thread process "
+                             f"(measured, {cores} processes) x {affinity} affinity cores, assuming "
+                             f"linear scaling across sockets",
+                    "gpu_over_cpu": value / whole}
             if var is not None:
                 vv, sv = cpu_var_baseline(args.var_N, args.var_M, D, args.cpu_seconds, nthr)
                 line["cpu_baseline"]["variational"] = {

@@ -125,6 +125,7 @@ __host__ __device__ inline ExactLds exact_lds_layout(int NB, int DC, int W) {
   o.rbfc = o.hbuf + 2 * 512;             // RbfK (16-byte aligned)
   o.red = o.rbfc + 4;
   o.total = o.red + 4 * W + 96;          // flag words (see the kFlag enum)
+  if (kEpochCheck) o.total += 48;        // (check builds: epoch shadows, kShadowPan..)
   return o;
 }
 
@@ -330,12 +331,17 @@ GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
 }
 
 // A worker wait inside a factorisation step. It does NOT watch the failure word: the restart
-// is correct because every wait a worker makes in step K is satisfied by work of steps < K of
-// the same attempt (panel / z / counter flags of step K-1 or earlier), while the diagonal wave
-// reports a failure no earlier than at the step it fails at, and a worker leaves the attempt
-// only at the R_KK^{-T} check of a step K >= that step ((fail - 1) >> 4 <= K). So all workers
-// have passed the same waits when they leave, and none waits for a step that never comes.
-// A new wait must keep that step-ordering invariant (else it spins until the 2^18-poll bound).
+// is correct because every wait a worker makes in step K is satisfied by work that its
+// producers do BEFORE they reach their own R_{K+1,K+1}^{-T} check: panel / z / counter flags of
+// step K-1 or earlier, and -- phase 4b of the column plan -- tiles of panel K itself, which
+// their owners write right after passing the step-K check. The diagonal wave reports a
+// failure no earlier than at the step F it fails at, and a worker leaves the attempt only at
+// the R_KK^{-T} check of a step K >= F ((fail - 1) >> 4 <= K). So for K < F every producer
+// passes its step-K check and does the awaited work before its step-(K+1) check <= F; at
+// K = F nobody gets past the check to wait for step-F work; all workers leave at the same
+// check, and none waits for work that never comes. A new wait must keep this invariant: wait
+// only for work of steps <= K that precedes the producer's next check (else it spins until
+// the 2^18-poll bound).
 #define GPK_WAITF(idx, target)                                                  \
   {                                                                             \
     unsigned long long _w0 = 0;                                                 \
@@ -344,6 +350,24 @@ GPK_DEVICE void spin_until(lds_vint* flags, int idx, int target) {
     if constexpr (ST) x.st[9] += __builtin_amdgcn_s_memtime() - _w0;            \
   }
 
+
+// Epoch shadows (GPK_EPOCH_CHECK builds only; gpk_exact_dev.h; every use is inside GPK_EP(...),
+// which expands to nothing in product builds, so their device code is unchanged). Flag words past the product
+// layout: panel tile j of step k at kShadowPan + (k & 1) (NB + 1) + j, the hand-over tiles of step
+// k at kShadowHo + 2 (k & 1) + {0: (k, k+1), 1: (k+1, k+1)}, R_kk^{-T} at kShadowW + k % 3. The
+// producer writes the epoch of the tile after the tile and before its flag release; the
+// consumer compares it after the acquire.
+constexpr int kFlagEpochBad = 84;   // site | slot << 8 of the first mismatch (check builds)
+constexpr int kShadowPan = 96, kShadowHo = 130, kShadowW = 134;
+GPK_DEVICE void epoch_mark(lds_vint* flags, int idx, int epoch, int lane) {
+  if (lane == 0) flags[idx] = epoch;
+}
+GPK_DEVICE void epoch_expect(lds_vint* flags, int idx, int epoch, int site) {
+  if (flags[idx] != epoch) {
+    flags[kFlagEpochBad] = site | (idx << 8);
+    flags[kFlagTmo] = 1;   // the window ends with info = kInfoTimeout; the launch still drains
+  }
+}
 
 GPK_DEVICE void publish_tile(float* dst, int lane, const f32x4 v, lds_vint* flags, int idx, int value) {
   *(f32x4*)&dst[lane * 4] = v;
@@ -500,6 +524,7 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
   // either value as (word - 1) >> 4, so a worker that is still at an earlier step does not
   // leave the attempt before the others (they all leave at step k)
   if (badm != 0 && lane == 0) *fail_flag = 16 * (epoch & 31) + 1;
+  GPK_EP(epoch_mark(flags, kShadowW + (epoch & 31) % 3, epoch, lane);)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   if (lane == 0) flags[kFlagFact] = epoch;
   if constexpr (ST) {
@@ -651,6 +676,16 @@ struct WorkerCtx {
   unsigned long long* tl;  // STAMPS builds only: per-step timeline [(k * 8 + wave) * 8 + event]
 };
 
+// Check builds (GPK_EPOCH_CHECK): the panel tile at `tile` (either parity buffer) carries the
+// epoch of the step that wrote it -- step K in the buffer of parity K & 1, else step K - 1.
+template <int NB, int K>
+GPK_DEVICE void epoch_pan(const WorkerCtx& x, const float* tile, int e0, int site) {
+  GPK_EP(const int s = (int)(tile - x.panel) >> 8; epoch_expect(x.vflag, kShadowPan + s, e0 + (s / (NB + 1) == (K & 1) ? K : K - 1), site);)
+}
+GPK_DEVICE void epoch_pan_mark(const WorkerCtx& x, const float* tile, int epoch) {
+  GPK_EP(epoch_mark(x.vflag, kShadowPan + ((int)(tile - x.panel) >> 8), epoch, x.lane);)
+}
+
 // Barrier among the WK worker waves only (the diagonal wave runs ahead of them
 // and never joins): monotone LDS counter, one ds_add per wave.
 // Split into arrive (publish this wave's LDS writes, count in) and wait, so
@@ -717,6 +752,8 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
   // wave-specialised gets hoisted out of the attempt loop)
   auto upd_ij = [&](f32x4& d, auto I, auto J) {
     constexpr int i = decltype(I)::value, j = decltype(J)::value;
+    GPK_EP(epoch_pan<NB, K>(x, pprev + i * 256, e0, 1);)
+    GPK_EP(epoch_pan<NB, K>(x, pprev + j * 256, e0, 1);)
     d = pan_mma(pan_load(pprev + i * 256, lane), pprev + j * 256, lane, d);
   };
   if constexpr (K > 0) {
@@ -724,10 +761,12 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);   // hand-over: the diagonal wave waits
       if (wv == TA % WK) {
         upd_ij(acc[TA / WK], IC<K>{}, IC<K + 1>{});
+        GPK_EP(epoch_mark(x.vflag, kShadowHo + 2 * (K & 1), e0 + K, lane);)
         publish_tile(hA, lane, acc[TA / WK], x.vflag, kFlagHA + (K & 1), e0 + K);
       }
       if (wv == TB % WK) {
         upd_ij(acc[TB / WK], IC<K + 1>{}, IC<K + 1>{});
+        GPK_EP(epoch_mark(x.vflag, kShadowHo + 2 * (K & 1) + 1, e0 + K, lane);)
         publish_tile(hA + 256, lane, acc[TB / WK], x.vflag, kFlagHB + (K & 1), e0 + K);
       }
       if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -740,6 +779,8 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     auto upd = [&](f32x4& d, auto I) {
       constexpr int s = decltype(I)::value;
       const int p = plan_tile<NB, WK * s, WK * s + WK - 1>(wv + WK * s);
+      GPK_EP(epoch_pan<NB, K>(x, pprev + (p & 255) * 256, e0, 2);)
+      GPK_EP(epoch_pan<NB, K>(x, pprev + (p >> 8) * 256, e0, 2);)
       if constexpr (kKoOneOperand) {   // knockout: one LDS operand per tile update
         const pan_op_t q = pan_load(pprev + (p & 255) * 256, lane);
         d = pan_mma_op(q, q, d);
@@ -776,6 +817,8 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     for (int i = rfirst; i < NB; i += WK) {
       f32x4 d = *(const f32x4*)&x.rw[16 * i + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+      GPK_EP(epoch_pan<NB, K>(x, pprev + i * 256, e0, 3);)
+      GPK_EP(epoch_pan<NB, K>(x, pprev + NB * 256, e0, 3);)
       d = pan_mma(pan_load(pprev + i * 256, lane), pprev + NB * 256, lane, d);
       if (c == 0) *(f32x4*)&x.rw[16 * i + 4 * grp] = d;
     }
@@ -800,6 +843,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     q = load_w_v(wbk, c, grp);
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
+  GPK_EP(epoch_expect(x.vflag, kShadowW + K % 3, e0 + K, 4);)
   if (!kKoAny && fail != 0 && ((fail - 1) >> 4) <= K) {   // the attempt failed at step <= K
     __builtin_amdgcn_s_setprio(0);   // the jitter-ladder retry starts at the base priority
     return 1;
@@ -817,6 +861,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
         if (t >= TLO && t <= THI) {
           const int j = plan_tile<NB, WK * s, WK * s + WK - 1>(t) >> 8;
           const f32x4 rkj = pan_store(pcur + j * 256, lane, kKoTrsmMfma ? acc[s] : trsm_tile(wq, acc[s]));
+          GPK_EP(epoch_pan_mark(x, pcur + j * 256, e0 + K);)
           // L[16j + c][16K + 4g + r] = R_Kj[4g + r][c] / sigma
           if (!kKoTrsmLStores && x.Lb != nullptr)
             store4<FULL>(x.Lb, x.N, 16 * j + c, 16 * K + 4 * grp, rkj * inv_sigma);
@@ -827,6 +872,7 @@ GPK_DEVICE int worker_step_split(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
       const f32x4 zk = pan_store(pcur + NB * 256, lane, trsm_tile_f32(q, d));   // (y unbounded: fp32)
+      GPK_EP(epoch_pan_mark(x, pcur + NB * 256, e0 + K);)
       if (c == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
@@ -935,8 +981,11 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     if (x.lane == 0) x.tl[(K * 8 + x.wv) * 8] = __builtin_amdgcn_s_memtime();
   }
   auto upd = [&](f32x4& d, const float* qt, const pan_op_t p_hl, const pan_op_t p_lh) {
+    GPK_EP(epoch_pan<NB, K>(x, qt, e0, 10);)
     d = pan_mma2(pan_load(qt, lane), p_hl, p_lh, d);
   };
+  // (check builds) a column operand P of this step's updates
+  GPK_EP(auto pck = [&](const float* t, int site) { epoch_pan<NB, K>(x, t, e0, site); };)
   // ---- 1. (the hand-over HO_K = (K, K+1), (K+1, K+1) was produced in step K-1: see 4b)
   // ---- 2. the other tiles of row K (K, j), j >= K+2, through panel K-1
   if constexpr (K > 0) {
@@ -949,17 +998,20 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if (c_row) { GPK_WAITF(kFlagPan + 8, e0 + K - 1) }
       const float* qt = pprev + K * 256;
       if (a_row) {
+        GPK_EP(pck(pprev + jA * 256, 11);)
         const pan_op_t p = pan_load(pprev + jA * 256, lane);
         upd(acc[K], qt, p, pan_swap(p));
       }
       if constexpr (17 - K >= 0 && 17 - K < 18) {
         if (b_row) {
+          GPK_EP(pck(pprev + jB * 256, 12);)
           const pan_op_t p = pan_load(pprev + jB * 256, lane);
           upd(acc[17 - K], qt, p, pan_swap(p));
         }
       }
       if constexpr (C8) {
         if (c_row) {
+          GPK_EP(pck(pprev + 8 * 256, 13);)
           const pan_op_t p = pan_load(pprev + 8 * 256, lane);
           upd(acc[18], qt, p, pan_swap(p));
         }
@@ -973,6 +1025,8 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       if constexpr (K == 8) { GPK_WAITF(kFlagPan + 8, e0 + K - 1) }
       f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+      GPK_EP(pck(pprev + K * 256, 14);)
+      GPK_EP(pck(pprev + NB * 256, 14);)
       d = pan_mma(pan_load(pprev + K * 256, lane), pprev + NB * 256, lane, d);
       if (c == 0) *(f32x4*)&x.rw[16 * K + 4 * grp] = d;
     }
@@ -990,6 +1044,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     q = load_w_v(wbk, c, grp);
   }
   GPK_WSTAMP(7, 4)  // wait for R_KK^{-T}
+  GPK_EP(epoch_expect(x.vflag, kShadowW + K % 3, e0 + K, 15);)
   if (!kKoAny && fail != 0 && ((fail - 1) >> 4) <= K) return 1;
   if constexpr (GPK_EXACT_PRIO) __builtin_amdgcn_s_setprio(GPK_EXACT_PRIO);
   // panel buffer K & 1 held panel K-2 (read in step K-1): every wave must be past step K-1's
@@ -1000,11 +1055,13 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     const bool a_t = (K + 1 <= jA), b_t = (K + 1 <= jB);
     if (a_t) {
       const f32x4 r = pan_store(pcur + jA * 256, lane, trsm_tile(wq, acc[K]));
+      GPK_EP(epoch_pan_mark(x, pcur + jA * 256, e0 + K + ((kEpochSabotage && K == 3) ? 1 : 0));)
       if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * jA + c, 16 * K + 4 * grp, r * inv_sigma);
     }
     if constexpr (17 - K >= 0 && 17 - K < 18) {
       if (b_t) {
         const f32x4 r = pan_store(pcur + jB * 256, lane, trsm_tile(wq, acc[17 - K]));
+        GPK_EP(epoch_pan_mark(x, pcur + jB * 256, e0 + K);)
         if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * jB + c, 16 * K + 4 * grp, r * inv_sigma);
       }
     }
@@ -1013,6 +1070,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     if constexpr (C8S >= 0) {
       if (wv == C8W) {
         const f32x4 r = pan_store(pcur + 8 * 256, lane, trsm_tile(wq, acc[C8S]));
+        GPK_EP(epoch_pan_mark(x, pcur + 8 * 256, e0 + K);)
         if (x.Lb != nullptr) store4<FULL>(x.Lb, x.N, 16 * 8 + c, 16 * K + 4 * grp, r * inv_sigma);
       }
     }
@@ -1020,6 +1078,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       f32x4 d = *(const f32x4*)&x.rw[16 * K + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
       const f32x4 zk = pan_store(pcur + NB * 256, lane, trsm_tile_f32(q, d));   // (y unbounded: fp32)
+      GPK_EP(epoch_pan_mark(x, pcur + NB * 256, e0 + K);)
       if (c == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) x.sumz2 = __builtin_fmaf(zk[r], zk[r], x.sumz2);
@@ -1057,6 +1116,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       float* hN = x.hbuf + (K1 & 1) * 512;
       if constexpr (K > 0) {   // panel K-1
         GPK_WAITF(kFlagPan + K1 + 1, e0 + K - 1)
+        GPK_EP(pck(pprev + (K1 + 1) * 256, 16);)
         const pan_op_t p = pan_load(pprev + (K1 + 1) * 256, lane);
         const pan_op_t pl = pan_swap(p);
         if (wv == HAW) {
@@ -1071,15 +1131,18 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       }
       // panel K (this step's TRSM)
       GPK_WAITF(kFlagPan + K1 + 1, e0 + K)
+      GPK_EP(pck(pcur + (K1 + 1) * 256, 17);)
       const pan_op_t p = pan_load(pcur + (K1 + 1) * 256, lane);
       const pan_op_t pl = pan_swap(p);
       if (wv == HAW) {
         GPK_WAITF(kFlagPan + K1, e0 + K)
         upd(acc[SA], pcur + K1 * 256, p, pl);
+        GPK_EP(epoch_mark(x.vflag, kShadowHo + 2 * (K1 & 1), e0 + K1, lane);)
         publish_tile(hN, lane, acc[SA], x.vflag, kFlagHA + (K1 & 1), e0 + K1);
       }
       if (wv == HBW) {
         acc[SB] = pan_mma2(p, p, pl, acc[SB]);
+        GPK_EP(epoch_mark(x.vflag, kShadowHo + 2 * (K1 & 1) + 1, e0 + K1, lane);)
         publish_tile(hN + 256, lane, acc[SB], x.vflag, kFlagHB + (K1 & 1), e0 + K1);
       }
     }
@@ -1092,6 +1155,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     GPK_WAITF(kFlagTrsm, WK * K)   // panel K-1 complete
     // column A (rows K+1 .. jA; (K+1, K+1) is HB: done)
     if (K + 1 <= jA) {
+      GPK_EP(pck(pprev + jA * 256, 18);)
       const pan_op_t p = pan_load(pprev + jA * 256, lane);
       const pan_op_t pl = pan_swap(p);
       static_for_range<K + 1, 15>([&](auto I) {
@@ -1104,6 +1168,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     // column B (rows K+1 .. jB <= 7)
     if constexpr (K + 1 <= 7) {
       if (K + 1 <= jB) {
+        GPK_EP(pck(pprev + jB * 256, 19);)
         const pan_op_t p = pan_load(pprev + jB * 256, lane);
         const pan_op_t pl = pan_swap(p);
         static_for_range<K + 1, 7>([&](auto I) {
@@ -1120,6 +1185,7 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
       const bool s19 = (wv <= 1) && (wv + 7 >= K + 1) && !(wv + 7 == 8 && K + 1 == 8) &&
                        !(K + 2 == 8 && (wv + 7 == K + 1 || wv + 7 == K + 2));   // HO_7: 4b
       if (s18 || s19) {
+        GPK_EP(pck(pprev + 8 * 256, 20);)
         const pan_op_t p = pan_load(pprev + 8 * 256, lane);
         const pan_op_t pl = pan_swap(p);
         if (s18) upd(acc[18], pprev + wv * 256, p, pl);
@@ -1131,6 +1197,8 @@ GPK_DEVICE int worker_step_col(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
     auto rhs = [&](int j) {
       f32x4 d = *(const f32x4*)&x.rw[16 * j + 4 * grp];
       if (c != 0) d = f32x4{0.f, 0.f, 0.f, 0.f};
+      GPK_EP(pck(pprev + j * 256, 21);)
+      GPK_EP(pck(pprev + NB * 256, 21);)
       d = pan_mma(pan_load(pprev + j * 256, lane), pprev + NB * 256, lane, d);
       if (c == 0) *(f32x4*)&x.rw[16 * j + 4 * grp] = d;
     };
@@ -1644,6 +1712,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
           }
           hw0 = hw1;
         }
+        GPK_EP(epoch_expect(vflag, kShadowHo + 2 * (k & 1), epoch, 30); epoch_expect(vflag, kShadowHo + 2 * (k & 1) + 1, epoch, 31);)
         const f32x4 q = load_w(wb, c, grp);
         const f32x4 ta = *(const f32x4*)&hk[lane * 4];
         f32x4 tb = *(const f32x4*)&hk[256 + lane * 4];
@@ -1716,6 +1785,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
           acc[17] = rbf_tile<NB, FULL>(smem, rk, 0, jB, lane, N);
           acc[16] = rbf_tile<NB, FULL>(smem, rk, 1, jB, lane, N);
           if (wv == 0) {
+            GPK_EP(epoch_mark(vflag, kShadowHo, e0, lane); epoch_mark(vflag, kShadowHo + 1, e0, lane);)
             publish_tile(hbuf, lane, acc[17], vflag, kFlagHA + 0, e0);
             publish_tile(hbuf + 256, lane, acc[16], vflag, kFlagHB + 0, e0);
           }
@@ -1737,10 +1807,12 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
         if constexpr (NB > 1) {
           if (wv == T01 % WK) {
             acc[T01 / WK] = rbf_tile<NB, FULL>(smem, rk, 0, 1, lane, N);
+            GPK_EP(epoch_mark(vflag, kShadowHo, e0, lane);)
             publish_tile(hbuf, lane, acc[T01 / WK], vflag, kFlagHA + 0, e0);
           }
           if (wv == P1 % WK) {
             acc[P1 / WK] = rbf_tile<NB, FULL>(smem, rk, 1, 1, lane, N);
+            GPK_EP(epoch_mark(vflag, kShadowHo + 1, e0, lane);)
             publish_tile(hbuf + 256, lane, acc[P1 / WK], vflag, kFlagHB + 0, e0);
           }
         }

@@ -41,6 +41,20 @@
 #ifndef GPK_TMO_DEBUG
 #define GPK_TMO_DEBUG 0   // 1 (debug builds): a timed-out window's info = flag index | target << 8
 #endif
+#ifndef GPK_EPOCH_CHECK
+#define GPK_EPOCH_CHECK 0   // 1 (check builds): every consumed panel / hand-over / R_kk^{-T} tile is checked
+                            // against the epoch its consumer expects (epoch shadows in LDS, written by the
+                            // producer before its flag release); a mismatch ends the window with
+                            // info = 1<<20 and the site in flag word kFlagEpochBad. 2: the same plus a
+                            // deliberate wrong mark (the check's own negative control).
+#endif
+constexpr bool kEpochCheck = GPK_EPOCH_CHECK != 0;
+#if GPK_EPOCH_CHECK
+#define GPK_EP(...) __VA_ARGS__
+#else
+#define GPK_EP(...)
+#endif
+constexpr bool kEpochSabotage = GPK_EPOCH_CHECK == 2;
 #ifndef GPK_KO
 #define GPK_KO 0   // knockout bits (timing only, results WRONG): see the constants below
 #endif

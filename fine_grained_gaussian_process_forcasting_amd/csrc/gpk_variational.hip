@@ -3544,13 +3544,18 @@ int launch_var_fwd(const GpkVarArgs& a, int* flags, hipStream_t stream) {
 
 // The saved-state adjoint (gpk_var_adjs_l_kernel + K-Gram) serves M > 64 when its LDS plan fits
 // (D <= 32 at M = 256); the training forward then keeps A for it.
+// 0: A/B builds with the LDS-tiled forward for M > 64 (that forward keeps no state, so the
+// saved-state training pair is off too: var_saved_path is false and saved_bytes 0)
+#ifndef GPK_VAR_LREG
+#define GPK_VAR_LREG 1
+#endif
 template <int MB, int DQ>
 constexpr bool var_saved_fits() {
   if constexpr (MB >= 5) return LAdjGeo<MB, DQ>::fits && (size_t)LGramGeo<MB, DQ>::total * 4 <= 160 * 1024;
   return false;
 }
 template <int MB, int DQ>
-bool var_saved_path(int M) { return var_saved_fits<MB, DQ>() && M > 64; }
+bool var_saved_path(int M) { return GPK_VAR_LREG && var_saved_fits<MB, DQ>() && M > 64; }
 
 template <int MB, int DQ>
 int launch_var_fwd_l(const GpkVarArgs& a, int* flags, hipStream_t stream) {
@@ -3576,9 +3581,6 @@ int launch_var_fwd_l(const GpkVarArgs& a, int* flags, hipStream_t stream) {
   return e == hipSuccess ? 0 : (int)e;
 }
 
-#ifndef GPK_VAR_LREG
-#define GPK_VAR_LREG 1   // 0: A/B builds with the LDS-tiled forward for M > 64
-#endif
 
 struct AdjPlan {
   int nchunks, nwg, P, ntiles, nsplit;

@@ -187,13 +187,17 @@ class MultivariateNormal:
 
     def __init__(self, mean: torch.Tensor, variance: Optional[torch.Tensor] = None,
                  exact=None, added_noise=None, clamp_flag: Optional[torch.Tensor] = None,
-                 preclamped: bool = False):
+                 preclamped: bool = False, covar_fn=None):
         self._mean = mean
         self._variance = variance
         self._exact = exact                # (X, kernel hyper) for exact-GP priors
         self._added_noise = added_noise    # likelihood noise folded in by GaussianLikelihood
         self._clamp_flag = clamp_flag      # (1,) int32 from gpk_variational_f32: clamp fired
         self._preclamped = preclamped      # variance already clamped by the kernel, no flag
+        # () -> dense (..., N, N) covariance of a variational output (its lazy covariance, as
+        # GPyTorch's VariationalStrategy builds it); materialised only by covariance_matrix /
+        # rsample, never on the hot path
+        self._covar_fn = covar_fn
 
     @property
     def mean(self):
@@ -257,27 +261,66 @@ class MultivariateNormal:
         the diagonal) + the added likelihood noise on the diagonal. Not on the hot path: no
         reference caller reads it. Variational outputs are diagonal-query (their marginals
         are what the reference reads) and do not carry a covariance."""
-        if self._exact is None:
-            raise NotImplementedError("covariance_matrix is provided for exact-GP / layer priors; "
-                                      "variational outputs carry their marginal variance only")
-        X, lengthscale, outputscale, _ = self._exact
-        K = rbf_covariance(X, lengthscale, outputscale)
+        if self._exact is None and self._covar_fn is None:
+            raise NotImplementedError("covariance_matrix is provided for exact-GP / layer priors and "
+                                      "variational outputs")
+        if self._exact is not None:
+            X, lengthscale, outputscale, _ = self._exact
+            K = rbf_covariance(X, lengthscale, outputscale)
+        else:
+            K = self._covar_fn()
         if self._added_noise is not None:
             K = K + torch.diag_embed(torch.as_tensor(self._added_noise, dtype=K.dtype, device=K.device)
                                      .expand(K.shape[:-1]))
-        return K.reshape(*self._mean.shape, self._mean.shape[-1])
+        n = self._mean.shape[-1]
+        if K.numel() != self._mean.numel() * n:   # an expanded distribution: the batch is a view
+            K = K.reshape(-1, *self._mean.shape[-1:], n).expand(*self._mean.shape, n) if K.dim() == 2 else \
+                K.expand(*self._mean.shape, n)
+        return K.reshape(*self._mean.shape, n)
+
+    @property
+    def lazy_covariance_matrix(self):
+        return self.covariance_matrix
+
+    def rsample(self, sample_shape=torch.Size(), base_samples: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Reparameterised sample mean + chol(Sigma) eps (upstream MultivariateNormal.rsample: the
+        covariance root by psd_safe_cholesky with the jitter ladder). Off the hot path: the dense
+        covariance is materialised (covariance_matrix)."""
+        cov = self.covariance_matrix
+        root = psd_safe_cholesky(cov)
+        shape = torch.Size(sample_shape) + self._mean.shape
+        if base_samples is None:
+            base_samples = torch.randn(shape, dtype=self._mean.dtype, device=self._mean.device)
+        elif base_samples.shape != shape:
+            raise RuntimeError(f"base_samples shape {tuple(base_samples.shape)} != {tuple(shape)}")
+        return self._mean + (root @ base_samples.unsqueeze(-1)).squeeze(-1)
+
+    def sample(self, sample_shape=torch.Size(), base_samples: Optional[torch.Tensor] = None) -> torch.Tensor:
+        with torch.no_grad():
+            return self.rsample(sample_shape, base_samples)
 
     def expand(self, batch_size):
         batch_size = torch.Size(batch_size)
         mean = self._mean.expand(*batch_size, *self.event_shape)
         var = self._variance.expand(*batch_size, *self.event_shape) if self._variance is not None else None
-        return MultivariateNormal(mean, var, self._exact, self._added_noise, self._clamp_flag,
-                                  self._preclamped)
+        exact = self._exact
+        if exact is not None:
+            # the prior's inputs follow the mean's batch, so covariance_matrix / log_prob of the
+            # expanded distribution see one input set per batch entry (GPyTorch expands the lazy
+            # kernel tensor the same way)
+            X = exact[0]
+            n, d = X.shape[-2:]
+            if X.numel() != self.batch_shape.numel() * n * d:
+                raise NotImplementedError("expand of an exact prior whose inputs do not follow its batch")
+            Xe = X.reshape(*self.batch_shape, n, d).expand(*batch_size, n, d).reshape(-1, n, d)
+            exact = (Xe,) + tuple(exact[1:])
+        return MultivariateNormal(mean, var, exact, self._added_noise, self._clamp_flag,
+                                  self._preclamped, self._covar_fn)
 
     def add_noise(self, noise):
         total = noise if self._added_noise is None else self._added_noise + noise
         return MultivariateNormal(self._mean, self._variance, self._exact, total, self._clamp_flag,
-                                  self._preclamped)
+                                  self._preclamped, self._covar_fn)
 
     def slice_points(self, start, stop):
         """The marginals of points [start, stop) (diagonal-query outputs of the variational
@@ -285,8 +328,10 @@ class MultivariateNormal:
         if self._exact is not None or self._variance is None:
             raise NotImplementedError("point slices are defined for variational outputs")
         sl = (Ellipsis, slice(start, stop))
+        cf = self._covar_fn
+        sub = (lambda: cf()[..., start:stop, start:stop]) if cf is not None else None
         return MultivariateNormal(self._mean[sl], self._variance[sl], None, self._added_noise, None,
-                                  preclamped=self._clamp_flag is not None or self._preclamped)
+                                  preclamped=self._clamp_flag is not None or self._preclamped, covar_fn=sub)
 
     def log_prob(self, value: torch.Tensor) -> torch.Tensor:
         """Exact-GP marginal log density (fused RBF + Cholesky + solve + logdet kernel)."""
@@ -319,6 +364,107 @@ def rbf_covariance(X: torch.Tensor, lengthscale, outputscale) -> torch.Tensor:
     d = d * (1.0 - torch.eye(X.shape[-2], device=X.device, dtype=X.dtype))
     s2 = torch.as_tensor(outputscale, device=X.device, dtype=X.dtype).reshape(())
     return s2 * torch.exp(-0.5 * d)
+
+
+def psd_safe_cholesky(A: torch.Tensor, max_tries: Optional[int] = None) -> torch.Tensor:
+    """Upstream linear_operator utils/cholesky.py psd_safe_cholesky for a dense matrix (the
+    covariance roots of rsample; the hot path's factorisations run in the gfx950 kernels):
+    torch.linalg.cholesky_ex, then up to max_tries retries with jitter 1e-6, 1e-5, ... (fp32;
+    1e-8.. for fp64) added to the diagonal, each retry warning NumericalWarning."""
+    L, info = torch.linalg.cholesky_ex(A)
+    if not bool((info > 0).any()):
+        return L
+    if torch.isnan(A).any():
+        from .errors import NanError
+        raise NanError(f"cholesky_cpu: {torch.isnan(A).sum().item()} of {A.numel()} elements of the "
+                       f"{tuple(A.shape)} tensor are NaN.")
+    jitter = settings.cholesky_jitter.value(A.dtype)
+    tries = settings.cholesky_max_tries.value() if max_tries is None else max_tries
+    Aprime = A.clone()
+    jitter_prev = 0.0
+    for i in range(tries):
+        jitter_new = jitter * (10 ** i)
+        Aprime.diagonal(dim1=-2, dim2=-1).add_(jitter_new - jitter_prev)
+        jitter_prev = jitter_new
+        warnings.warn(f"A not p.d., added jitter of {jitter_new:.1e} to the diagonal", NumericalWarning)
+        L, info = torch.linalg.cholesky_ex(Aprime)
+        if not bool((info > 0).any()):
+            return L
+    from .errors import NotPSDError
+    raise NotPSDError(f"Matrix not positive definite after repeatedly adding jitter up to {jitter_new:.1e}.")
+
+
+class MultitaskMultivariateNormal:
+    """Upstream distributions/multitask_multivariate_normal.py as a multi-output DeepGP layer
+    returns it (DeepGPLayer.__call__: ``MultitaskMultivariateNormal(output.loc.transpose(-1, -2),
+    BlockDiagLinearOperator(output.lazy_covariance_matrix, block_dim=-3), interleaved=False)``):
+    a batch of O independent per-output MultivariateNormals (batch (..., O), event N) viewed with
+    event shape (N, O). mean / variance are the per-output marginals transposed; the dense
+    covariance is block diagonal in task-major (non-interleaved) order; rsample draws every
+    output from its own full covariance."""
+
+    def __init__(self, base: MultivariateNormal):
+        self._base = base      # batch (..., O), event N
+
+    @classmethod
+    def from_batch_mvn(cls, batch_mvn: MultivariateNormal, task_dim: int = -1):
+        if task_dim not in (-1, batch_mvn._mean.dim() - 2):
+            raise NotImplementedError("the task dimension is the last batch dimension")
+        return cls(batch_mvn)
+
+    @property
+    def num_tasks(self):
+        return self._base.mean.shape[-2]
+
+    @property
+    def mean(self):
+        return self._base.mean.transpose(-1, -2)
+
+    @property
+    def loc(self):
+        return self.mean
+
+    @property
+    def variance(self):
+        return self._base.variance.transpose(-1, -2)
+
+    @property
+    def stddev(self):
+        return self.variance.sqrt()
+
+    @property
+    def batch_shape(self):
+        return self._base.mean.shape[:-2]
+
+    @property
+    def event_shape(self):
+        return self.mean.shape[-2:]
+
+    @property
+    def covariance_matrix(self):
+        blocks = self._base.covariance_matrix          # (..., O, N, N)
+        return torch.block_diag(*blocks.unbind(-3)) if blocks.dim() == 3 else \
+            torch.stack([torch.block_diag(*b.unbind(-3)) for b in blocks.reshape(-1, *blocks.shape[-3:])]) \
+            .reshape(*blocks.shape[:-3], blocks.shape[-3] * blocks.shape[-1], blocks.shape[-3] * blocks.shape[-1])
+
+    @property
+    def lazy_covariance_matrix(self):
+        return self.covariance_matrix
+
+    def expand(self, batch_size):
+        return MultitaskMultivariateNormal(self._base.expand(torch.Size(batch_size) + self._base.mean.shape[-2:-1]))
+
+    def add_noise(self, noise):
+        return MultitaskMultivariateNormal(self._base.add_noise(noise))
+
+    def rsample(self, sample_shape=torch.Size(), base_samples: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if base_samples is not None:
+            base_samples = base_samples.transpose(-1, -2)
+        return self._base.rsample(sample_shape, base_samples).transpose(-1, -2)
+
+    def sample(self, sample_shape=torch.Size(), base_samples: Optional[torch.Tensor] = None) -> torch.Tensor:
+        with torch.no_grad():
+            return self.rsample(sample_shape, base_samples)
 
 
 # ---------------------------------------------------------------------------

@@ -515,6 +515,10 @@ def variational_adjoint(X: torch.Tensor, Z: torch.Tensor, Linv: torch.Tensor, vm
     gvar = gvar.detach().reshape(B, N).contiguous().float()
     lib = _native.lib()
     if saved is not None:
+        # the C entry point receives a bare pointer: the dtype and device are checked here
+        if saved.dtype != torch.float32 or saved.device != dev:
+            raise ValueError(f"saved state must be float32 on {dev} (got {saved.dtype} on {saved.device}): "
+                             f"pass variational_forward(save=True).saved unchanged")
         if saved.numel() * 4 != lib.gpk_variational_saved_bytes(B, N, M, D):
             raise ValueError("saved state does not match this shape (variational_forward(save=True))")
         nbytes = lib.gpk_variational_adjoint_saved_workspace_bytes(B, N, M, D)

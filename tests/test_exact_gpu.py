@@ -207,8 +207,10 @@ def test_exact_cfg2_full_batch(cuda_device):
     assert np.max(np.abs(mll - ref.mll) / np.abs(ref.mll)) <= 1e-4
 
 
-def _cumulative_jitter(t):
-    """Total diagonal jitter after t rungs of the fp32 ladder (1e-6, 1e-5, ... added in turn)."""
+def _ladder_jitter(t):
+    """Diagonal jitter in force after t rungs of the fp32 ladder: the CURRENT rung 1e-6 * 10^(t-1)
+    (upstream psd_safe_cholesky adds only the difference from the previous rung at each retry,
+    so the total added equals the current rung, not a sum of rungs)."""
     return 1e-6 * 10 ** (t - 1) if t > 0 else 0.0
 
 
@@ -259,7 +261,7 @@ def test_exact_layout_ladder_and_failures(cuda_device, B, N, D, dup, nanw):
     assert np.max(np.abs(mll - ref.mll[ok]) / np.abs(ref.mll[ok])) <= 1e-4
     for b in dup:
         t = -int(info[b])
-        K = np.ones((N, N)) + _cumulative_jitter(t) * np.eye(N)
+        K = np.ones((N, N)) + _ladder_jitter(t) * np.eye(N)
         assert np.all(np.triu(L[b], 1) == 0.0)
         err = np.linalg.norm(L[b] @ L[b].T - K) / np.linalg.norm(K)
         assert err <= 1e-5, (b, t, err)

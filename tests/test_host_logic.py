@@ -245,3 +245,18 @@ def test_graphed_step_requires_capturable_optimizer_and_device():
     p = torch.nn.Parameter(torch.zeros(3))
     with pytest.raises((RuntimeError, ValueError)):
         GraphedStep(lambda x: (p * x).sum(), torch.optim.Adam([p]), (torch.ones(3),))
+
+
+def test_expanded_layer_prior_keeps_inputs_per_batch_entry():
+    """MultivariateNormal.expand carries the exact prior's inputs along the batch, so the
+    expanded prior's dense covariance is the unexpanded one repeated."""
+    from fine_grained_gaussian_process_forcasting_amd.denoising_model.DeepGP import ToyDeepGPHiddenLayer
+    layer = ToyDeepGPHiddenLayer(input_dims=3, output_dims=None, seed=1, num_inducing=8, mean_type='linear')
+    x = torch.randn(2, 5, 3)
+    prior = layer.forward(x)
+    K = prior.covariance_matrix
+    assert K.shape == (2, 5, 5)
+    pe = prior.expand(torch.Size([4, 2]))
+    Ke = pe.covariance_matrix
+    assert Ke.shape == (4, 2, 5, 5)
+    assert torch.equal(Ke, K.unsqueeze(0).expand(4, 2, 5, 5))

@@ -277,6 +277,20 @@ def test_custom_ops_opcheck(cuda_device):
     args = (X, Linv, Z, torch.zeros(M, device=dev), torch.ones(M, device=dev), s2, ls,
             torch.randn(D, generator=g).to(dev), torch.tensor(0.1, device=dev), 1e-4)
     torch.library.opcheck(torch.ops.gpk.variational_fwd.default, args, test_utils=tests)
+    # the training forward (save=True) at M > 64: its 5th output is the saved state whose size
+    # the fake impl takes from the native saved_bytes query; the state then feeds the adjoint
+    M2, N2 = 96, 40
+    X2 = (torch.randn(B, N2, D, generator=g) / 2).to(dev)
+    Z2 = (torch.randn(M2, D, generator=g) / 2).to(dev)
+    Linv2 = torch.ops.gpk.kzz_factor(Z2, s2, ls, 1e-4, 1e-8, 3)[0]
+    args2 = (X2, Linv2, Z2, 1e-3 * torch.randn(M2, generator=g).to(dev), torch.ones(M2, device=dev), s2, ls,
+             torch.randn(D, generator=g).to(dev), torch.tensor(0.1, device=dev), 1e-4, True)
+    torch.library.opcheck(torch.ops.gpk.variational_fwd.default, args2, test_utils=tests)
+    mean2, var2, _, hyp2, saved2 = torch.ops.gpk.variational_fwd(*args2)
+    assert saved2.numel() > 0 and saved2.dtype == torch.float32
+    adj_args = (X2, Linv2, Z2, args2[3], args2[4], hyp2, torch.randn_like(mean2), torch.randn_like(var2), saved2)
+    torch.library.opcheck(torch.ops.gpk.variational_adj.default, adj_args,
+                          test_utils=("test_schema", "test_faketensor"))
     # with gradients requested, the registered autograd formulas are exercised
     Xr = X.clone().requires_grad_(True)
     torch.library.opcheck(torch.ops.gpk.exact_mll.default, (Xr, y, h, 1e-6, 3, True),
