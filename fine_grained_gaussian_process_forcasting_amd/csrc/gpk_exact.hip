@@ -460,35 +460,56 @@ GPK_DEVICE f32x4 pan_self(const f32x4 v, f32x4 d) { return mma_tn(v, v, d); }
 GPK_DEVICE f32x4 pan_mma_op(const pan_op_t q, const pan_op_t p, f32x4 d) { return mma_tn(q, p, d); }
 #endif
 
+// Lane moves of the sweep operand (one wave, no LDS round trip): x of the odd rows in the
+// even rows' lanes (row 1 -> 0, 3 -> 2; permlane16_swap, new src0) and of rows 2, 3 in rows
+// 0, 1 (permlane32_swap, new src0).
+GPK_DEVICE float from_odd_row_f(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  return __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_permlane16_swap(u, u, false, false)[1]);
+}
+GPK_DEVICE float from_upper_half_f(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  return __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_permlane32_swap(u, u, false, false)[1]);
+}
+
 // Factor one 16x16 diagonal tile T in ONE wave (the diagonal wave).
 //   lanes  0-15 (column c): v[m] <- R[m][c]             (R^T R = T, upper)
 //   lanes 16-31 (column c): v[m] <- W[m][c], W = R^{-T}  (lower), started from I
 // from one instruction stream: at step m every lane does
 //   v[m] *= rsqrt(pivot);   v[i] -= R[m][i] * v[m]   (i > m)
-// with R[m][i] broadcast from R-lane i by readlane. `tile` holds -T in acc
-// layout. -W (transposed: wbuf[c*kWS+m] = -W[m][c]) is published FIRST together
-// with the pass/fail verdict (every pivot checked positive-finite on the scalar
-// broadcast: v_cmp_class), then the factor-done flag is raised; only then the L
-// diagonal block, the exact failing column and log|T| are produced.
+// with R[m][i] broadcast from R-lane i by DPP. `t` holds -T in acc layout IN REGISTERS
+// (lane 16 g + c: rows 4 g + r of column c); lane c gathers its column by permlane swaps.
+// -W (transposed: wbuf[c*kWS+m] = -W[m][c]) is published FIRST together with the pass/fail
+// verdict (every pivot checked positive-finite), then the factor-done flag is raised. The L
+// diagonal block and log|T| come later, from `v` and `dg`, in diag_finish: the caller issues
+// them under the next look-ahead's MFMAs instead of ahead of them.
 template <bool ST, bool FULL>
-GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_vint* fail_flag,
-                           int epoch, float* Lb, int N, int row0, float inv_sigma, float& logdet,
-                           unsigned long long* dst = nullptr) {
+GPK_DEVICE int diag_factor(const f32x4 t, float (&v)[16], float& dg, float* wbuf, lds_vint* flags,
+                           lds_vint* fail_flag, int epoch, const float* tile, unsigned long long* dst = nullptr) {
   unsigned long long t0 = 0;
   if constexpr (ST) t0 = __builtin_amdgcn_s_memtime();
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));  // keep per-lane masks local to this call
   const int c = lane & 15, grp = lane >> 4;
-  float v[16];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 t = *(const f32x4*)&tile[(16 * g + c) * 4];
+  if (GPK_DIAG_PERMLANE) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = 4 * g + r;
-      v[i] = (grp == 0) ? -t[r] : ((grp == 1 && i == c) ? 1.f : 0.f);
+      const float a2 = from_upper_half_f(t[r]);     // rows 2, 3 -> rows 0, 1
+      v[r] = t[r];
+      v[4 + r] = from_odd_row_f(t[r]);
+      v[8 + r] = a2;
+      v[12 + r] = from_odd_row_f(a2);
+    }
+  } else {   // (A/B: the same gather through the tile in LDS)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 u = *(const f32x4*)&tile[(16 * g + c) * 4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[4 * g + r] = u[r];
     }
   }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = (grp == 0) ? -v[i] : ((grp == 1 && i == c) ? 1.f : 0.f);
   if constexpr (ST) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -515,7 +536,7 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
       *(f32x4*)&wbuf[c * kWS + 4 * g] = f32x4{-v[4 * g], -v[4 * g + 1], -v[4 * g + 2], -v[4 * g + 3]};
   }
   // diagonal of R (lane c < 16 holds R[c][c] in v[c])
-  float dg = v[0];
+  dg = v[0];
 #pragma unroll
   for (int i = 1; i < 16; ++i) dg = (c == i) ? v[i] : dg;
   const bool okd = (dg > 0.f) && (dg < __builtin_huge_valf());
@@ -534,9 +555,18 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
     if (lane == 0) dst[2] += t1 - t0;
     __builtin_amdgcn_sched_barrier(0);
   }
-  const int fail = badm ? __builtin_ctzll(badm) + 1 : 0;
-  // per-lane partial log2|T| (lanes 0-15); reduced across lanes once, at the end
-  // (a per-step shuffle reduction is 4 LDS round trips on the critical path)
+  return badm ? __builtin_ctzll(badm) + 1 : 0;
+}
+
+// The rest of a factored diagonal step, off the chain: per-lane partial log2|T| (lanes 0-15;
+// reduced across lanes once, at the end -- a per-step shuffle reduction is 4 LDS round trips)
+// and L's diagonal block from the R lanes.
+template <bool FULL>
+GPK_DEVICE void diag_finish(float (&v)[16], float dg, float* Lb, int N, int row0, float inv_sigma,
+                            float& logdet) {
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int c = lane & 15, grp = lane >> 4;
   logdet += (lane < 16) ? __builtin_amdgcn_logf(dg * dg) : 0.f;
   if (grp == 0) {
     // R lanes: zero below-diagonal garbage, write L[row0 + c][row0 + m] = R[m][c]
@@ -550,7 +580,6 @@ GPK_DEVICE int diag_factor(const float* tile, float* wbuf, lds_vint* flags, lds_
                f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]} * inv_sigma);
     }
   }
-  return fail;
 }
 
 // ---------------------------------------------------------------------------
@@ -1668,6 +1697,9 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
       logdet = 0.f;
       failed = 0;
       spin_until(vflag, kFlagT00, 32 * attempt);
+      // the tile being factored, acc layout in registers: (0,0) from the worker that built it,
+      // then each look-ahead's (k+1,k+1) straight from its MFMAs
+      f32x4 tcur = *(const f32x4*)&dsc[lane * 4];
       for (int k = 0; k < NB; ++k) {
         const int epoch = 32 * attempt + k;
         float* wb = wbuf + (k % 3) * kWBuf;
@@ -1679,9 +1711,9 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
             flag[17] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
           }
         }
-        const int f = diag_factor<STAMPS, FULL>(dsc, wb, vflag, vflag + kFlagFail + attempt, epoch, Lb, N,
-                                          16 * k, inv_sigma, logdet,
-                                          (unsigned long long*)(red + 4 * W + 32));
+        float dv[16], dg;
+        const int f = diag_factor<STAMPS, FULL>(tcur, dv, dg, wb, vflag, vflag + kFlagFail + attempt, epoch, dsc,
+                                                (unsigned long long*)(red + 4 * W + 32));
         if constexpr (STAMPS) {
           const unsigned long long dt1 = __builtin_amdgcn_s_memtime();
           if (lane == 0) {
@@ -1696,10 +1728,19 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
           if (lane == 0) vflag[kFlagFail + attempt] = failed;
           break;
         }
-        if (k == NB - 1) break;
+        if (k == NB - 1) {
+          diag_finish<FULL>(dv, dg, Lb, N, 16 * k, inv_sigma, logdet);
+          break;
+        }
         // look-ahead: R_{k,k+1} = R_kk^{-T} T'_{k,k+1}, then the last update of
         // (k+1,k+1); both tiles arrive (updated through panel k-1) in hbuf[k & 1]
         const float* hk = hbuf + (k & 1) * 512;
+        // R_kk^{-T} back in the MFMA A layout (this wave's own LDS writes: no flag needed, and
+        // the read is in flight while the wave waits for the hand-over)
+        const f32x4 q = load_w(wb, c, grp);
+        // step k's L block and log|T|: ahead of the wait (in the in-order wave, work after the
+        // wait sits on the chain)
+        if (!GPK_DIAG_FINISH_LATE) diag_finish<FULL>(dv, dg, Lb, N, 16 * k, inv_sigma, logdet);
         unsigned long long hw0 = 0;
         if constexpr (STAMPS) hw0 = __builtin_amdgcn_s_memtime();
         spin_until(vflag, kFlagHA + (k & 1), epoch);
@@ -1713,11 +1754,12 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
           hw0 = hw1;
         }
         GPK_EP(epoch_expect(vflag, kShadowHo + 2 * (k & 1), epoch, 30); epoch_expect(vflag, kShadowHo + 2 * (k & 1) + 1, epoch, 31);)
-        const f32x4 q = load_w(wb, c, grp);
         const f32x4 ta = *(const f32x4*)&hk[lane * 4];
         f32x4 tb = *(const f32x4*)&hk[256 + lane * 4];
         tb = pan_self(trsm_tile(w_split(q), ta), tb);
-        *(f32x4*)&dsc[lane * 4] = tb;
+        if (GPK_DIAG_FINISH_LATE) diag_finish<FULL>(dv, dg, Lb, N, 16 * k, inv_sigma, logdet);
+        tcur = tb;
+        if (!GPK_DIAG_PERMLANE) *(f32x4*)&dsc[lane * 4] = tb;
         if constexpr (STAMPS) {
           const unsigned long long hw2 = __builtin_amdgcn_s_memtime();
           if (lane == 0) {

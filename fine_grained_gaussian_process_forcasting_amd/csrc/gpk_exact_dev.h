@@ -26,6 +26,15 @@
 #ifndef GPK_DIAG_DPP
 #define GPK_DIAG_DPP 1   // diagonal sweep as DPP-broadcast FMAs (gpk_diag_dpp.inc); 0 = readlane form
 #endif
+#ifndef GPK_DIAG_PERMLANE
+#define GPK_DIAG_PERMLANE 0   // 1: the diagonal wave gathers its sweep operand by permlane swaps from the
+                              // look-ahead's registers (measured 0.6-0.8 us SLOWER per launch at B = 64 / 128);
+                              // 0: through its LDS tile
+#endif
+#ifndef GPK_DIAG_FINISH_LATE
+#define GPK_DIAG_FINISH_LATE 0   // 1: step k's L block + log|T| after the look-ahead MFMAs (measured
+                                 // slower: the in-order wave puts them on the chain); 0: before the wait
+#endif
 #ifndef GPK_EXACT_COL
 #define GPK_EXACT_COL 1   // 1: column-ownership worker plan for N = 256 at 8 waves (worker_step_col)
 #endif

@@ -20,23 +20,27 @@ import torch
 import torch.nn as nn
 
 from ..gp import (ConstantMean, GaussianLikelihood, LinearMean, MeanFieldVariationalDistribution,
-                  MultivariateNormal, RBFKernel, ScaleKernel, VariationalStrategy,
-                  _DeepGPVariationalStrategy, settings)
+                  MultitaskMultivariateNormal, MultivariateNormal, RBFKernel, ScaleKernel,
+                  VariationalStrategy, _DeepGPVariationalStrategy, settings)
 
 
 class ToyDeepGPHiddenLayer(nn.Module):
-    """Reference DeepGP.py:14-73 (output_dims=None is the only configuration used)."""
+    """Reference DeepGP.py:14-73. output_dims=None (what DeepGPp builds) gives one GP; an
+    integer O gives O independent output GPs (inducing points (O, M, D), q(u) and kernel
+    hyper-parameters batched over O) whose output is a MultitaskMultivariateNormal with event
+    shape (N, O), as GPyTorch's DeepGPLayer returns it."""
 
     def __init__(self, input_dims, output_dims, seed, num_inducing=256, mean_type='constant'):
         super().__init__()
         np.random.seed(seed)
         random.seed(seed)
         torch.manual_seed(seed)
-        if output_dims is not None:
-            raise NotImplementedError("multi-output DeepGP layers are not on the reference path "
-                                      "(DeepGPp uses output_dims=None, DeepGP.py:77-82)")
-        inducing_points = torch.randn(num_inducing, input_dims)          # DeepGP.py:22
-        batch_shape = torch.Size([])
+        if output_dims is None:
+            inducing_points = torch.randn(num_inducing, input_dims)          # DeepGP.py:22
+            batch_shape = torch.Size([])
+        else:
+            inducing_points = torch.randn(output_dims, num_inducing, input_dims)   # DeepGP.py:25
+            batch_shape = torch.Size([output_dims])
         variational_distribution = MeanFieldVariationalDistribution(num_inducing, batch_shape)
         self.variational_strategy = VariationalStrategy(self, inducing_points, variational_distribution,
                                                         learn_inducing_locations=True)
@@ -71,17 +75,33 @@ class ToyDeepGPHiddenLayer(nn.Module):
         expanded again. Otherwise the deterministic inputs give q(f) with batch (..., )
         expanded to (S, ...), S = settings.num_likelihood_samples (1 under train.py:20).
         Both mean types run on the fused kernel: ConstantMean is LinearMean with w = 0
-        and b0 = the constant (ops_autograd.variational_predict)."""
+        and b0 = the constant (ops_autograd.variational_predict).
+
+        A MultitaskMultivariateNormal ``x`` (a multi-output layer's output): with skip inputs it
+        is ``rsample()``d from its full covariance first (DeepGP.py:62-64); alone it is sampled
+        from its marginals, as DeepGPLayer.__call__ does (``Normal(mean, variance.sqrt())``), and
+        the output is then not expanded. A layer with output_dims = O runs its O output GPs on
+        the inputs expanded to (..., O, N, D) and returns q(f) as a MultitaskMultivariateNormal."""
         are_samples = bool(len(other_inputs))
         S = settings.num_likelihood_samples.value()
         if are_samples:
+            if isinstance(x, MultitaskMultivariateNormal):
+                x = x.rsample()
             processed = [inp.unsqueeze(0).expand(S, *inp.shape) for inp in other_inputs]
             x = torch.cat([x] + processed, dim=-1)
+        deterministic = not are_samples
+        if isinstance(x, MultitaskMultivariateNormal):
+            x = torch.distributions.Normal(loc=x.mean, scale=x.variance.sqrt()).rsample()
+            deterministic = False
         if x.size(-1) != self.input_dims:
             raise RuntimeError(f"Input shape did not match self.input_dims. Got total feature dims "
                                f"[{x.size(-1)}], expected [{self.input_dims}]")
+        if self.output_dims is not None:
+            x = x.unsqueeze(-3).expand(*x.shape[:-2], self.output_dims, *x.shape[-2:])
         output = self.variational_strategy(x)
-        if are_samples:
+        if self.output_dims is not None:
+            output = MultitaskMultivariateNormal.from_batch_mvn(output, task_dim=-1)
+        if not deterministic:
             return output
         return output.expand(torch.Size([S]) + output.batch_shape)
 

@@ -273,9 +273,8 @@ class MultivariateNormal:
             K = K + torch.diag_embed(torch.as_tensor(self._added_noise, dtype=K.dtype, device=K.device)
                                      .expand(K.shape[:-1]))
         n = self._mean.shape[-1]
-        if K.numel() != self._mean.numel() * n:   # an expanded distribution: the batch is a view
-            K = K.reshape(-1, *self._mean.shape[-1:], n).expand(*self._mean.shape, n) if K.dim() == 2 else \
-                K.expand(*self._mean.shape, n)
+        if K.numel() != self._mean.numel() * n:   # an expanded distribution: its batch is a view
+            K = K.expand(*self._mean.shape, n)
         return K.reshape(*self._mean.shape, n)
 
     @property
@@ -546,6 +545,43 @@ class MeanFieldVariationalDistribution(nn.Module):
         return 0.5 * (s2.sum(-1) + m.pow(2).sum(-1) - m.shape[-1] - s2.log().sum(-1))
 
 
+class _MeanOutput:
+    """Output o's view of a layer mean (DeepGP.py:42-45): ConstantMean(batch_shape=[O]) has one
+    constant per output, the reference's LinearMean(input_dims) one weight vector for all."""
+
+    def __init__(self, mean_module, o):
+        if hasattr(mean_module, "weights"):
+            w = mean_module.weights
+            self.weights = w[o] if w.dim() == 3 else w
+            b = mean_module.bias
+            self.bias = (b[o] if b.dim() == 2 else b) if b is not None else None
+        elif hasattr(mean_module, "constant"):
+            c = mean_module.constant
+            self.constant = c[o] if c.dim() == 2 else c
+        else:
+            raise NotImplementedError(f"mean module {type(mean_module).__name__}")
+
+
+def variational_dense_covariance(x, Z, Linv, vstd, outputscale, lengthscale, jitter):
+    """The full predictive covariance of q(f) at x (B', N, D), as upstream
+    VariationalStrategy.forward (whitened) builds it lazily: K_XX + jitter I + A^T (S - I) A with
+    A = L^{-1} K_ZX solved in fp64 and cast back (``L.solve(induc_data_covar.double())``),
+    S = diag(stddev^2). Dense torch arithmetic on request (covariance_matrix / rsample) -- the
+    hot path reads the marginals from the kernels and never calls this."""
+    ls = lengthscale.reshape(-1)
+    s2 = outputscale.reshape(())
+    Kxx = rbf_covariance(x, ls, s2)
+    zs = (Z / ls).double()
+    xs = (x / ls).double()
+    d = (zs.pow(2).sum(-1)[:, None] + xs.pow(2).sum(-1).unsqueeze(-2)
+         - 2.0 * zs @ xs.transpose(-1, -2)).clamp_min(0.0)             # (B', M, N)
+    Kzx = s2.double() * torch.exp(-0.5 * d)
+    A = (Linv.double() @ Kzx).to(x.dtype)
+    mid = (vstd.reshape(-1).pow(2) - 1.0).to(x.dtype)
+    eye = torch.eye(x.shape[-2], dtype=x.dtype, device=x.device)
+    return Kxx + jitter * eye + A.transpose(-1, -2) @ (mid[:, None] * A)
+
+
 class VariationalStrategy(nn.Module):
     """Whitened VariationalStrategy for one DeepGP layer (output_dims=None).
 
@@ -571,14 +607,19 @@ class VariationalStrategy(nn.Module):
         self._initialized = False     # host mirror of the buffer: no device sync per call
         from .ops_autograd import KzzCache
         self._kzz_cache = KzzCache()
+        self._kzz_caches = []            # multi-output layers: one cache per output
 
     def _load_from_state_dict(self, *args, **kwargs):
         super()._load_from_state_dict(*args, **kwargs)
         self._initialized = bool(int(self.variational_params_initialized))
         self._kzz_cache.clear()
+        for c in self._kzz_caches:
+            c.clear()
 
     def train(self, mode: bool = True):
         self._kzz_cache.clear()      # GPyTorch clears its cholesky cache on mode switches
+        for c in self._kzz_caches:
+            c.clear()
         return super().train(mode)
 
     @property
@@ -596,19 +637,73 @@ class VariationalStrategy(nn.Module):
             self._variational_distribution.initialize_variational_distribution()
             self.variational_params_initialized.fill_(1)
             self._initialized = True
+        if self.inducing_points.dim() == 3:
+            return self._call_batched(x)
         model = self.model
         batch = x.shape[:-2]
         N, D = x.shape[-2:]
         xf = x.reshape(-1, N, D)
-        from .ops_autograd import variational_predict
         kern = model.covar_module
         key = (self.inducing_points, kern.raw_outputscale, kern.base_kernel.raw_lengthscale)
-        mean, var, flag = variational_predict(
-            xf, self.inducing_points, self._variational_distribution.variational_mean,
-            self._variational_distribution._variational_stddev,
-            kern.outputscale, kern.base_kernel.lengthscale,
-            model.mean_module, self._jitter(x.dtype), cache=self._kzz_cache, key_tensors=key)
-        return MultivariateNormal(mean.reshape(*batch, N), var.reshape(*batch, N), clamp_flag=flag)
+        q = self._variational_distribution
+        mean, var, flag, cov = self._predict_one(
+            xf, self.inducing_points, q.variational_mean, q._variational_stddev, kern.outputscale,
+            kern.base_kernel.lengthscale, model.mean_module, self._jitter(x.dtype), self._kzz_cache, key)
+        return MultivariateNormal(mean.reshape(*batch, N), var.reshape(*batch, N), clamp_flag=flag,
+                                  covar_fn=lambda: cov().reshape(*batch, N, N))
+
+    @staticmethod
+    def _predict_one(xf, Z, vmean, vstd, outputscale, lengthscale, mean_module, jitter, cache, key):
+        """q(f) of one output on the kernels + a lazy dense covariance for covariance_matrix /
+        rsample (upstream VariationalStrategy.forward's predictive_covar)."""
+        from .ops_autograd import variational_predict
+        mean, var, flag, Linv = variational_predict(
+            xf, Z, vmean, vstd, outputscale, lengthscale, mean_module, jitter, cache=cache,
+            key_tensors=key, return_linv=True)
+
+        def cov():
+            return variational_dense_covariance(xf, Z, Linv, vstd, outputscale, lengthscale, jitter)
+        return mean, var, flag, cov
+
+    def _call_batched(self, x: torch.Tensor) -> MultivariateNormal:
+        """Multi-output layer (output_dims = O, DeepGP.py:24-26): inducing points (O, M, D), q(u)
+        batch (O,), kernel hyper-parameters per output; x (..., O, N, D) as DeepGPLayer.__call__
+        expands it. The O outputs are independent GPs: one K_ZZ factor (cached per output) and
+        one variational launch each. Returns the batch (..., O) of per-output q(f)."""
+        Z = self.inducing_points
+        O, M, D = Z.shape
+        if x.dim() < 3 or x.shape[-3] != O:
+            raise RuntimeError(f"a layer with {O} outputs takes inputs (..., {O}, N, D); got {tuple(x.shape)}")
+        batch = x.shape[:-3]
+        N = x.shape[-2]
+        model = self.model
+        kern = model.covar_module
+        q = self._variational_distribution
+        if len(self._kzz_caches) != O:
+            from .ops_autograd import KzzCache
+            self._kzz_caches = [KzzCache() for _ in range(O)]
+        key = (Z, kern.raw_outputscale, kern.base_kernel.raw_lengthscale)
+        s2 = kern.outputscale.reshape(O)
+        ls = kern.base_kernel.lengthscale.reshape(O, -1)
+        vm = q.variational_mean.reshape(O, M)
+        vs = q._variational_stddev.reshape(O, M)
+        means, variances, flags, covs = [], [], [], []
+        for o in range(O):
+            xo = x[..., o, :, :].reshape(-1, N, D)
+            m, v, f, c = self._predict_one(xo, Z[o], vm[o], vs[o], s2[o], ls[o], _MeanOutput(model.mean_module, o),
+                                           self._jitter(x.dtype), self._kzz_caches[o], key)
+            means.append(m.reshape(*batch, N))
+            variances.append(v.reshape(*batch, N))
+            flags.append(f)
+            covs.append(c)
+        flag = flags[0]
+        for f in flags[1:]:
+            flag = torch.bitwise_or(flag, f)
+
+        def cov():
+            return torch.stack([c().reshape(*batch, N, N) for c in covs], dim=-3)
+        return MultivariateNormal(torch.stack(means, dim=-2), torch.stack(variances, dim=-2), clamp_flag=flag,
+                                  covar_fn=cov)
 
 
 # ---------------------------------------------------------------------------
@@ -645,7 +740,8 @@ class VariationalELBO(_ApproximateMarginalLogLikelihood):
         (gpk::variational_elbo) when the terms are the hot path's: a Gaussian likelihood, a
         variational output of the kernels, one unbatched mean-field strategy. Same warnings as
         the unfused expression (the variance clamp flag)."""
-        if not self.combine_terms or not isinstance(self.likelihood, GaussianLikelihood):
+        if (not self.combine_terms or not isinstance(self.likelihood, GaussianLikelihood)
+                or not isinstance(dist, MultivariateNormal)):
             return None
         # the fused op takes one scalar noise and returns no target gradient: a batched noise
         # model or a target that requires grad takes the unfused path

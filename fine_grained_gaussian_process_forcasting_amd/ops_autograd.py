@@ -131,9 +131,10 @@ def _mean_params(mean_module, D, device):
 
 
 def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module, jitter,
-                        cache: Optional[KzzCache] = None, key_tensors=None):
+                        cache: Optional[KzzCache] = None, key_tensors=None, return_linv: bool = False):
     """q(f) mean / variance / clamp flag for (B, N, D) windows (HIP forward and backward;
-    see module docstring). ``cache`` shares the K_ZZ factor between calls."""
+    see module docstring). ``cache`` shares the K_ZZ factor between calls; ``return_linv``
+    appends the factor's L^{-1} (for a lazily materialised covariance)."""
     w, b0 = _mean_params(mean_module, x.shape[-1], x.device)
     s2 = outputscale.reshape(())
     ls = lengthscale.reshape(-1)
@@ -149,4 +150,6 @@ def variational_predict(x, Z, vmean, vstd, outputscale, lengthscale, mean_module
                                                            float(jitter), save)
     cache.note_consumers(mean, var)
     cache.check_pending()
+    if return_linv:
+        return mean, var, flags, Linv
     return mean, var, flags

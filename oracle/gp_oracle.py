@@ -314,6 +314,24 @@ def variational_forward(X, Z, lengthscale, outputscale, weights, bias, m, s,
     return VariationalResult(mean.astype(dtype), var, L, A, int(res.jitter_steps))
 
 
+def variational_covariance(X, Z, lengthscale, outputscale, s, jitter=1e-4, dtype=np.float64):
+    """The full predictive covariance of q(f) that ``VariationalStrategy.forward`` (whitened)
+    builds lazily (upstream variational_strategy.py: ``SumLinearOperator(data_data_covar
+    .add_jitter(jitter), MatmulLinearOperator(interp_term^T, (S - I) interp_term))``):
+    K_XX + jitter I + A^T diag(s^2 - 1) A per window, A = L^{-1} K_ZX from the fp64 factor.
+    What ``MultivariateNormal.rsample`` / ``covariance_matrix`` of a DeepGP layer output
+    (DeepGP.py:62-64 ``x.rsample()``) factor."""
+    X = np.asarray(X, dtype=dtype)
+    res = variational_forward(X, Z, lengthscale, outputscale, np.zeros(X.shape[-1]), 0.0,
+                              np.zeros(np.asarray(Z).shape[0]), s, jitter=jitter, dtype=dtype)
+    ls = np.asarray(lengthscale, dtype=dtype).reshape(-1)
+    Kxx = np.stack([rbf(x, x, ls, outputscale, x1_eq_x2=True) for x in X])
+    s2m1 = np.asarray(s, dtype=dtype) ** 2 - 1.0
+    A = res.A
+    N = X.shape[-2]
+    return Kxx + dtype(jitter) * np.eye(N, dtype=dtype) + np.einsum('bmi,m,bmj->bij', A, s2m1, A)
+
+
 def expected_log_prob(y, mean, var, noise):
     """GaussianLikelihood.expected_log_prob: -0.5 [((y-mu)^2 + v)/s2n + log s2n + log 2pi]."""
     return -0.5 * (((y - mean) ** 2 + var) / noise + np.log(noise) + LOG_2PI)
