@@ -1698,343 +1698,6 @@ gpk_var_adjk_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 
 
 // ---------------------------------------------------------------------------
-// Adjoint for M > 64 from the training forward's saved state (gpk_variational_train_f32):
-// ONE kernel in the adjk layout (wave w holds the L^{-1} COLUMN blocks of block rows
-// pA = w, pB = MB-1-w). Per chunk: A (fp32, LSaved layout) straight into the LDS dA tiles,
-// the clamp mask onto gvar; each wave turns ITS rows of A into dA = gmean m + 2 gvar (s^2 - 1) A
-// in place (with the dvmean / dvstd row sums); then dK = L^{-T} dA, K_ZX of the wave's rows
-// recomputed straight into registers (f32 MFMA, zs rows fed in pi order so the tile lands in the
-// f64 C layout of dK; computed after the GEMM, where it does not push L^{-1} into scratch),
-// Q = dK o K and the rest exactly as gpk_var_adjk_l_kernel. dL^{-1} no longer comes from a dA / K_ZX
-// workspace: gpk_var_kgram_l_kernel accumulates G' = A diag(gvar) K_ZX^T and u = K_ZX gmean from
-// the same saved A (below). LDS: the adjk geometry; rows / xn / gvar live in its misc area.
-// ---------------------------------------------------------------------------
-template <int MB, int DQ>
-__global__ void __launch_bounds__(64 * ((MB + 1) / 2), 2)
-gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
-                      const double* __restrict__ Linv, const float* __restrict__ vmean,
-                      const float* __restrict__ vstd, const float* __restrict__ hyp,
-                      const float* __restrict__ gmean, const float* __restrict__ gvar,
-                      const float* __restrict__ saved, int N, int M, int D, int nchunks,
-                      float* __restrict__ wspart, float* __restrict__ dX, float* __restrict__ cm_out) {
-  using G = LAdjGeo<MB, DQ>;
-  using SV = LSaved<MB>;
-  constexpr int NWV = G::NWV, NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV, NDT = G::NDT;
-  constexpr int NU = SV::tiles / 4;                 // f32x4 units of A per chunk
-  static_assert(NU % NT == 0, "A block: whole passes");
-  extern __shared__ __attribute__((aligned(16))) float vsm[];
-  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4, sub = tid & 15;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pA = wave, pB = MB - 1 - wave;
-  const bool two = pB != pA;
-  const float s2 = hyp[0];
-  const float* w = hyp + 4;
-  const float* ls = hyp + 4 + D;
-  const int nch = (N + LTW - 1) / LTW;
-  // rows (dvm | dsm accumulators), xn and gvar (chunk parity) live in the epilogue's misc area
-  constexpr int oRows = G::kMisc, oXn = G::kMisc + 2 * G::MP, oGv = oXn + 2 * LTW;
-  static_assert(2 * G::MP + 4 * LTW <= 2 * NT + NWV, "misc area");
-
-  // L^{-1} column blocks, k-order g + 4u (as gpk_var_adjk_l_kernel)
-  double Lc[MB + 1][4];
-  {
-    const bool full = (M & 15) == 0;
-    const int NA = MB - pA;
-#pragma unroll
-    for (int s = 0; s <= MB; ++s) {
-      const bool isA = s < NA;
-      const int P = isA ? pA : pB, rt = isA ? pA + s : pB + (s - NA);
-      const bool ok = isA || (two && rt < MB);
-      const int col = 16 * P + c;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int row = 16 * rt + g + 4 * u;
-        const bool in = ok && (full || (row < M && col < M));
-        const double v = Linv[in ? (size_t)row * M + col : 0];
-        Lc[s][u] = in ? v : 0.0;
-      }
-      if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  float lsr[DV];
-#pragma unroll
-  for (int v = 0; v < DV; ++v) lsr[v] = ls[sub + 16 * v < D ? sub + 16 * v : 0];
-  float xr[NPASS][DV];
-  lload_points<NPASS, DV, NT>(X, blockIdx.x, nchunks, nch, N, D, xr);
-  stage_inducing(Z, ls, vmean, vstd, M, D, G::MP, DQ, DS, vsm + G::kZs, vsm + G::kZn, vsm + G::kCm,
-                 vsm + G::kVm, vsm + G::kSm1, vsm + G::kKl);
-  for (int e = tid; e < G::MP; e += NT) vsm[G::kQ + e] = 0.f;
-  for (int e = tid; e < 2 * G::MP; e += NT) vsm[oRows + e] = 0.f;
-  // A blocks are copied global -> LDS by LDS-DMA (global_load_lds, no registers), double-buffered
-  // over the adjk geometry's dA and K_ZX tile areas (K_ZX lives in registers here): the copy for
-  // chunk t + grid is issued before chunk t's GEMM and retired at chunk t + grid's first barrier
-  auto copy_a = [&](int t, float* buf) {
-    const float* sb = saved + (size_t)t * SV::blk;
-#pragma unroll
-    for (int q = 0; q < NU / NT; ++q) {
-      const int u0 = (q * NWV + wave) * 64;   // this wave-instruction's 64 units (1 KiB)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(sb + 4 * (u0 + lane)),
-                                       (__attribute__((address_space(3))) void*)(buf + 4 * u0), 16, 0, 0);
-    }
-  };
-  copy_a(blockIdx.x, vsm + G::kdA);
-  lds_barrier();
-  if (blockIdx.x == 0 && tid < D) cm_out[tid] = vsm[G::kCm + tid];   // the finisher's centre
-  float cmr[DV];
-#pragma unroll
-  for (int v = 0; v < DV; ++v) cmr[v] = vsm[G::kCm + sub + 16 * v];
-  const int dd = tid % DQ;   // the dX phase's dim for this thread (NT % DQ == 0)
-  const float il_dd = dd < D ? 1.f / ls[dd < D ? dd : 0] : 0.f;
-  const float w_dd = dd < D ? w[dd < D ? dd : 0] : 0.f;
-  float rx2 = 0.f, gxa = 0.f, sumQ = 0.f, sumgm = 0.f, sumgv = 0.f;
-  f32x4 qx[2][NDT];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) qx[h][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int par = 0;
-
-  for (int t = blockIdx.x; t < nchunks; t += gridDim.x, par ^= 1) {
-    const int b = t / nch, i0 = (t - b * nch) * LTW;
-    const int nvalid = N - i0 < LTW ? N - i0 : LTW;
-    const long long col0 = (long long)b * N + i0;
-    float* sm = (float*)fresh_lds(vsm);
-    float* dAl = sm + (par ? G::kKl : G::kdA);
-    float* xzl = sm + G::kXz;
-    float* red = sm + G::kRed;
-    const float* zs = sm + G::kZs;
-    const float* zn = sm + G::kZn;
-    const float* vm = sm + G::kVm;
-    const float* sm1 = sm + G::kSm1;
-    float* qrow = sm + G::kQ;
-    float* scr = sm + G::kScr + wave * 320;
-    float* xs = sm + G::kXs + par * LTW * DS;
-    float* xn = sm + oXn + par * LTW;
-    float* gmc = sm + G::kGm + par * LTW;
-    float* gvc = sm + oGv + par * LTW;
-    float* rows = sm + oRows;
-    // ---- the chunk's A tiles are (being) copied into dAl; points; gmean / gvar
-    {
-      const float* sb = saved + (size_t)t * SV::blk;
-      if (tid < LTW) {
-        const bool ok = tid < nvalid;
-        const float keep = sb[SV::tiles + tid];
-        const float gm = gmean[ok ? col0 + tid : 0], gv = gvar[ok ? col0 + tid : 0];
-        const float gvk = (ok && keep != 0.f) ? gv : 0.f;
-        gmc[tid] = ok ? gm : 0.f;
-        gvc[tid] = gvk;
-        sumgm += ok ? gm : 0.f;
-        sumgv += gvk;
-      }
-    }
-    lstage_points<NPASS, DV, NT, DS>(xr, lsr, cmr, D, nvalid, xs, xn);
-    if (t + (int)gridDim.x < nchunks) lload_points<NPASS, DV, NT>(X, t + gridDim.x, nchunks, nch, N, D, xr);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's A copy has landed
-    lds_barrier();
-    // ---- the wave's own rows: row sums of A, A -> dA in place
-    {
-      float gmq[2], gvq[2];
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        gmq[ct] = gmc[16 * ct + c];
-        gvq[ct] = gvc[16 * ct + c];
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !two) break;
-        const int rt = h == 0 ? pA : pB;
-        float pm[4] = {0.f, 0.f, 0.f, 0.f}, ps[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          float* at = dAl + ((rt * 2 + ct) * 64 + lane) * 4;
-          const f32x4 av = *(const f32x4*)at;
-          f32x4 da;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int p = 16 * rt + g + 4 * r;
-            pm[r] = __builtin_fmaf(gmq[ct], av[r], pm[r]);
-            ps[r] = __builtin_fmaf(gvq[ct], av[r] * av[r], ps[r]);
-            da[r] = gmq[ct] * vm[p] + 2.f * gvq[ct] * sm1[p] * av[r];
-          }
-          *(f32x4*)at = da;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float a = row16_sum_f(pm[r]), q = row16_sum_f(ps[r]);
-          if (c == 0) {
-            const int p = 16 * rt + g + 4 * r;
-            lds_acc(rows + p, a);
-            lds_acc(rows + G::MP + p, q);
-          }
-        }
-      }
-    }
-    lds_barrier();
-    // ---- dK = L^{-T} dA on the wave's block rows; Q = dK o K
-    f32x4 Qt[2][2];
-    {
-      f64x4 dK[2][2];
-      // the next chunk's A into the other buffer (its last reader, the previous chunk's GEMM,
-      // is behind this chunk's barriers); it lands while this chunk's GEMM runs
-      if (t + (int)gridDim.x < nchunks) copy_a(t + gridDim.x, sm + (par ? G::kdA : G::kKl));
-      lcol_gemm_for<MB, 0>(wave, Lc, dAl, lane, dK[0], dK[1]);
-      // K_ZX of the wave's rows (f32 MFMA, zs rows fed in pi order: reg r <-> row g + 4r, the
-      // f64 C layout of dK), Q = dK o K
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int rt = h == 0 ? pA : pB;
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          const float* za = zs + (16 * rt + pi16(c)) * DS + g;
-          const float* xb = xs + (16 * ct + c) * DS + g;
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int k = 0; k < DQ / 4; ++k) acc = mfma32(za[4 * k], xb[4 * k], acc);
-          const int col = 16 * ct + c;
-          const float xnc = xn[col];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int p = 16 * rt + g + 4 * r;
-            float dist = zn[p] + xnc - 2.f * acc[r];
-            dist = dist < 0.f ? 0.f : dist;
-            const float kv = (p < M && col < nvalid) ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * dist) : 0.f;
-            Qt[h][ct][r] = (h == 1 && !two) ? 0.f : (float)dK[h][ct][r] * kv;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !two) break;
-      const int rt = h == 0 ? pA : pB;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = row16_sum_f(Qt[h][0][r] + Qt[h][1][r]);
-        if (c == 0) lds_acc(qrow + 16 * rt + g + 4 * r, v);
-      }
-    }
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      float v = 0.f;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) v += (Qt[h][ct][0] + Qt[h][ct][1]) + (Qt[h][ct][2] + Qt[h][ct][3]);
-      sumQ += v;
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (g == 0) red[wave * LTW + 16 * ct + c] = v;
-    }
-    {
-      f32x4 xz[2][NDT];
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) xz[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !two) break;
-        const int rt = h == 0 ? pA : pB;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) {
-            const float zb = zs[(16 * rt + g + 4 * r) * DS + 16 * dt + c];
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) xz[ct][dt] = mfma32(Qt[h][ct][r], zb, xz[ct][dt]);
-          }
-      }
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            xzl[(wave * LTW + 16 * ct + 4 * g + r) * DQ + 16 * dt + c] = xz[ct][dt][r];
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !two) break;
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = Qt[h][ct][r];
-        adj_lds_order();
-        float aq[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) aq[s] = scr[((c & 3) * 16 + 4 * s + g) * 5 + (c >> 2)];
-        adj_lds_order();
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-            qx[h][dt] = mfma32(aq[s], xs[(16 * ct + 4 * s + g) * DS + 16 * dt + c], qx[h][dt]);
-      }
-    }
-    lds_barrier();
-    for (int e = tid; e < LTW * DQ; e += NT) {
-      const int col = e / DQ;
-      float v = 0.f, r = 0.f;
-#pragma unroll
-      for (int q = 0; q < NWV; ++q) {
-        v += xzl[(q * LTW + col) * DQ + dd];
-        r += red[q * LTW + col];
-      }
-      const float xv = xs[col * DS + dd];
-      if (col < nvalid && dd < D) {
-        dX[(col0 + col) * D + dd] = (v - xv * r) * il_dd + gmc[col] * w_dd;
-        rx2 = __builtin_fmaf(r * xv, xv, rx2);
-        gxa = __builtin_fmaf(gmc[col], xv, gxa);
-      }
-    }
-  }
-  lds_barrier();
-  // partial fields: QX (M x D) | q (M) | dvm (M) | dsm (M) | rx2 (D) | sumQ | sumgv | gx (D) | sumgm
-  const int P = M * D + 3 * M + 2 * D + 3;
-  float* po = wspart + (size_t)blockIdx.x * P;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (h == 1 && !two) break;
-    const int rt = h == 0 ? pA : pB;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int p = 16 * rt + 4 * g + r, d = 16 * dt + c;
-        if (p < M && d < D) po[p * D + d] = qx[h][dt][r];
-      }
-  }
-  for (int m = tid; m < M; m += NT) {
-    po[M * D + m] = vsm[G::kQ + m];
-    po[M * D + M + m] = vsm[oRows + m];
-    po[M * D + 2 * M + m] = vsm[oRows + G::MP + m];
-  }
-  lds_barrier();   // the rows are read out before misc overwrites them
-  float* misc = vsm + G::kMisc;
-  misc[tid] = rx2;
-  misc[NT + tid] = gxa;
-  sumQ = wave_sum(sumQ);
-  if (lane == 0) misc[2 * NT + wave] = sumQ;
-  lds_barrier();
-  for (int d = tid; d < D; d += NT) {
-    float v = 0.f, u = 0.f;
-    for (int q = d; q < NT; q += DQ) { v += misc[q]; u += misc[NT + q]; }
-    po[M * D + 3 * M + d] = v;
-    po[M * D + 3 * M + D + 2 + d] = u;
-  }
-  if (tid == 0) {
-    float v = 0.f;
-    for (int q = 0; q < NWV; ++q) v += misc[2 * NT + q];
-    po[M * D + 3 * M + D] = v;
-  }
-  if (wave == 0) {
-    const float u = wave_sum(sumgm), v = wave_sum(sumgv);   // accumulated on lanes 0..LTW-1
-    if (lane == 0) {
-      po[M * D + 3 * M + 2 * D + 2] = u;
-      po[M * D + 3 * M + D + 1] = v;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // dL^{-1} of the saved-state adjoint (M > 64), from the forward's A instead of a dA / K_ZX
 // workspace: with dA = gmean m + 2 gvar (s^2 - 1) A,
 //   dL^{-1} = sum_i dA_i K_i^T = m u^T + 2 diag(s^2 - 1) G',   u = sum_i gmean_i K_i,
@@ -2242,30 +1905,25 @@ gpk_var_kgram_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
 }
 
 // ---------------------------------------------------------------------------
-// Saved-state adjoint for M > 64 in ONE pass over the training forward's A (round 6; replaces
-// gpk_var_adjs_l_kernel + gpk_var_kgram_l_kernel, which read A, X and recomputed K_ZX twice):
-// the adjs flow with
-//  * dK = L^{-T} dA on f32 MFMA from an fp32 copy of the wave's L^{-1} column blocks (half the
-//    registers of the fp64 blocks, twice the MFMA rate; the reference's dK is fp64: the
-//    measured gradient error vs the fp64 oracle stays ~1e-6);
-//  * dL^{-1} = sum_i dA_i K_i^T accumulated in the same pass. Wave w owns the dL^{-1} tile
-//    COLUMNS pA = w and pB = MB-1-w -- exactly the K_ZX row blocks it computes -- so K never
-//    leaves its registers: one per-wave transpose (the Q transpose's scratch) puts the chunk's
-//    points on the MFMA k index, and the dA operand of each tile row P is gathered from the
-//    chunk's LDS block (8 scalar reads per row block, shared by both columns). The MB + 1 tiles
-//    of the two columns are f32 accumulators (products exact, fp32 sums like kgram's G').
-// Partials per workgroup: the adjs fields | the dL^{-1} lower tiles (acc layout) -> one
-// gpk_var_red_kernel launch -> gpk_var_fin_kernel copies the totals (VarGdlArgs::MB < 0).
-// Every f32 MFMA output here is in the f32 C layout (lane (g, c) reg r <-> row 4 g + r,
-// column c), so K_ZX is built with the z rows in natural order (no pi16).
+// Adjoint for M > 64 from the training forward's saved state (gpk_variational_train_f32):
+// ONE kernel in the adjk layout (wave w holds the L^{-1} COLUMN blocks of block rows
+// pA = w, pB = MB-1-w). Per chunk: A (fp32, LSaved layout) straight into the LDS dA tiles by
+// LDS-DMA (double-buffered), the clamp mask onto gvar; each wave turns ITS rows of A into
+// dA = gmean m + 2 gvar (s^2 - 1) A in place (with the dvmean / dvstd row sums); then
+// dK = L^{-T} dA on f32 MFMA from an fp32 copy of the wave's L^{-1} column blocks (round 6; the
+// reference's dK is fp64: 68 instead of 136 VGPRs and twice the MFMA rate, 0.229 -> 0.180 ms at
+// N = 192; the gradients stay within ~1e-6 of the fp64 oracle), K_ZX of the
+// wave's rows recomputed (f32 MFMA, natural row order: every f32 MFMA output here is in the f32
+// C layout, lane (g, c) reg r <-> row 4 g + r), Q = dK o K and the Q^T zs / QX contractions, dX
+// per point and the fixed-order partials. dL^{-1} comes from gpk_var_kgram_l_kernel (G' = A
+// diag(gvar) K_ZX^T from the same saved A, below). (Accumulating dL^{-1} = sum dA K^T in this
+// pass as well -- the wave's tile columns are its K rows -- needs 68 more VGPRs than the 256 of
+// two waves per SIMD: 98 VGPRs of spills, L^{-1} reloaded from scratch inside the GEMM, measured
+// 0.232 ms; not kept.)
 // ---------------------------------------------------------------------------
-template <int MB, int DQ>
-struct LAdjG {
-  static constexpr int NTILE = MB * (MB + 1) / 2;
-  static constexpr int PG = NTILE * 256;                // dL^{-1} lower tiles per partial row
-};
-
-// dK of the wave with pA = RA from fp32 column-block registers (lcol_gemm on f32 MFMA).
+// dK of the wave with pA = RA from its fp32 column-block registers: slots 0..NA-1 are blocks
+// (rt = RA + s, RA), the rest (rt = RB + s - NA, RB); B operands dA[rt] from LDS (the next slot's
+// read while this slot's 8 MFMAs run).
 template <int MB, int RA>
 GPK_DEVICE void lcol_gemm32(const float (&Lc)[MB + 1][4], const float* dAl, int lane,
                             f32x4 (&dKa)[2], f32x4 (&dKb)[2]) {
@@ -2315,82 +1973,20 @@ GPK_DEVICE void lcol_gemm32_for(int wave, const float (&Lc)[MB + 1][4], const fl
   }
 }
 
-// dL^{-1} tiles of columns RA, RB += sum over the chunk's points of dA[P rows] K[col rows]^T.
-// kt[h][ct][s] (lane (g, c)) = K[16 P_h + c][16 ct + 4 s + g]; the dA operand of row block P is
-// dA[16 P + c][16 ct + 4 s + g], gathered from the LSaved tile layout (element u of lane
-// (c', g') of tile (P, ct) <-> row 16 P + g' + 4u, point 16 ct + c'). Slots: column RA rows
-// P = RA..MB-1 -> 0..MB-1-RA, column RB rows P = RB..MB-1 -> MB-RA.. (MB + 1 in all).
-template <int MB, int RA>
-GPK_DEVICE void gdl_accum(f32x4 (&gacc)[MB + 1], const float (&kt)[2][2][4], const float* dAl, int c, int g) {
-  constexpr int RB = MB - 1 - RA;
-  constexpr int PLO = RA < RB ? RA : RB;
-#pragma unroll
-  for (int P = PLO; P < MB; ++P) {
-    float aop[2][4];
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-        aop[ct][s4] = dAl[((P * 2 + ct) * 64 + 16 * (c & 3) + 4 * s4 + g) * 4 + (c >> 2)];
-    if (P >= RA) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) gacc[P - RA] = mfma32(aop[ct][s4], kt[0][ct][s4], gacc[P - RA]);
-    }
-    if (RB != RA && P >= RB) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-          gacc[MB - RA + P - RB] = mfma32(aop[ct][s4], kt[1][ct][s4], gacc[MB - RA + P - RB]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-template <int MB, int RA>
-GPK_DEVICE void gdl_accum_for(int wave, f32x4 (&gacc)[MB + 1], const float (&kt)[2][2][4], const float* dAl,
-                              int c, int g) {
-  if constexpr (RA < (MB + 1) / 2) {
-    if (wave == RA) gdl_accum<MB, RA>(gacc, kt, dAl, c, g);
-    else gdl_accum_for<MB, RA + 1>(wave, gacc, kt, dAl, c, g);
-  }
-}
-// the partial row: dL^{-1} tile (I, J) at (I (I + 1) / 2 + J) * 256 + lane * 4 + r (acc layout)
-template <int MB, int RA>
-GPK_DEVICE void gdl_store(const f32x4 (&gacc)[MB + 1], float* po, int lane) {
-  constexpr int RB = MB - 1 - RA;
-#pragma unroll
-  for (int s = 0; s <= MB; ++s) {
-    const bool isA = s < MB - RA;
-    if (!isA && RB == RA) break;
-    const int I = isA ? RA + s : RB + (s - (MB - RA)), J = isA ? RA : RB;
-    *(f32x4*)(po + (I * (I + 1) / 2 + J) * 256 + lane * 4) = gacc[s];
-  }
-}
-template <int MB, int RA>
-GPK_DEVICE void gdl_store_for(int wave, const f32x4 (&gacc)[MB + 1], float* po, int lane) {
-  if constexpr (RA < (MB + 1) / 2) {
-    if (wave == RA) gdl_store<MB, RA>(gacc, po, lane);
-    else gdl_store_for<MB, RA + 1>(wave, gacc, po, lane);
-  }
-}
-
 template <int MB, int DQ>
 __global__ void __launch_bounds__(64 * ((MB + 1) / 2), 2)
-gpk_var_adjg_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
+gpk_var_adjs_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
                       const double* __restrict__ Linv, const float* __restrict__ vmean,
                       const float* __restrict__ vstd, const float* __restrict__ hyp,
                       const float* __restrict__ gmean, const float* __restrict__ gvar,
                       const float* __restrict__ saved, int N, int M, int D, int nchunks,
-                      float* __restrict__ wspart, float* __restrict__ gpart, float* __restrict__ dX,
-                      float* __restrict__ cm_out) {
+                      float* __restrict__ wspart, float* __restrict__ dX, float* __restrict__ cm_out) {
   using G = LAdjGeo<MB, DQ>;
   using SV = LSaved<MB>;
   constexpr int NWV = G::NWV, NT = G::NT, DS = G::DS, NPASS = G::NPASS, DV = G::DV, NDT = G::NDT;
   constexpr int NU = SV::tiles / 4;                 // f32x4 units of A per chunk
   static_assert(NU % NT == 0, "A block: whole passes");
-  static_assert(MB % 2 == 0, "two distinct column blocks per wave");
+  static_assert(MB % 2 == 0, "two distinct column blocks per wave");   // (MB in {6, 8, 12, 16})
   extern __shared__ __attribute__((aligned(16))) float vsm[];
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4, sub = tid & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2456,9 +2052,6 @@ gpk_var_adjg_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) qx[h][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 gacc[MB + 1];
-#pragma unroll
-  for (int s = 0; s <= MB; ++s) gacc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
   int par = 0;
 
   for (int t = blockIdx.x; t < nchunks; t += gridDim.x, par ^= 1) {
@@ -2535,14 +2128,12 @@ gpk_var_adjg_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       }
     }
     lds_barrier();
-    // ---- dK = L^{-T} dA (f32 MFMA) on the wave's block rows; K_ZX of those rows; Q = dK o K;
-    // then the chunk's dL^{-1} contribution of the wave's tile columns from K and the LDS dA
+    // ---- dK = L^{-T} dA (f32 MFMA) on the wave's block rows; K_ZX of those rows; Q = dK o K
     f32x4 Qt[2][2];
     {
       f32x4 dK[2][2];
       if (t + (int)gridDim.x < nchunks) copy_a(t + gridDim.x, sm + (par ? G::kdA : G::kKl));
       lcol_gemm32_for<MB, 0>(wave, Lc, dAl, lane, dK[0], dK[1]);
-      float kt[2][2][4];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int rt = h == 0 ? pA : pB;
@@ -2564,16 +2155,8 @@ gpk_var_adjg_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
             kv[r] = (p < M && col < nvalid) ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * dist) : 0.f;
             Qt[h][ct][r] = dK[h][ct][r] * kv[r];
           }
-          // K^T for the dL^{-1} MFMAs: lane (g, c) <- K[16 rt + c][16 ct + 4 s + g]
-#pragma unroll
-          for (int r = 0; r < 4; ++r) scr[lane * 5 + r] = kv[r];
-          adj_lds_order();
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) kt[h][ct][s4] = scr[(16 * (c >> 2) + 4 * s4 + g) * 5 + (c & 3)];
-          adj_lds_order();
         }
       }
-      gdl_accum_for<MB, 0>(wave, gacc, kt, dAl, c, g);
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -2670,7 +2253,6 @@ gpk_var_adjg_l_kernel(const float* __restrict__ X, const float* __restrict__ Z,
         if (p < M && d < D) po[p * D + d] = qx[h][dt][r];
       }
   }
-  gdl_store_for<MB, 0>(wave, gacc, gpart + (size_t)blockIdx.x * LAdjG<MB, DQ>::PG, lane);
   for (int m = tid; m < M; m += NT) {
     po[M * D + m] = vsm[G::kQ + m];
     po[M * D + M + m] = vsm[oRows + m];
@@ -2713,13 +2295,9 @@ GPK_DEVICE void var_gdl_elem(long long e, const double* __restrict__ gtot, const
   if (q <= p) {
     const int ti = p >> 4, tj = q >> 4, ra = p & 15, cb = q & 15;
     const double gp = gtot[(ti * (ti + 1) / 2 + tj) * 256 + ((ra >> 2) * 16 + cb) * 4 + (ra & 3)];
-    if (MB < 0) {
-      v = gp;   // gpk_var_adjg_l_kernel: the totals ARE dL^{-1} = sum dA K^T
-    } else {
-      const double u = gtot[(size_t)(MB * (MB + 1) / 2) * 256 + q];
-      const double sd = (double)vstd[p];
-      v = (double)vmean[p] * u + 2.0 * (sd * sd - 1.0) * gp;
-    }
+    const double u = gtot[(size_t)(MB * (MB + 1) / 2) * 256 + q];
+    const double sd = (double)vstd[p];
+    v = (double)vmean[p] * u + 2.0 * (sd * sd - 1.0) * gp;
   }
   dLinv[e] = v;
 }
@@ -3315,6 +2893,9 @@ extern "C" int gpk_dev_adjr_stamps(unsigned* host, int n) {
 #ifndef GPK_ADJR_SKIP
 #define GPK_ADJR_SKIP 0   // timing-only ablations (wrong results): 1 G, 2 dK, 4 Q^T zs, 8 QX, 16 dX, 64 A
 #endif
+#ifndef GPK_ADJR_DK32
+#define GPK_ADJR_DK32 1   // dK = L^{-T} dA on f32 MFMA (0: fp64, the round-5 form)
+#endif
 template <int DQ, int NW, bool FG>
 __global__ void __launch_bounds__(64 * NW, 8 / NW)
 gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
@@ -3493,22 +3074,42 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
       }
     }
     GPK_ADJR_ST(4)
-    // dK = L^{-T} dA (fp64; L^{-T} upper: kb >= rt), then Q = dK o K_ZX (in K's registers)
+    // dK = L^{-T} dA (L^{-T} upper: kb >= rt), then Q = dK o K_ZX (in K's registers). Round 6:
+    // on f32 MFMA (GPK_ADJR_DK32; the reference's dK is fp64, the gradients stay ~1e-6 from the
+    // fp64 oracle) with the L^{-1} columns fed in pi order, so the f32 C layout of the result
+    // (row 4 g + r) holds dK row g + 4 r -- K's layout -- in register r.
 #pragma unroll
     for (int rt = 0; rt < 4 && !(GPK_ADJR_SKIP & 2); ++rt) {
-      f64x4 acc[2] = {f64x4{0.0, 0.0, 0.0, 0.0}, f64x4{0.0, 0.0, 0.0, 0.0}};
+      if constexpr (GPK_ADJR_DK32) {
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        const int cp = pi16(c);
 #pragma unroll
-      for (int kb = rt; kb < 4; ++kb)
+        for (int kb = rt; kb < 4; ++kb)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const double la = li[(16 * kb + g + 4 * u) * RLS + 16 * rt + c];
+          for (int u = 0; u < 4; ++u) {
+            const float la = (float)li[(16 * kb + g + 4 * u) * RLS + 16 * rt + cp];
 #pragma unroll
-          for (int q = 0; q < 2; ++q) acc[q] = mfma64(la, (double)dA[kb][q][u], acc[q]);
-        }
+            for (int q = 0; q < 2; ++q) acc[q] = mfma32(la, dA[kb][q][u], acc[q]);
+          }
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) K[rt][q][r] = (float)acc[q][r] * K[rt][q][r];
+          for (int r = 0; r < 4; ++r) K[rt][q][r] = acc[q][r] * K[rt][q][r];
+      } else {
+        f64x4 acc[2] = {f64x4{0.0, 0.0, 0.0, 0.0}, f64x4{0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+        for (int kb = rt; kb < 4; ++kb)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const double la = li[(16 * kb + g + 4 * u) * RLS + 16 * rt + c];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) acc[q] = mfma64(la, (double)dA[kb][q][u], acc[q]);
+          }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) K[rt][q][r] = (float)acc[q][r] * K[rt][q][r];
+      }
     }
     GPK_ADJR_ST(5)
     // r_i = sum_p Q_pi (every lane c of a column), q_p row partials, sum Q
@@ -4322,33 +3923,9 @@ AdjSavedPlan adj_saved_plan(int B, int N, int M, int D) {
   return p;
 }
 
-#ifndef GPK_VAR_ADJG
-#define GPK_VAR_ADJG 1   // 1: one-pass saved-state adjoint (gpk_var_adjg_l_kernel); 0: adjs + kgram (round 5)
-#endif
 template <int MB, int DQ>
 int launch_var_adj_saved(const GpkVarAdjArgs& a, hipStream_t stream) {
-  if constexpr (var_saved_fits<MB, DQ>() && GPK_VAR_ADJG) {
-    using LA = LAdjGeo<MB, DQ>;
-    const AdjSavedPlan p = adj_saved_plan<MB, DQ>(a.B, a.N, a.M, a.D);
-    constexpr int PG = LAdjG<MB, DQ>::PG;
-    char* ws = (char*)a.ws;
-    float* gpart = (float*)(ws + p.off_gpart);     // (sized for kgram's PG >= this PG)
-    float* wspart = (float*)(ws + p.off_part);
-    double* tot = (double*)(ws + p.off_tot);
-    double* gtot = (double*)(ws + p.off_gtot);
-    set_lds_once<gpk_var_adjg_l_kernel<MB, DQ>>();
-    hipLaunchKernelGGL((gpk_var_adjg_l_kernel<MB, DQ>), dim3(p.nwg), dim3(LA::NT), (size_t)LA::k_total * sizeof(float),
-                       stream, a.X, a.Z, a.Linv, a.vmean, a.vstd, a.hyp, a.gmean, a.gvar, a.saved, a.N, a.M,
-                       a.D, p.nchunks, wspart, gpart, a.dX, (float*)(ws + p.off_cm));
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.P + 31) / 32 + (PG + 31) / 32), dim3(256), 0, stream,
-                       wspart, p.nwg, p.P, tot, nullptr, 0, 0, 0, nullptr, gpart, PG, gtot);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    const VarGdlArgs gd{gtot, a.Linv, a.vmean, a.vstd, a.dLinv, -MB};
-    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream,
-                          (const float*)(ws + p.off_cm), &gd);
-  } else if constexpr (var_saved_fits<MB, DQ>()) {
+  if constexpr (var_saved_fits<MB, DQ>()) {
     using LA = LAdjGeo<MB, DQ>;
     using LG = LGramGeo<MB, DQ>;
     const AdjSavedPlan p = adj_saved_plan<MB, DQ>(a.B, a.N, a.M, a.D);

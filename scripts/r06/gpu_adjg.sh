@@ -13,3 +13,7 @@ for rep in 1 2 3; do for n in 192 96; do for nl in base=$BASE new=$NEW; do
   o=$(GPK_LIB=$R/$lib timeout -k 10 120 python scripts/r06/time_var_saved.py 256 $n 256 32 2>/dev/null | tail -n 1) || { echo FAIL $name; exit 3; }
   echo "$rep $name N=$n $o" | tee -a $O/ab.txt
 done; done; done
+# the product exact kernel after the round-6 diagonal-wave change
+timeout -k 10 300 python -u -m pytest tests/test_exact_gpu.py tests/test_golden_gpu.py tests/test_posterior_gpu.py tests/test_exact_grad_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_exact.log 2>&1; rc=$?
+tail -n 2 $O/pytest_exact.log
+exit $rc
