@@ -5,8 +5,9 @@ synthetic exact-GP windows, N=256, D=32 -- per step the fused kernel builds the 
 runs the jittered Cholesky, the forward solve and the MLL for every window and writes L
 (B,N,N) and the MLL. Weak scaling (default): every rank owns B=512 windows. Strong
 scaling (--strong): B=512 windows in total, sharded with shard_range. The K timed steps
-are bracketed by one pair of HIP events on the launch stream (roofline.kernel_ms = their
-elapsed time / K, which agrees with the rocprofv3 kernel average). The per-step MLL
+(one eager launch each; --graph: one HIP-graph replay of the K launches) are bracketed by
+one pair of HIP events on the launch stream (roofline.kernel_ms = their elapsed time / K,
+which agrees with the rocprofv3 kernel average plus the inter-kernel gap). The per-step MLL
 partial sums stay on the device and are SUM-all-reduced across ranks once (RCCL over
 xGMI) at the end of the timed region (distributed.ObjectiveAccumulator), so no
 collective sits on a step's critical path.
@@ -128,7 +129,7 @@ def time_graph(fn, n, warm=3):
     untimed (the first replay of a fresh graph exec uploads it), then one timed replay
     between HIP events, / n. No host work sits between the launches, so this is what the
     kernels take back to back -- the way a captured training step (graphs.GraphedStep) runs
-    them. Side legs only; the headline loop is eager."""
+    them. (The headline loop captures its K launches the same way, in main.)"""
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -409,6 +410,9 @@ def main():
                     help="skip the measurement-only variant builds (e.g. under rocprofv3)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend (nccl = RCCL; gloo only for the one-GPU world-2 test)")
+    ap.add_argument("--graph", action="store_true",
+                    help="time one HIP-graph replay of the K launches instead of K eager launches "
+                         "(measured slower on MI355X: 72.5 vs 60.9 us per launch, DESIGN.md §6)")
     ap.add_argument("--share-device", action="store_true",
                     help="every rank uses cuda:0 (tests/test_world2_gpu.py: two ranks on one GPU)")
     args = ap.parse_args()
@@ -454,18 +458,40 @@ def main():
     torch.cuda.synchronize()
     ops.check_cholesky_info(out.info, 1e-6, inputs=(X,))   # one sync, outside the timed region
 
-    # the timed region: K eager launches bracketed by ONE pair of HIP events on the launch
-    # stream; roofline.kernel_ms = their elapsed time / K (an event pair around every
-    # launch adds 4-12 us of event overhead per 70 us kernel, and the same to the timed loop)
+    # the timed region: the K steps (one exact-kernel launch each, each writing its own
+    # accumulator row) bracketed by ONE pair of HIP events on the launch stream;
+    # roofline.kernel_ms = their elapsed time / K (an event pair around every launch adds 4-12 us
+    # of event overhead per 70 us kernel, and the same to the timed loop). --graph: the K
+    # launches are captured into ONE HIP graph outside the timed region (one untimed replay
+    # uploads it) and the timed region replays it; measured SLOWER than the eager loop on
+    # MI355X (72.5 vs 60.9 us per launch): the replay's per-node overhead exceeds the host
+    # launch work, which the eager loop hides behind 60 us kernels.
     acc = ObjectiveAccumulator(args.steps, dev, width=B)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    graph = None
+    if args.graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step(warm.rows[0])
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(args.steps):
+                step(acc.slot())
+        graph.replay()          # upload (the same values the timed replay writes)
+        torch.cuda.synchronize()
     if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(args.steps):
-        step(acc.slot())
+    if graph is not None:
+        graph.replay()
+    else:
+        for _ in range(args.steps):
+            step(acc.slot())
     ev1.record()
     totals, work = acc.reduce()
     torch.cuda.synchronize()
@@ -484,6 +510,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = (float(v) for v in t.tolist())
     mean_mll = float(totals[-1].item()) / B_total
+    eager_kern_ms = None
+    if graph is not None:   # the eager loop beside the graph replay (same launches)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            step(warm.rows[0])
+        e1.record()
+        torch.cuda.synchronize()
+        eager_kern_ms = e0.elapsed_time(e1) / args.steps
 
     # BASELINE configs[1] (B=128, N=128, D=32): a side leg, same kernel, its own roofline
     cfg2 = None
@@ -512,7 +548,7 @@ def main():
             Ls_ = torch.empty(Bs, N, N, device=dev)
             f = lambda: ops.exact_mll(Xs_, ys_, None, None, None, None, hyper=hyper, L_out=Ls_)  # noqa: E731
             gG, eG, _ = time_side(f, 20)
-            msG = eG   # eager, like the headline loop it is compared with
+            msG = gG if (gG is not None and graph is not None) else eG   # as the headline loop is timed
             strong_share[f"G{G}"] = {"windows_per_rank": Bs, "kernel_ms": msG, "graph_ms": gG,
                                      "implied_speedup": kern_ms / msG if B == 512 else None}
 
@@ -569,6 +605,9 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": load_traffic(f"exact_B{B}_N{N}_D{D}"),
                          "kernel": "gpk_exact_kernel", "kernel_ms": kern_ms,
+                         "timed_loop": "one HIP-graph replay of the K launches" if graph is not None
+                                       else "K eager launches",
+                         "eager_kernel_ms": eager_kern_ms,
                          "bytes_per_window": bpw, "fp32_flops_per_window": fpw,
                          "fp32_frac": fpw * B / (kern_ms * 1e-3) / FP32_PEAK},
             "mean_mll": mean_mll,
