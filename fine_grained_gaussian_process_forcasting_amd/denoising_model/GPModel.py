@@ -27,7 +27,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..errors import GPInputWarning
-from ..gp import ConstantMean, MultivariateNormal, RBFKernel, ScaleKernel
+from ..gp import ConstantMean, MultivariateNormal, RBFKernel, ScaleKernel, psd_safe_cholesky
 
 
 def _as_batch(x: torch.Tensor) -> torch.Tensor:
@@ -131,9 +131,7 @@ class ExactGPModel(nn.Module):
     def _posterior(self, x):
         params = [p for p in self.parameters()] + [x, self.train_inputs[0], self.train_targets]
         if torch.is_grad_enabled() and any(t.requires_grad for t in params):
-            raise NotImplementedError(
-                "gradients through the exact-GP posterior are not provided; evaluate predictions "
-                "under torch.no_grad() (as GPyTorch's prediction examples do)")
+            return self._posterior_autograd(x)
         Xb, L, z, hyper = self._train_factor()
         xs = _as_batch(x).float()
         if xs.shape[0] != Xb.shape[0]:
@@ -142,6 +140,48 @@ class ExactGPModel(nn.Module):
         mean, var = torch.ops.gpk.exact_posterior(Xb, L, z, hyper, xs.contiguous())
         if x.dim() == 3 or Xb.shape[0] > 1:
             shape = mean.shape                    # (B, Ns): one posterior per training window
+        else:
+            shape = x.shape[:-1] if x.dim() > 1 else x.shape
+        return MultivariateNormal(mean.reshape(shape), var.reshape(shape))
+
+    def _posterior_autograd(self, x):
+        """The eval posterior WITH gradients (GPyTorch allows them; upstream
+        exact_prediction_strategies.py): the same quantities as gpk_exact_posterior_f32,
+        restated in differentiable torch ops on the caller's device -- K_hat = s2 RBF(X, X) +
+        noise I, L = psd_safe_cholesky(K_hat) (the fp32 jitter ladder), K* = s2 RBF(X, x) over the
+        joint inputs in upstream ``_sq_dist``'s centred GEMM form, V = L^{-1} K*,
+        z = L^{-1} (y - c), mean = c + V^T z, var = s2 - colsum(V o V). Taken only when a
+        gradient will flow (a parameter, the inputs or the training data require grad): the
+        prediction cache is not used, as GPyTorch does not cache through autograd either.
+        Off the hot path: no HIP kernel serves this."""
+        train_x, train_y = self.train_inputs[0], self.train_targets
+        if not (x.is_cuda and train_x.is_cuda):
+            raise ValueError("ExactGPModel runs on the GPU: move the model and inputs to a cuda device")
+        Xb = _as_batch(train_x)
+        yb = train_y.reshape(Xb.shape[0], Xb.shape[1])
+        xs = _as_batch(x)
+        if xs.shape[0] != Xb.shape[0]:
+            xs = xs.expand(Xb.shape[0], *xs.shape[1:])
+        kern = self.covar_module
+        ls = kern.base_kernel.lengthscale.reshape(-1)
+        s2 = kern.outputscale.reshape(())
+        c = self.mean_module.constant.reshape(())
+        noise = self.likelihood.noise.reshape(())
+        n = Xb.shape[-2]
+        full = torch.cat([Xb, xs], -2) / ls
+        a = full - full.mean(-2, keepdim=True)
+        nrm = a.pow(2).sum(-1, keepdim=True)
+        d = (nrm + nrm.transpose(-1, -2) - 2.0 * a @ a.transpose(-1, -2)).clamp_min(0.0)
+        K = s2 * torch.exp(-0.5 * d)
+        eye = torch.eye(n, dtype=K.dtype, device=K.device)
+        Kxx = K[..., :n, :n] * (1.0 - eye) + s2 * eye        # exact diagonal, as _sq_dist zeroes it
+        L = psd_safe_cholesky(Kxx + noise * eye)
+        V = torch.linalg.solve_triangular(L, K[..., :n, n:], upper=False)
+        zz = torch.linalg.solve_triangular(L, (yb - c).unsqueeze(-1), upper=False)
+        mean = c + (V * zz).sum(-2)
+        var = s2 - (V * V).sum(-2)
+        if x.dim() == 3 or Xb.shape[0] > 1:
+            shape = mean.shape
         else:
             shape = x.shape[:-1] if x.dim() > 1 else x.shape
         return MultivariateNormal(mean.reshape(shape), var.reshape(shape))

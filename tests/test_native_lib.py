@@ -171,7 +171,7 @@ def test_posterior_entry_validation_without_device():
 
 def test_exact_model_input_shapes_and_eval_guard():
     """ExactGPModel accepts (N,), (N, D) and (B, N, D) inputs (GPyTorch's shapes); the
-    eval-mode posterior refuses to build an autograd graph it cannot differentiate."""
+    eval-mode posterior (with or without gradients) refuses CPU tensors: no CPU path."""
     from fine_grained_gaussian_process_forcasting_amd.denoising_model.GPModel import ExactGPModel, _as_batch
     from fine_grained_gaussian_process_forcasting_amd.gp import GaussianLikelihood
     assert _as_batch(torch.zeros(7)).shape == (1, 7, 1)
@@ -183,5 +183,5 @@ def test_exact_model_input_shapes_and_eval_guard():
     prior = m(torch.zeros(7, 3))
     assert prior.mean.shape == (7,) and prior._exact[0].shape == (1, 7, 3)
     m.eval()
-    with pytest.raises(NotImplementedError, match="no_grad"):
+    with pytest.raises(ValueError, match="GPU"):
         m(torch.ones(5, 3))
