@@ -520,6 +520,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         eager_kern_ms = e0.elapsed_time(e1) / args.steps
+    else:                   # the timed loop itself was the eager one
+        eager_kern_ms = kern_ms
 
     # BASELINE configs[1] (B=128, N=128, D=32): a side leg, same kernel, its own roofline
     cfg2 = None

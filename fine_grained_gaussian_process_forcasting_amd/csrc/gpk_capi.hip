@@ -21,7 +21,7 @@ const char* gpk_strerror(int code) {
   return hipGetErrorString((hipError_t)code);
 }
 
-int gpk_exact_max_n(void) { return 256; }
+int gpk_exact_max_n(void) { return kGpkExactMaxN; }
 
 int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp, int n_lengthscale,
                       int B, int N, int D, double jitter, int max_tries, float* L, float* z,
@@ -38,13 +38,17 @@ int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp, int n_le
   if (mll == nullptr) return -12;
   if (info == nullptr) return -13;
   if (N > gpk_exact_max_n()) return -6;
+  if (N > kGpkExactRegMaxN && L == nullptr) return -10;   // the blocked path factors in L
+  if (N > kGpkExactRegMaxN && D > 64) return -7;
   if (B == 0) return 0;
   GpkExactArgs a{X, y, hyp, n_lengthscale, B, N, D, jitter, max_tries, L, z, mll, info};
+  if (N > kGpkExactRegMaxN) return gpk_launch_exact_large(a, (hipStream_t)stream);
   return gpk_launch_exact(a, (hipStream_t)stream);
 }
 
 size_t gpk_exact_grad_workspace_bytes(int B, int N) {
   if (B < 0 || N < 1 || N > gpk_exact_max_n()) return 0;
+  if (N > kGpkExactRegMaxN) return gpk_exact_large_grad_ws_floats(B, N) * sizeof(float);
   return gpk_exact_grad_ws_floats(B, N) * sizeof(float);
 }
 
@@ -60,10 +64,11 @@ int gpk_exact_mll_grad_f32(const float* X, const float* L, const float* z, const
   if (N < 1 || N > gpk_exact_max_n()) return -7;
   if (D < 1 || D > 64) return -8;
   if (gout == nullptr) return -9;
-  if (workspace == nullptr && B > 0 && gpk_exact_grad_ws_floats(B, N) > 0) return -10;
+  if (workspace == nullptr && B > 0 && gpk_exact_grad_workspace_bytes(B, N) > 0) return -10;
   if (dhyp == nullptr) return -13;
   if (B == 0) return 0;
   GpkExactGradArgs a{X, L, z, hyp, n_lengthscale, B, N, D, gout, (float*)workspace, dX, dy, dhyp};
+  if (N > kGpkExactRegMaxN) return gpk_launch_exact_large_grad(a, (hipStream_t)stream);
   return gpk_launch_exact_grad(a, (hipStream_t)stream);
 }
 
@@ -84,6 +89,7 @@ int gpk_exact_posterior_f32(const float* X, const float* L, const float* z, cons
   if (var == nullptr) return -12;
   if (B == 0 || Ns == 0) return 0;
   GpkPostArgs a{X, L, z, hyp, n_lengthscale, Xs, B, N, Ns, D, mean, var};
+  if (N > kGpkExactRegMaxN) return gpk_launch_exact_large_posterior(a, (hipStream_t)stream);
   return gpk_launch_exact_posterior(a, (hipStream_t)stream);
 }
 

@@ -120,4 +120,12 @@ struct GpkPostArgs {
 };
 
 size_t gpk_post_lds_bytes(int N, int D);
+
+// 256 < N <= 800 (gpk_exact_large.hip): blocked kernels with the window's matrix in HBM.
+constexpr int kGpkExactRegMaxN = 256;     // largest N of the register / LDS-resident kernels
+constexpr int kGpkExactMaxN = 800;        // GPyTorch settings.max_cholesky_size
+size_t gpk_exact_large_grad_ws_floats(int B, int N);
+int gpk_launch_exact_large(const GpkExactArgs& a, hipStream_t stream);
+int gpk_launch_exact_large_grad(const GpkExactGradArgs& a, hipStream_t stream);
+int gpk_launch_exact_large_posterior(const GpkPostArgs& a, hipStream_t stream);
 int gpk_launch_exact_posterior(const GpkPostArgs& a, hipStream_t stream);

@@ -51,6 +51,9 @@ class ExactMLLOut:
     info: torch.Tensor           # (B,) int32 (0 / -t / k, see include/gpk.h)
 
 
+EXACT_REG_MAX_N = 256   # largest N of the register / LDS-resident exact kernels (gpk_internal.h)
+
+
 def exact_mll(X: torch.Tensor, y: torch.Tensor, lengthscale, outputscale, mean_constant, noise,
               jitter: float = 1e-6, max_tries: int = 3, want_L: bool = True,
               want_z: bool = False, hyper: Optional[torch.Tensor] = None,
@@ -87,14 +90,17 @@ def exact_mll(X: torch.Tensor, y: torch.Tensor, lengthscale, outputscale, mean_c
     if L_out is not None and (L_out.shape != (B, N, N) or L_out.dtype != torch.float32
                               or not L_out.is_contiguous() or L_out.device != dev):
         raise ValueError("L_out must be a contiguous (B, N, N) float32 tensor on X's device")
-    L = (L_out if L_out is not None else torch.empty(B, N, N, device=dev, dtype=torch.float32)) if want_L else None
+    # Above EXACT_REG_MAX_N the blocked kernels (gpk_exact_large.hip) factor in place in L, so
+    # it is allocated even when the caller does not keep it.
+    need_L = want_L or N > EXACT_REG_MAX_N
+    L = (L_out if L_out is not None else torch.empty(B, N, N, device=dev, dtype=torch.float32)) if need_L else None
     z = torch.empty(B, N, device=dev, dtype=torch.float32) if want_z else None
     rc = _native.lib().gpk_exact_mll_f32(
         X.data_ptr(), y.data_ptr(), hyper.data_ptr(), n_ls, B, N, D, float(jitter), int(max_tries),
         L.data_ptr() if L is not None else None, z.data_ptr() if z is not None else None,
         mll.data_ptr(), info.data_ptr(), _stream_ptr(dev))
     _native.check(rc, "gpk_exact_mll_f32")
-    return ExactMLLOut(mll, L, z, info)
+    return ExactMLLOut(mll, L if want_L else None, z, info)
 
 
 @dataclass

@@ -26,7 +26,10 @@ int gpk_version(void);
 /* Human-readable text for a return code of any gpk_* function. */
 const char* gpk_strerror(int code);
 
-/* Largest N gpk_exact_mll_f32 accepts (padded to 16, register-resident). */
+/* Largest N the exact entry points accept: 800, GPyTorch's settings.max_cholesky_size (the
+ * exact MLL leaves Cholesky for CG / Lanczos above it). N <= 256 runs the fused register /
+ * LDS-resident kernels; 256 < N <= 800 the blocked kernels of gpk_exact_large.hip, which
+ * factor in place in L (so L is required there) and need D <= 64. */
 int gpk_exact_max_n(void);
 
 /*
@@ -48,7 +51,8 @@ int gpk_exact_max_n(void);
  *        (constrained values: softplus already applied by the caller)
  * n_lengthscale : 1 (GPModel.py:8) or D (ARD)
  * jitter, max_tries : ladder (GPyTorch defaults 1e-6 and 3 for fp32)
- * L    : (B, N, N) float out, lower factor with zeroed upper triangle; may be NULL
+ * L    : (B, N, N) float out, lower factor with zeroed upper triangle; may be NULL for
+ *        N <= 256 (required above: the blocked path's working storage, -10 if NULL)
  * z    : (B, N) float out; may be NULL
  * mll  : (B,) float out
  * info : (B,) int out: 0 = factored without jitter; -t = factored after t
@@ -75,7 +79,8 @@ int gpk_exact_mll_f32(const float* X, const float* y, const float* hyp,
  *
  * L : (B, N, N) float, z : (B, N) float (gpk_exact_mll_f32 outputs)   gout : (B,) float
  * workspace : gpk_exact_grad_workspace_bytes(B, N) bytes of device memory (the lower block
- *             tiles of K_hat^{-1} per window, ~145 KB at N = 256, plus small vectors)
+ *             tiles of K_hat^{-1} per window, ~145 KB at N = 256, plus small vectors; for
+ *             N > 256, L^{-1} and K_hat^{-1} as Np x Np each, Np = N rounded up to 32)
  * dX : (B, N, D) float out or NULL (D <= 64)   dy : (B, N) float out or NULL
  * dhyp : (B, 3 + n_lengthscale) float out (per window; the caller sums over b)
  */
@@ -97,7 +102,7 @@ int gpk_exact_mll_grad_f32(const float* X, const float* L, const float* z, const
  * exact_prediction_strategies.py exact_predictive_mean / exact_predictive_covar (diag).
  *
  * X : (B, N, D) float training inputs   L : (B, N, N) float   z : (B, N) float
- * hyp : as gpk_exact_mll_f32   Xs : (B, Ns, D) float test inputs (D <= 64, N <= 256)
+ * hyp : as gpk_exact_mll_f32   Xs : (B, Ns, D) float test inputs (D <= 64, N <= 800)
  * mean, var : (B, Ns) float out
  */
 int gpk_exact_posterior_f32(const float* X, const float* L, const float* z, const float* hyp,

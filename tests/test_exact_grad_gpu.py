@@ -108,7 +108,7 @@ def test_exact_grad_native_kernel_loaded(cuda_device):
     from fine_grained_gaussian_process_forcasting_amd import _native
     lib = _native.lib()
     assert lib.gpk_exact_grad_workspace_bytes(2, 256) == 2 * 36224 * 4
-    assert lib.gpk_exact_grad_workspace_bytes(1, 300) == 0
+    assert lib.gpk_exact_grad_workspace_bytes(1, 801) == 0
     # a NULL workspace is refused before anything is launched; a real one runs
     import torch
     from fine_grained_gaussian_process_forcasting_amd import ops

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
         assert n in _native.SIGNATURES, f"{n} declared in gpk.h but not bound in _native.py"
     assert lib.gpk_version() >= 100
-    assert lib.gpk_exact_max_n() == 256
+    assert lib.gpk_exact_max_n() == 800   # GPyTorch settings.max_cholesky_size
     assert b"success" == lib.gpk_strerror(0)
 
 
@@ -35,7 +35,10 @@ def test_argument_validation_without_device():
     one = ctypes.c_void_p(16)  # never dereferenced: validation returns first
     assert lib.gpk_exact_mll_f32(None, one, one, 1, 1, 8, 2, 1e-6, 3, None, None, one, one, None) == -1
     assert lib.gpk_exact_mll_f32(one, one, one, 5, 1, 8, 2, 1e-6, 3, None, None, one, one, None) == -4
-    assert lib.gpk_exact_mll_f32(one, one, one, 1, 1, 300, 2, 1e-6, 3, None, None, one, one, None) == -6
+    assert lib.gpk_exact_mll_f32(one, one, one, 1, 1, 801, 2, 1e-6, 3, None, None, one, one, None) == -6
+    # 256 < N <= 800: the blocked kernels factor in place, so L is required; D <= 64
+    assert lib.gpk_exact_mll_f32(one, one, one, 1, 1, 300, 2, 1e-6, 3, None, None, one, one, None) == -10
+    assert lib.gpk_exact_mll_f32(one, one, one, 1, 1, 300, 65, 1e-6, 3, one, None, one, one, None) == -7
     assert lib.gpk_exact_mll_f32(one, one, one, 1, 1, 8, 2, -1.0, 3, None, None, one, one, None) == -8
     assert lib.gpk_exact_mll_f32(one, one, one, 1, 0, 8, 2, 1e-6, 3, None, None, one, one, None) == 0
     assert lib.gpk_kzz_chol_f64(one, one, 300, 4, 1e-4, 1e-8, 3, one, one, one, None) == -3
@@ -98,13 +101,16 @@ def test_grad_entry_validation_without_device():
     one = ctypes.c_void_p(16)  # never dereferenced: validation returns first
     # K^-1 lower tiles (136 x 1 KiB) + alpha, means, partials per window, 64-float aligned
     assert lib.gpk_exact_grad_workspace_bytes(3, 256) == 3 * 36224 * 4
-    assert lib.gpk_exact_grad_workspace_bytes(3, 257) == 0
+    # N > 256: L^-1 and K_hat^-1 (Np x Np each, Np = N rounded up to 32) per window
+    assert lib.gpk_exact_grad_workspace_bytes(3, 257) == 3 * 2 * 288 * 288 * 4
+    assert lib.gpk_exact_grad_workspace_bytes(3, 800) == 3 * 2 * 800 * 800 * 4
+    assert lib.gpk_exact_grad_workspace_bytes(3, 801) == 0
     args = [one, one, one, one, 1, 2, 16, 4, one, one, None, None, one, None]
     bad = list(args); bad[0] = None
     assert lib.gpk_exact_mll_grad_f32(*bad) == -1
     bad = list(args); bad[4] = 3
     assert lib.gpk_exact_mll_grad_f32(*bad) == -5
-    bad = list(args); bad[6] = 300
+    bad = list(args); bad[6] = 801
     assert lib.gpk_exact_mll_grad_f32(*bad) == -7
     bad = list(args); bad[7] = 65
     assert lib.gpk_exact_mll_grad_f32(*bad) == -8
@@ -161,7 +167,7 @@ def test_posterior_entry_validation_without_device():
         assert lib.gpk_exact_posterior_f32(*bad) == code
     bad = list(args); bad[4] = 3
     assert lib.gpk_exact_posterior_f32(*bad) == -5
-    bad = list(args); bad[7] = 257
+    bad = list(args); bad[7] = 801
     assert lib.gpk_exact_posterior_f32(*bad) == -8
     bad = list(args); bad[9] = 65
     assert lib.gpk_exact_posterior_f32(*bad) == -10
