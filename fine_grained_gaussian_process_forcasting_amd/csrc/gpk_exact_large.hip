@@ -35,7 +35,22 @@
 
 namespace {
 
-constexpr int kLgWaves = 16;
+#ifndef GPK_LG_WAVES
+#define GPK_LG_WAVES 16
+#endif
+// Timing-only knockouts of the forward's phases (bit 1 trailing update, 2 panel TRSM, 4 the
+// diagonal block's factor / inverse / z, 8 the K_hat build); failures are ignored. Never set
+// in a product build.
+#ifndef GPK_LG_KO
+#define GPK_LG_KO 0
+#endif
+// Software-pipelined trailing update (the next unit's loads before this unit's MFMAs):
+// measured slower (16 waves: 110 VGPRs of spills, N = 800: 1.755 / 4.435 ms at B = 64 / 512
+// vs 1.673 / 4.209 ms without; 8 waves: 1.783 / 4.144), so off.
+#ifndef GPK_LG_PIPE
+#define GPK_LG_PIPE 0
+#endif
+constexpr int kLgWaves = GPK_LG_WAVES;   // waves per window workgroup (forward, backward)
 constexpr int kLgThreads = 64 * kLgWaves;
 constexpr int kPostThreads = 128;
 constexpr int kPS = 36;          // LDS row stride of a 32-wide panel / block (floats; 16-B rows)
@@ -117,24 +132,36 @@ GPK_DEVICE void lg_load_diag_row(const float* __restrict__ A, int ld, int r0, in
 }
 
 // Centring mean of x / l over the N training rows (GPyTorch _sq_dist: adj = x1.mean(-2)),
-// the lengthscales, and the squared norms of the centred rows: mu[D], ils[D], nrm[Np] in
-// LDS (rows >= N get 0).
+// 1 / l, and the squared norms of the centred rows: mu[D], ils[D], nrm[Np] in LDS (rows >= N
+// get 0). The column sums are split over every thread of the workgroup (row groups of a
+// dimension, 8 loads in flight each), then summed over the groups in a fixed order; `part`
+// is nthreads floats of LDS scratch. Inputs are scaled by 1 / l like the N <= 256 kernels.
 GPK_DEVICE void lg_centre(const float* __restrict__ X, const float* __restrict__ hyp, int n_ls,
-                          int N, int Np, int D, float* mu, float* ls, float* nrm, int tid,
-                          int nthreads) {
-  if (tid < D) {
-    const float l = hyp[3 + (n_ls == 1 ? 0 : tid)];
-    ls[tid] = l;
+                          int N, int Np, int D, float* mu, float* ils, float* nrm, float* part,
+                          int tid, int nthreads) {
+  const int ngrp = nthreads / D;            // D <= 64 <= nthreads
+  if (tid < ngrp * D) {
+    const int d = tid % D, grp = tid / D;
+    const float il = 1.f / hyp[3 + (n_ls == 1 ? 0 : d)];
     float s = 0.f;
-    for (int i = 0; i < N; ++i) s += X[(size_t)i * D + tid] / l;
+#pragma unroll 8
+    for (int i = grp; i < N; i += ngrp) s += X[(size_t)i * D + d] * il;
+    part[tid] = s;
+    if (grp == 0) ils[d] = il;
+  }
+  __syncthreads();
+  if (tid < D) {
+    float s = 0.f;
+    for (int grp = 0; grp < ngrp; ++grp) s += part[grp * D + tid];
     mu[tid] = s / (float)N;
   }
   __syncthreads();
   for (int i = tid; i < Np; i += nthreads) {
     float s = 0.f;
     if (i < N)
+#pragma unroll 8
       for (int d = 0; d < D; ++d) {
-        const float a = X[(size_t)i * D + d] / ls[d] - mu[d];
+        const float a = X[(size_t)i * D + d] * ils[d] - mu[d];
         s = fmaf(a, a, s);
       }
     nrm[i] = s;
@@ -143,9 +170,9 @@ GPK_DEVICE void lg_centre(const float* __restrict__ X, const float* __restrict__
 }
 
 // Centred, scaled input (x / l - mu)[row][d]; 0 outside the matrix.
-GPK_DEVICE float lg_xs(const float* __restrict__ X, const float* mu, const float* ls, int row,
+GPK_DEVICE float lg_xs(const float* __restrict__ X, const float* mu, const float* ils, int row,
                        int d, int N, int D) {
-  return (row < N && d < D) ? X[(size_t)row * D + d] / ls[d] - mu[d] : 0.f;
+  return (row < N && d < D) ? X[(size_t)row * D + d] * ils[d] - mu[d] : 0.f;
 }
 
 // clamp_min(0) of a squared distance, NaN-propagating like torch (fmaxf would drop a NaN).
@@ -155,13 +182,23 @@ GPK_DEVICE float lg_clamp0(float d) { return d < 0.f ? 0.f : d; }
 // layout, on f32 MFMA (k = d = 4t + q).
 GPK_DEVICE f32x4 lg_gram_tile(const float* __restrict__ X1, int N1, int r0,
                               const float* __restrict__ X2, int N2, int c0, const float* mu,
-                              const float* ls, int D, int lane) {
+                              const float* ils, int D, int lane) {
   const int i = lane & 15, q = lane >> 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int t = 0; 4 * t < D; ++t) {
     const int d = 4 * t + q;
-    acc = mfma4(lg_xs(X1, mu, ls, r0 + i, d, N1, D), lg_xs(X2, mu, ls, c0 + i, d, N2, D), acc);
+    acc = mfma4(lg_xs(X1, mu, ils, r0 + i, d, N1, D), lg_xs(X2, mu, ils, c0 + i, d, N2, D), acc);
   }
+  return acc;
+}
+
+// The same tile from centred inputs staged in LDS (row stride 33 floats, D <= 32).
+GPK_DEVICE f32x4 lg_gram_tile_lds(const float* xsl, int r0, int c0, int D, int lane) {
+  const int i = lane & 15, q = lane >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (4 * t < D) acc = mfma4(xsl[(r0 + i) * 33 + 4 * t + q], xsl[(c0 + i) * 33 + 4 * t + q], acc);
   return acc;
 }
 
@@ -169,7 +206,7 @@ GPK_DEVICE f32x4 lg_gram_tile(const float* __restrict__ X1, int N1, int r0,
 // Forward: K_hat -> L (in the caller's buffer), z, mll, info.
 // =========================================================================================
 struct LgFwdLds {
-  int panel, linv, lkk, rv, zb, nrm, mu, ls, misc, total;
+  int panel, linv, lkk, rv, zb, nrm, mu, ils, misc, total;
 };
 __host__ __device__ inline LgFwdLds lg_fwd_layout(int Np) {
   LgFwdLds o{};
@@ -180,8 +217,8 @@ __host__ __device__ inline LgFwdLds lg_fwd_layout(int Np) {
   o.zb = o.rv + Np;                 // Np: z = L^-1 (y - c)
   o.nrm = o.zb + Np;                // Np: squared norms of the centred rows
   o.mu = o.nrm + Np;                // 64
-  o.ls = o.mu + 64;                 // 64
-  o.misc = o.ls + 64;               // 8 ints: [0] failing column (1-based) of this attempt
+  o.ils = o.mu + 64;                 // 64
+  o.misc = o.ils + 64;               // 8 ints: [0] failing column (1-based) of this attempt
   o.total = o.misc + 8;
   return o;
 }
@@ -199,7 +236,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
   float* zb = smem + lay.zb;
   float* nrm = smem + lay.nrm;
   float* mu = smem + lay.mu;
-  float* ls = smem + lay.ls;
+  float* ils = smem + lay.ils;   // 1 / lengthscale
   volatile int* misc = (volatile int*)(smem + lay.misc);
   const float* X = a.X + (size_t)b * N * D;
   const float* y = a.y + (size_t)b * N;
@@ -207,7 +244,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
   const float s2 = a.hyp[0], noise = a.hyp[1], cmean = a.hyp[2];
   const int g = lane >> 4, c = lane & 15, q = lane >> 4, il = lane & 15;
 
-  lg_centre(X, a.hyp, a.n_ls, N, Np, D, mu, ls, nrm, tid, kLgThreads);
+  lg_centre(X, a.hyp, a.n_ls, N, Np, D, mu, ils, nrm, panel, tid, kLgThreads);
   // the strict upper triangle of L is zero and never touched again
   for (int i = wave; i < N; i += kLgWaves)
     for (int j = i + 1 + lane; j < N; j += 64) Lg[(size_t)i * N + j] = 0.f;
@@ -226,13 +263,24 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
     }
     __syncthreads();   // every wave has read the previous attempt's verdict
     if (tid == 0) misc[0] = 0;
-    // ---- K_hat (lower 16x16 tiles, diagonal tiles whole) into L
+    // ---- K_hat (lower 16x16 tiles, diagonal tiles whole) into L. For D <= 32 the centred
+    //      inputs are staged in the panel's LDS (free until the first panel): the Gram's
+    //      strided global loads were the build's whole cost.
+    const bool xs_lds = D <= 32;
+    if (xs_lds) {
+      for (int e = tid; e < Np * 32; e += kLgThreads) {
+        const int i = e >> 5, d = e & 31;
+        panel[i * 33 + d] = lg_xs(X, mu, ils, i, d, N, D);
+      }
+      __syncthreads();
+    }
     const int npair = nsub * (nsub + 1) / 2;
-    for (int p = wave; p < npair; p += kLgWaves) {
+    for (int p = wave; p < npair && !(GPK_LG_KO & 8); p += kLgWaves) {
       int I, J;
       tri_decode(p, I, J);
       if (16 * I >= N) continue;
-      const f32x4 dot = lg_gram_tile(X, N, 16 * I, X, N, 16 * J, mu, ls, D, lane);
+      const f32x4 dot = xs_lds ? lg_gram_tile_lds(panel, 16 * I, 16 * J, D, lane)
+                               : lg_gram_tile(X, N, 16 * I, X, N, 16 * J, mu, ils, D, lane);
       const int col = 16 * J + c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -255,8 +303,8 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
         const int cr = lane & 31;
         float v[32];
         lg_load_diag_row(Lg, N, r0, cr, N, v);
-        const int f = lg_chol32(v, cr, ld);
-        if (f >= 0) {
+        const int f = (GPK_LG_KO & 4) ? -1 : lg_chol32(v, cr, ld);
+        if (f >= 0 && !GPK_LG_KO) {
           if (lane == 0) misc[0] = r0 + f + 1;
         } else {
           const int row = r0 + cr;
@@ -267,7 +315,12 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
           }
           lg_rows_to_lds(v, cr, lane, lkk);
           float x[32];
-          lg_inv32(lkk, cr, x);
+          if (GPK_LG_KO & 4) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) x[i] = v[i];
+          } else {
+            lg_inv32(lkk, cr, x);
+          }
           if (lane < 32) {
 #pragma unroll
             for (int i = 0; i < 32; ++i) linv[i * kPS + cr] = x[i];
@@ -289,7 +342,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
       //      16-column halves: A_Ik is read in place and overwritten by L_Ik, so one wave
       //      must own the whole 32-wide row segment)
       const int s0 = 2 * (k + 1);
-      for (int I = s0 + wave; I < nsub; I += kLgWaves) {
+      for (int I = s0 + wave; I < nsub && !(GPK_LG_KO & 2); I += kLgWaves) {
         if (16 * I >= N) break;
         const int row = 16 * I + il;
         const float* arow = Lg + (size_t)row * N + r0 + 8 * q;
@@ -318,31 +371,87 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
         for (int m = 0; m < 32; ++m) s = fmaf(panel[i * kPS + m], zb[r0 + m], s);
         rv[i] -= s;
       }
-      const int mt = nsub - s0, npr = mt * (mt + 1) / 2;
-      for (int p = wave; p < npr; p += kLgWaves) {
-        int ii, jj;
-        tri_decode(p, ii, jj);
-        const int I = s0 + ii, J = s0 + jj;
-        if (16 * I >= N) continue;
-        const int col = 16 * J + c;
-        f32x4 acc;
+      // 32x32 units (four 16x16 tiles: 16 loads in flight per lane, the panel operands read
+      // once per unit; a diagonal unit skips its upper tile), software-pipelined: the next
+      // unit's loads are issued before this unit's MFMAs. Units never overlap, and every
+      // unit's first row block is real (32 (nb - 1) < N).
+      const int mb = nb - (k + 1), nbp = mb * (mb + 1) / 2;
+      auto unit_of = [&](int p, int& I0, int& J0, bool& dg) {
+        int bi, bj;
+        tri_decode(p, bi, bj);
+        I0 = s0 + 2 * bi;
+        J0 = s0 + 2 * bj;
+        dg = bi == bj;
+      };
+      auto load_unit = [&](int I0, int J0, f32x4 (&acc)[2][2]) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * I + 4 * g + r;
-          acc[r] = (row < N && col < N) ? Lg[(size_t)row * N + col] : 0.f;
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < 2; ++tj) {
+            const int col = 16 * (J0 + tj) + c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * (I0 + ti) + 4 * g + r;
+              acc[ti][tj][r] = (row < N && col < N) ? Lg[(size_t)row * N + col] : 0.f;
+            }
+          }
+      };
+      int p = wave, I0 = 0, J0 = 0;
+      bool dg = false;
+      f32x4 cur[2][2];
+      if (p < nbp && !(GPK_LG_KO & 1)) {
+        unit_of(p, I0, J0, dg);
+        load_unit(I0, J0, cur);
+      }
+      for (; p < nbp && !(GPK_LG_KO & 1); p += kLgWaves) {
+        const int pn = p + kLgWaves;
+        int nI0 = 0, nJ0 = 0;
+        bool ndg = false;
+        f32x4 nxt[2][2];
+        if (GPK_LG_PIPE && pn < nbp) {
+          unit_of(pn, nI0, nJ0, ndg);
+          load_unit(nI0, nJ0, nxt);
         }
-        const f32x4 a0 = *(const f32x4*)&panel[(16 * I + il) * kPS + 8 * q];
-        const f32x4 a1 = *(const f32x4*)&panel[(16 * I + il) * kPS + 8 * q + 4];
-        const f32x4 b0 = *(const f32x4*)&panel[(16 * J + il) * kPS + 8 * q];
-        const f32x4 b1 = *(const f32x4*)&panel[(16 * J + il) * kPS + 8 * q + 4];
+        f32x4 ao[2][2], bo[2][2];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma4(-a0[s], b0[s], acc);
+        for (int t = 0; t < 2; ++t) {
+          ao[t][0] = *(const f32x4*)&panel[(16 * (I0 + t) + il) * kPS + 8 * q];
+          ao[t][1] = *(const f32x4*)&panel[(16 * (I0 + t) + il) * kPS + 8 * q + 4];
+          bo[t][0] = *(const f32x4*)&panel[(16 * (J0 + t) + il) * kPS + 8 * q];
+          bo[t][1] = *(const f32x4*)&panel[(16 * (J0 + t) + il) * kPS + 8 * q + 4];
+        }
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma4(-a1[s], b1[s], acc);
+        for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * I + 4 * g + r;
-          if (row < N && col < N) Lg[(size_t)row * N + col] = acc[r];
+          for (int tj = 0; tj < 2; ++tj) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) cur[ti][tj] = mfma4(-ao[ti][0][s], bo[tj][0][s], cur[ti][tj]);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) cur[ti][tj] = mfma4(-ao[ti][1][s], bo[tj][1][s], cur[ti][tj]);
+          }
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < 2; ++tj) {
+            if (dg && ti == 0 && tj == 1) continue;   // above the diagonal
+            const int col = 16 * (J0 + tj) + c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * (I0 + ti) + 4 * g + r;
+              if (row < N && col < N) Lg[(size_t)row * N + col] = cur[ti][tj][r];
+            }
+          }
+        if (GPK_LG_PIPE) {
+#pragma unroll
+          for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) cur[ti][tj] = nxt[ti][tj];
+          I0 = nI0;
+          J0 = nJ0;
+          dg = ndg;
+        } else if (pn < nbp) {
+          unit_of(pn, I0, J0, dg);
+          load_unit(I0, J0, cur);
         }
       }
       __syncthreads();
@@ -369,7 +478,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
 // Backward: X = L^-1, K_hat^-1 = X^T X (workspace), then the gram contractions.
 // =========================================================================================
 struct LgGradLds {
-  int alpha, zb, nrm, mu, ls, scr, red, total;
+  int alpha, zb, nrm, mu, ils, scr, red, total;
 };
 constexpr int kRedStride = 2 + 64;
 __host__ __device__ inline LgGradLds lg_grad_layout(int Np) {
@@ -378,8 +487,8 @@ __host__ __device__ inline LgGradLds lg_grad_layout(int Np) {
   o.zb = o.alpha + Np;                  // Np
   o.nrm = o.zb + Np;                    // Np
   o.mu = o.nrm + Np;                    // 64
-  o.ls = o.mu + 64;                     // 64
-  o.scr = o.ls + 64;                    // 16 waves x 32 x kPS: L_kk / the T block of a row step
+  o.ils = o.mu + 64;                     // 64
+  o.scr = o.ils + 64;                    // 16 waves x 32 x kPS: L_kk / the T block of a row step
   o.red = o.scr + kLgWaves * 32 * kPS;  // 16 waves x kRedStride fp64 partial sums (2 floats each)
   o.total = o.red + 2 * kLgWaves * kRedStride;
   return o;
@@ -395,7 +504,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
   float* zb = smem + lay.zb;
   float* nrm = smem + lay.nrm;
   float* mu = smem + lay.mu;
-  float* ls = smem + lay.ls;
+  float* ils = smem + lay.ils;   // 1 / lengthscale
   float* scr = smem + lay.scr + wave * (32 * kPS);
   double* red = (double*)(smem + lay.red);
   const float* X = a.X + (size_t)b * N * D;
@@ -404,7 +513,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
   float* Kw = Xw + (size_t)Np * Np;             // K_hat^-1 (lower 16x16 tiles)
   const int g = lane >> 4, c = lane & 15, q = lane >> 4, il = lane & 15;
 
-  lg_centre(X, a.hyp, a.n_ls, N, Np, D, mu, ls, nrm, tid, kLgThreads);
+  lg_centre(X, a.hyp, a.n_ls, N, Np, D, mu, ils, nrm, smem + lay.scr, tid, kLgThreads);
   for (int i = tid; i < Np; i += kLgThreads) zb[i] = i < N ? a.z[(size_t)b * N + i] : 0.f;
   // ---- 1. diagonal-block inverses X_kk = L_kk^-1
   for (int k = wave; k < nb; k += kLgWaves) {
@@ -455,25 +564,43 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
     }
     __syncthreads();
   }
-  // ---- 3. K_hat^-1 = X^T X (lower tiles) and alpha = X^T z
-  const int npair = nsub * (nsub + 1) / 2;
-  for (int p = wave; p < npair; p += kLgWaves) {
-    int I, J;
-    tri_decode(p, I, J);
-    if (16 * I >= N) continue;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int pp = I; pp < nsub && 16 * pp < N; ++pp) {
-      f32x4 qv, pv;
+  // ---- 3. K_hat^-1 = X^T X (lower tiles, in 32x32 units: the four tiles share each 16-row
+  //      step's X loads) and alpha = X^T z
+  const int nbp = nb * (nb + 1) / 2;
+  for (int p = wave; p < nbp; p += kLgWaves) {
+    int bi, bj;
+    tri_decode(p, bi, bj);
+    const int I0 = 2 * bi, J0 = 2 * bj;
+    if (16 * I0 >= N) continue;
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int pp = I0; pp < nsub && 16 * pp < N; ++pp) {
+      f32x4 qv[2], pv[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const size_t row = (size_t)(16 * pp + 4 * g + r) * Np;
-        qv[r] = Xw[row + 16 * I + c];
-        pv[r] = Xw[row + 16 * J + c];
+        qv[0][r] = Xw[row + 16 * I0 + c];
+        qv[1][r] = Xw[row + 16 * I0 + 16 + c];
+        pv[0][r] = Xw[row + 16 * J0 + c];
+        pv[1][r] = Xw[row + 16 * J0 + 16 + c];
       }
-      acc = mma_tn(qv, pv, acc);
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = mma_tn(qv[ti], pv[tj], acc[ti][tj]);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Kw[(size_t)(16 * I + 4 * g + r) * Np + 16 * J + c] = acc[r];
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj) {
+        if (bi == bj && ti == 0 && tj == 1) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Kw[(size_t)(16 * (I0 + ti) + 4 * g + r) * Np + 16 * (J0 + tj) + c] = acc[ti][tj][r];
+      }
   }
   for (int j = tid; j < Np; j += kLgThreads) {
     float s = 0.f;
@@ -493,7 +620,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
   for (int I = wave; I < nsub && 16 * I < N; I += kLgWaves) {
     float bI[16];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) bI[t] = 4 * t < D ? lg_xs(X, mu, ls, 16 * I + il, 4 * t + q, N, D) : 0.f;
+    for (int t = 0; t < 16; ++t) bI[t] = 4 * t < D ? lg_xs(X, mu, ils, 16 * I + il, 4 * t + q, N, D) : 0.f;
     f32x4 wx[4];
 #pragma unroll
     for (int dc = 0; dc < 4; ++dc) wx[dc] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -503,7 +630,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
       f32x4 dot = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < 16; ++t)
-        if (4 * t < D) dot = mfma4(lg_xs(X, mu, ls, 16 * J + il, 4 * t + q, N, D), bI[t], dot);
+        if (4 * t < D) dot = mfma4(lg_xs(X, mu, ils, 16 * J + il, 4 * t + q, N, D), bI[t], dot);
       f32x4 wt;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -527,7 +654,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
         if (dc < nDQ) {
           f32x4 xj;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) xj[r] = lg_xs(X, mu, ls, 16 * J + 4 * g + r, 16 * dc + c, N, D);
+          for (int r = 0; r < 4; ++r) xj[r] = lg_xs(X, mu, ils, 16 * J + 4 * g + r, 16 * dc + c, N, D);
           wx[dc] = mma_tn(wt, xj, wx[dc]);   // Wx[16I + 4g + r][16dc + c] += sum_j W_ij xs_j
         }
     }
@@ -542,9 +669,9 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
           const float w1r = __shfl(w1c, 4 * g + r, 64);
           const int pt = 16 * I + 4 * g + r, d = 16 * dc + c;
           if (pt < N && d < D) {
-            const float xs = lg_xs(X, mu, ls, pt, d, N, D);
+            const float xs = lg_xs(X, mu, ils, pt, d, N, D);
             const float t = fmaf(xs, w1r, -wx[dc][r]);   // xs w1 - Wx
-            if (a.dX != nullptr) a.dX[((size_t)b * N + pt) * D + d] = -2.f * t / ls[d];
+            if (a.dX != nullptr) a.dX[((size_t)b * N + pt) * D + d] = -2.f * t * ils[d];
             p_dl[dc] += (double)(xs * t);
           }
         }
@@ -579,11 +706,11 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
     } else if (a.n_ls == 1) {
       for (int d = 0; d < D; ++d)
         for (int w = 0; w < kLgWaves; ++w) v += red[w * kRedStride + 2 + d];
-      v = 2.0 * v / (double)ls[0];
+      v = 2.0 * v * (double)ils[0];
     } else {
       const int d = tid - 3;
       for (int w = 0; w < kLgWaves; ++w) v += red[w * kRedStride + 2 + d];
-      v = 2.0 * v / (double)ls[d];
+      v = 2.0 * v * (double)ils[d];
     }
     a.dhyp[(size_t)b * nh + tid] = (float)v;
   }
@@ -593,7 +720,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
 // Posterior: V = L^-1 K* (16 test points per workgroup), mean and latent variance.
 // =========================================================================================
 struct LgPostLds {
-  int V, lkk, zb, nrm, mu, ls, tn, total;
+  int V, lkk, zb, nrm, mu, ils, tn, total;
 };
 __host__ __device__ inline LgPostLds lg_post_layout(int Np) {
   LgPostLds o{};
@@ -602,8 +729,8 @@ __host__ __device__ inline LgPostLds lg_post_layout(int Np) {
   o.zb = o.lkk + 32 * kPS;    // Np
   o.nrm = o.zb + Np;          // Np
   o.mu = o.nrm + Np;          // 64
-  o.ls = o.mu + 64;           // 64
-  o.tn = o.ls + 64;           // 16: test-point norms
+  o.ils = o.mu + 64;           // 64
+  o.tn = o.ils + 64;           // 16: test-point norms
   o.total = o.tn + 16;
   return o;
 }
@@ -619,7 +746,7 @@ __global__ void __launch_bounds__(kPostThreads) gpk_lg_post_kernel(GpkPostArgs a
   float* zb = smem + lay.zb;
   float* nrm = smem + lay.nrm;
   float* mu = smem + lay.mu;
-  float* ls = smem + lay.ls;
+  float* ils = smem + lay.ils;   // 1 / lengthscale
   float* tn = smem + lay.tn;
   const float* X = a.X + (size_t)b * N * D;
   const float* Xs = a.Xs + (size_t)b * Ns * D;
@@ -627,11 +754,11 @@ __global__ void __launch_bounds__(kPostThreads) gpk_lg_post_kernel(GpkPostArgs a
   const float s2 = a.hyp[0], cmean = a.hyp[2];
   const int g = lane >> 4, c = lane & 15, q = lane >> 4, il = lane & 15;
 
-  lg_centre(X, a.hyp, a.n_ls, N, Np, D, mu, ls, nrm, tid, kPostThreads);
+  lg_centre(X, a.hyp, a.n_ls, N, Np, D, mu, ils, nrm, V, tid, kPostThreads);
   if (tid < 16) {
     float s = 0.f;
     for (int d = 0; d < D; ++d) {
-      const float v = lg_xs(Xs, mu, ls, t0 + tid, d, Ns, D);
+      const float v = lg_xs(Xs, mu, ils, t0 + tid, d, Ns, D);
       s = fmaf(v, v, s);
     }
     tn[tid] = s;
@@ -650,7 +777,7 @@ __global__ void __launch_bounds__(kPostThreads) gpk_lg_post_kernel(GpkPostArgs a
     // R = K*[rows r0 + 16 wave, cols t0..] - L[rows, :r0] V[:r0, :]
     {
       const int rows = r0 + 16 * wave;
-      const f32x4 dot = lg_gram_tile(X, N, rows, Xs, Ns, t0, mu, ls, D, lane);
+      const f32x4 dot = lg_gram_tile(X, N, rows, Xs, Ns, t0, mu, ils, D, lane);
       f32x4 acc;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
