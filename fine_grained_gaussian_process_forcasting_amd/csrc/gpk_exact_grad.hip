@@ -14,7 +14,8 @@
 // linear_operator inv_quad_logdet + psd_safe_cholesky backward) when train.py:166
 // calls loss.backward(); oracle: oracle/gp_oracle.py::exact_mll_grads.
 //
-// Two launches (three in the fp32 form), inputs are the forward's L and z (nothing is refactored):
+// Two phases (three launches in the fp32 form; ONE launch, gpk_grad_fused_kernel,
+// for NB = 16), inputs are the forward's L and z (nothing is refactored):
 //   gpk_grad_solve_kernel  one workgroup (16 waves) per window: alpha = L^-T z, dy, and the
 //       lower block tiles of K^-1: wave J solves block column J with its tiles in registers
 //         forward   V_I = -Linv_II sum_{K=J}^{I-1} L_IK V_K       (I > J, V_J = Linv_JJ)
@@ -59,6 +60,11 @@
 #endif
 #ifndef GPK_GRAD_STAMPS
 #define GPK_GRAD_STAMPS 0
+#endif
+// 1: NB = 16 windows (N in 241..256) run the solve and the gram as one launch
+// (gpk_grad_fused_kernel); 0: two launches.
+#ifndef GPK_GRAD_FUSED
+#define GPK_GRAD_FUSED 1
 #endif
 
 namespace {
@@ -176,9 +182,8 @@ __host__ __device__ inline SolveLds solve_lds(int NB) {
 }
 
 template <int NB, bool FULL>
-__global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs a) {
+GPK_DEVICE void grad_solve_body(const GpkExactGradArgs& a, float* smem) {
   constexpr bool SPLIT = GPK_GRAD_SPLIT && NB > 0;   // (dependent: the other branch is discarded)
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NP = 16 * NB;
   constexpr int TS = (NB > 1 ? NB - 1 : 1) * 256;
   const SolveLds lay = solve_lds(NB);
@@ -496,6 +501,12 @@ __global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs
   }
 }
 
+template <int NB, bool FULL>
+__global__ void __launch_bounds__(kST, 1) gpk_grad_solve_kernel(GpkExactGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  grad_solve_body<NB, FULL>(a, smem);
+}
+
 // ======================================================================================
 // 2. contractions per (window, block row I): W, w1, Wx, dX and the partials.
 //    One workgroup (16 waves) per window: xs = x / l - mean, ||xs||^2 and alpha are
@@ -669,8 +680,7 @@ __host__ __device__ inline GramLds gram_lds(int NP, int DQ) {
 }
 
 template <int DQ, bool FULL>
-__global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : GPK_GRAM_WPE) gpk_grad_gram_split_kernel(GpkExactGradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+GPK_DEVICE void grad_gram_split_body(const GpkExactGradArgs& a, float* smem) {
   constexpr int DP = 16 * DQ, DW = DP < 32 ? 32 : DP, KC = DW / 32;
   const int N = a.N, D = a.D;
   const GradWs ws = grad_ws(N);
@@ -893,6 +903,24 @@ __global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : GPK_GRAM_WPE) gpk_grad
   }
 }
 
+template <int DQ, bool FULL>
+__global__ void __launch_bounds__(64 * kGW, DQ == 4 ? 4 : GPK_GRAM_WPE) gpk_grad_gram_split_kernel(GpkExactGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  grad_gram_split_body<DQ, FULL>(a, smem);
+}
+
+// The solve and the gram in ONE launch (NB = 16, split form): the same 16-wave workgroup runs
+// the gram after the solve, so the K^-1 tiles the solve's waves store are read back by the
+// other waves of the same workgroup (L2-resident) instead of by a second launch from HBM; the
+// gram re-stages its LDS from offset 0 once the solve is done with it.
+template <int DQ, bool FULL>
+__global__ void __launch_bounds__(kST, 1) gpk_grad_fused_kernel(GpkExactGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  grad_solve_body<16, FULL>(a, smem);
+  __syncthreads();   // every wave's workspace stores visible (workgroup scope); LDS reusable
+  grad_gram_split_body<DQ, FULL>(a, smem);
+}
+
 // ======================================================================================
 // 3. fixed-order sums of the block-row partials -> dhyp
 // ======================================================================================
@@ -984,7 +1012,30 @@ size_t gpk_exact_grad_ws_floats(int B, int N) {
   return (size_t)B * grad_ws(N).per;
 }
 
+template <int DQ>
+int launch_fused(const GpkExactGradArgs& a, hipStream_t stream) {
+  const size_t l1 = (size_t)solve_lds(16).total * sizeof(float);
+  const size_t l2 = (size_t)gram_lds(256, DQ).total_bytes;
+  const size_t lds = l1 > l2 ? l1 : l2;
+  if (lds > 160 * 1024) return -7;
+  static std::once_flag once;
+  std::call_once(once, [&] {
+    (void)hipFuncSetAttribute((const void*)gpk_grad_fused_kernel<DQ, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)gpk_grad_fused_kernel<DQ, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();
+  });
+  if (a.N == 256)
+    hipLaunchKernelGGL((gpk_grad_fused_kernel<DQ, true>), dim3(a.B), dim3(kST), lds, stream, a);
+  else
+    hipLaunchKernelGGL((gpk_grad_fused_kernel<DQ, false>), dim3(a.B), dim3(kST), lds, stream, a);
+  return (int)hipGetLastError();
+}
+
 int gpk_launch_exact_grad(const GpkExactGradArgs& a, hipStream_t stream) {
+  if (GPK_GRAD_FUSED && GPK_GRAD_SPLIT && !GPK_GRAD_STAMPS && (a.N + 15) / 16 == 16)
+    return a.D <= 16 ? launch_fused<1>(a, stream) : (a.D <= 32 ? launch_fused<2>(a, stream) : launch_fused<4>(a, stream));
   int rc;
   switch ((a.N + 15) / 16) {
 #define GPK_CASE(nb) case nb: rc = launch_solve<nb>(a, stream); break;

@@ -789,14 +789,29 @@ __global__ void __launch_bounds__(kPostThreads) gpk_lg_post_kernel(GpkPostArgs a
         }
         acc[r] = v;
       }
+      // k order kk = 16p + 4q + t: a lane's four A values are consecutive floats of its L
+      // row (one 16-byte load when the rows are 16-byte aligned), two chunks in flight
       const int ra = rows + il;
       const float* lrow = Lg + (size_t)ra * N;
-      for (int p = 0; p < 2 * k; ++p) {
+      const bool vec = (N & 3) == 0;
+      auto lrow4 = [&](int p) -> f32x4 {
+        const int k0 = 16 * p + 4 * q;
+        if (ra >= N) return f32x4{0.f, 0.f, 0.f, 0.f};
+        if (vec) return *(const f32x4*)&lrow[k0];
+        return f32x4{lrow[k0], lrow[k0 + 1], lrow[k0 + 2], lrow[k0 + 3]};
+      };
+      int p = 0;
+      for (; p + 1 < 2 * k; p += 2) {
+        const f32x4 l0 = lrow4(p), l1 = lrow4(p + 1);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int kk = 16 * p + 4 * t + q;
-          acc = mfma4(ra < N ? -lrow[kk] : 0.f, V[kk * kVS + il], acc);
-        }
+        for (int t = 0; t < 4; ++t) acc = mfma4(-l0[t], V[(16 * p + 4 * q + t) * kVS + il], acc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc = mfma4(-l1[t], V[(16 * p + 16 + 4 * q + t) * kVS + il], acc);
+      }
+      if (p < 2 * k) {
+        const f32x4 l0 = lrow4(p);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc = mfma4(-l0[t], V[(16 * p + 4 * q + t) * kVS + il], acc);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) V[(rows + 4 * g + r) * kVS + c] = acc[r];
