@@ -10,9 +10,10 @@
 //     built straight into L by an f32-MFMA Gram of the centred inputs (GPyTorch _sq_dist
 //     form), then a right-looking blocked Cholesky with 32-wide panels: the diagonal block
 //     factored by one wave with a row per lane (v_readlane broadcasts, no LDS round trips),
-//     its inverse formed the same way, the panel below by TRSM-as-GEMM (A L_kk^-T) into an
-//     LDS-resident panel, the trailing update A_IJ -= L_Ik L_Jk^T on f32 MFMA 16x16 tiles from
-//     that panel; z = L^-1 (y - c) and log|L| ride along per panel. The psd_safe_cholesky
+//     its inverse formed column per lane from an LDS copy, the panel below by TRSM-as-GEMM
+//     (A L_kk^-T, one wave per 16-row tile) into an LDS-resident panel, the trailing update
+//     A_IJ -= L_Ik L_Jk^T on f32 MFMA in 32x32 units from that panel; z = L^-1 (y - c) and
+//     log|L| ride along per panel. The psd_safe_cholesky
 //     ladder (jitter * 10^t, failing windows only, cumulative fp32 diagonal adds) restarts the
 //     window in-kernel: one launch, no host sync.
 //   gpk_lg_grad_kernel   (one workgroup per window) -- X = L^-1 by blocked forward
@@ -488,8 +489,8 @@ __host__ __device__ inline LgGradLds lg_grad_layout(int Np) {
   o.nrm = o.zb + Np;                    // Np
   o.mu = o.nrm + Np;                    // 64
   o.ils = o.mu + 64;                     // 64
-  o.scr = o.ils + 64;                    // 16 waves x 32 x kPS: L_kk / the T block of a row step
-  o.red = o.scr + kLgWaves * 32 * kPS;  // 16 waves x kRedStride fp64 partial sums (2 floats each)
+  o.scr = o.ils + 64;                    // waves x 32 x kPS: L_kk / the T block of a row step
+  o.red = o.scr + kLgWaves * 32 * kPS;  // waves x kRedStride fp64 partial sums (2 floats each)
   o.total = o.red + 2 * kLgWaves * kRedStride;
   return o;
 }
