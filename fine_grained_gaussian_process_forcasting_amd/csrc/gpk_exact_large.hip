@@ -48,6 +48,11 @@ namespace {
 // Software-pipelined trailing update (the next unit's loads before this unit's MFMAs):
 // measured slower (16 waves: 110 VGPRs of spills, N = 800: 1.755 / 4.435 ms at B = 64 / 512
 // vs 1.673 / 4.209 ms without; 8 waves: 1.783 / 4.144), so off.
+// Timing-only knockouts of the backward (bit 1 block-row substitution of L^-1, 2 X^T X,
+// 4 the gram); never set in a product build.
+#ifndef GPK_LG_GKO
+#define GPK_LG_GKO 0
+#endif
 #ifndef GPK_LG_PIPE
 #define GPK_LG_PIPE 0
 #endif
@@ -533,7 +538,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
   }
   __syncthreads();
   // ---- 2. block rows: X_iJ = -X_ii sum_{p = J/2}^{i-1} L_ip X_pJ (16-column tiles J)
-  for (int i = 1; i < nb; ++i) {
+  for (int i = 1; i < nb && !(GPK_LG_GKO & 1); ++i) {
     for (int J = wave; J < 2 * i; J += kLgWaves) {
       const int ra = 32 * i + il, rb = ra + 16;
       f32x4 t0 = {0.f, 0.f, 0.f, 0.f}, t1 = {0.f, 0.f, 0.f, 0.f};
@@ -568,7 +573,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
   // ---- 3. K_hat^-1 = X^T X (lower tiles, in 32x32 units: the four tiles share each 16-row
   //      step's X loads) and alpha = X^T z
   const int nbp = nb * (nb + 1) / 2;
-  for (int p = wave; p < nbp; p += kLgWaves) {
+  for (int p = wave; p < nbp && !(GPK_LG_GKO & 2); p += kLgWaves) {
     int bi, bj;
     tri_decode(p, bi, bj);
     const int I0 = 2 * bi, J0 = 2 * bj;
@@ -618,7 +623,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
   // the hyper-parameter sums cancel heavily (sum G o E of a well-fit model is ~1e-3 of its
   // terms): fp64 accumulators, fixed-order reduction
   double p_s2 = 0.0, p_tr = 0.0, p_dl[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int I = wave; I < nsub && 16 * I < N; I += kLgWaves) {
+  for (int I = wave; I < nsub && 16 * I < N && !(GPK_LG_GKO & 4); I += kLgWaves) {
     float bI[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) bI[t] = 4 * t < D ? lg_xs(X, mu, ils, 16 * I + il, 4 * t + q, N, D) : 0.f;
