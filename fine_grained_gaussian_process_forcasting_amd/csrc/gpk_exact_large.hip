@@ -484,7 +484,7 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_exact_kernel(GpkExactArg
 // Backward: X = L^-1, K_hat^-1 = X^T X (workspace), then the gram contractions.
 // =========================================================================================
 struct LgGradLds {
-  int alpha, zb, nrm, mu, ils, scr, red, total;
+  int alpha, zb, nrm, mu, ils, scr, red, lrow, total;
 };
 constexpr int kRedStride = 2 + 64;
 __host__ __device__ inline LgGradLds lg_grad_layout(int Np) {
@@ -494,9 +494,12 @@ __host__ __device__ inline LgGradLds lg_grad_layout(int Np) {
   o.nrm = o.zb + Np;                    // Np
   o.mu = o.nrm + Np;                    // 64
   o.ils = o.mu + 64;                     // 64
-  o.scr = o.ils + 64;                    // waves x 32 x kPS: L_kk / the T block of a row step
-  o.red = o.scr + kLgWaves * 32 * kPS;  // waves x kRedStride fp64 partial sums (2 floats each)
-  o.total = o.red + 2 * kLgWaves * kRedStride;
+  o.scr = o.ils + 64;                    // waves x 32 x kVS: the T block of a row step
+  o.red = o.scr + kLgWaves * 32 * kVS;  // waves x kRedStride fp64 partial sums (2 floats each)
+  o.lrow = o.red + 2 * kLgWaves * kRedStride;   // 32 x (Np + 4): the row step's block row of L
+                                                // (phase 1: the waves' L_kk, 32 x kPS each)
+  const int lrow_n = 32 * (Np + 4), lkk_n = kLgWaves * 32 * kPS;
+  o.total = o.lrow + (lrow_n > lkk_n ? lrow_n : lkk_n);
   return o;
 }
 
@@ -511,7 +514,9 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
   float* nrm = smem + lay.nrm;
   float* mu = smem + lay.mu;
   float* ils = smem + lay.ils;   // 1 / lengthscale
-  float* scr = smem + lay.scr + wave * (32 * kPS);
+  float* scr = smem + lay.scr + wave * (32 * kVS);
+  float* lrow = smem + lay.lrow;
+  const int LS = Np + 4;
   double* red = (double*)(smem + lay.red);
   const float* X = a.X + (size_t)b * N * D;
   const float* Lg = a.L + (size_t)b * N * N;
@@ -528,28 +533,64 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
     {
       float v[32];
       lg_load_diag_row(Lg, N, 32 * k, cr, N, v);
-      lg_rows_to_lds(v, cr, lane, scr);
+      lg_rows_to_lds(v, cr, lane, lrow + wave * (32 * kPS));
     }
-    lg_inv32(scr, cr, x);
+    lg_inv32(lrow + wave * (32 * kPS), cr, x);
     if (lane < 32) {
 #pragma unroll
       for (int i = 0; i < 32; ++i) Xw[(size_t)(32 * k + i) * Np + 32 * k + cr] = x[i];
     }
   }
   __syncthreads();
-  // ---- 2. block rows: X_iJ = -X_ii sum_{p = J/2}^{i-1} L_ip X_pJ (16-column tiles J)
+  // ---- 2. block rows: X_iJ = -X_ii sum_{p = J/2}^{i-1} L_ip X_pJ (16-column tiles J). The
+  //      step's block row L[32i .. 32i+31][0 .. 32i) is staged in LDS once (coalesced) and read
+  //      as the A operand by every tile J (a lane's 8 values: two 16-byte reads); the X_pJ
+  //      operands come from the workspace, two 32-row chunks in flight.
   for (int i = 1; i < nb && !(GPK_LG_GKO & 1); ++i) {
-    for (int J = wave; J < 2 * i; J += kLgWaves) {
-      const int ra = 32 * i + il, rb = ra + 16;
-      f32x4 t0 = {0.f, 0.f, 0.f, 0.f}, t1 = {0.f, 0.f, 0.f, 0.f};
-      for (int p = J >> 1; p < i; ++p) {
+    for (int e = tid; e < 32 * 8 * i; e += kLgThreads) {   // float4 pieces of the block row
+      const int r = e / (8 * i), c4 = e - r * (8 * i), row = 32 * i + r;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (row < N) {
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const int kk = 32 * p + 8 * q + s;
-          const float bv = Xw[(size_t)kk * Np + 16 * J + il];
-          t0 = mfma4(ra < N ? Lg[(size_t)ra * N + kk] : 0.f, bv, t0);
-          t1 = mfma4(rb < N ? Lg[(size_t)rb * N + kk] : 0.f, bv, t1);
+        for (int t = 0; t < 4; ++t) v[t] = Lg[(size_t)row * N + 4 * c4 + t];
+      }
+      *(f32x4*)&lrow[r * LS + 4 * c4] = v;
+    }
+    __syncthreads();
+    for (int J = wave; J < 2 * i; J += kLgWaves) {
+      f32x4 t0 = {0.f, 0.f, 0.f, 0.f}, t1 = {0.f, 0.f, 0.f, 0.f};
+      auto chunk = [&](int p, const float (&bv)[8]) {
+        const f32x4 a00 = *(const f32x4*)&lrow[il * LS + 32 * p + 8 * q];
+        const f32x4 a01 = *(const f32x4*)&lrow[il * LS + 32 * p + 8 * q + 4];
+        const f32x4 a10 = *(const f32x4*)&lrow[(16 + il) * LS + 32 * p + 8 * q];
+        const f32x4 a11 = *(const f32x4*)&lrow[(16 + il) * LS + 32 * p + 8 * q + 4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          t0 = mfma4(a00[s], bv[s], t0);
+          t1 = mfma4(a10[s], bv[s], t1);
         }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          t0 = mfma4(a01[s], bv[4 + s], t0);
+          t1 = mfma4(a11[s], bv[4 + s], t1);
+        }
+      };
+      auto xload = [&](int p, float (&bv)[8]) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) bv[s] = Xw[(size_t)(32 * p + 8 * q + s) * Np + 16 * J + il];
+      };
+      int p = J >> 1;
+      for (; p + 1 < i; p += 2) {
+        float b0[8], b1[8];
+        xload(p, b0);
+        xload(p + 1, b1);
+        chunk(p, b0);
+        chunk(p + 1, b1);
+      }
+      if (p < i) {
+        float b0[8];
+        xload(p, b0);
+        chunk(p, b0);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
