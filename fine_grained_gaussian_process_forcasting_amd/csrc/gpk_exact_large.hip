@@ -23,7 +23,8 @@
 //     dX / dy / dhyp formulas as the N <= 256 backward (gpk_exact_grad.hip), partial sums
 //     reduced in a fixed order (deterministic).
 //   gpk_lg_post_kernel   (one workgroup per (window, 16 test points)) -- V = L^-1 K* by
-//     blocked forward substitution with V in LDS, mean = c + V^T z, var = s2 - colsum(V o V).
+//     blocked forward substitution with V in LDS (two waves form R = K*_k - L_k,<k V, a third
+//     forms L_kk^-1 meanwhile, V_k = L_kk^-1 R on MFMA), mean = c + V^T z, var = s2 - colsum(V o V).
 //
 // Tile conventions: gpk_common.h ("acc layout"). Operands of a K = 32 product are fed with
 // the k order k = 8q + s (lane l: q = l >> 4 picks the MFMA k slot, s the instruction), so a
@@ -58,7 +59,7 @@ namespace {
 #endif
 constexpr int kLgWaves = GPK_LG_WAVES;   // waves per window workgroup (forward, backward)
 constexpr int kLgThreads = 64 * kLgWaves;
-constexpr int kPostThreads = 128;
+constexpr int kPostThreads = 192;   // posterior: 2 waves for R, 1 for L_kk^-1
 constexpr int kPS = 36;          // LDS row stride of a 32-wide panel / block (floats; 16-B rows)
 constexpr int kVS = 17;          // LDS row stride of 16-column scratch (V, T)
 constexpr float kLog2PiL = 1.8378770664093453f;
@@ -767,18 +768,20 @@ __global__ void __launch_bounds__(kLgThreads, 1) gpk_lg_grad_kernel(GpkExactGrad
 // Posterior: V = L^-1 K* (16 test points per workgroup), mean and latent variance.
 // =========================================================================================
 struct LgPostLds {
-  int V, lkk, zb, nrm, mu, ils, tn, total;
+  int V, lkk, linv, zb, nrm, mu, ils, tn, red, total;
 };
 __host__ __device__ inline LgPostLds lg_post_layout(int Np) {
   LgPostLds o{};
   o.V = 0;                    // Np x kVS
   o.lkk = o.V + Np * kVS;     // 32 x kPS: L_kk (identity-padded)
-  o.zb = o.lkk + 32 * kPS;    // Np
+  o.linv = o.lkk + 32 * kPS;  // 32 x kPS: L_kk^-1
+  o.zb = o.linv + 32 * kPS;   // Np
   o.nrm = o.zb + Np;          // Np
   o.mu = o.nrm + Np;          // 64
   o.ils = o.mu + 64;           // 64
   o.tn = o.ils + 64;           // 16: test-point norms
-  o.total = o.tn + 16;
+  o.red = o.tn + 16;           // 2 x 32: per-wave mean / variance partials
+  o.total = o.red + 64;
   return o;
 }
 
@@ -790,11 +793,13 @@ __global__ void __launch_bounds__(kPostThreads) gpk_lg_post_kernel(GpkPostArgs a
   const LgPostLds lay = lg_post_layout(Np);
   float* V = smem + lay.V;
   float* lkk = smem + lay.lkk;
+  float* linv = smem + lay.linv;
   float* zb = smem + lay.zb;
   float* nrm = smem + lay.nrm;
   float* mu = smem + lay.mu;
   float* ils = smem + lay.ils;   // 1 / lengthscale
   float* tn = smem + lay.tn;
+  float* red = smem + lay.red;
   const float* X = a.X + (size_t)b * N * D;
   const float* Xs = a.Xs + (size_t)b * Ns * D;
   const float* Lg = a.L + (size_t)b * N * N;
@@ -811,7 +816,7 @@ __global__ void __launch_bounds__(kPostThreads) gpk_lg_post_kernel(GpkPostArgs a
     tn[tid] = s;
   }
   for (int i = tid; i < Np; i += kPostThreads) zb[i] = i < N ? a.z[(size_t)b * N + i] : 0.f;
-  float mp = 0.f, vp = 0.f;
+  float mp = 0.f, vp = 0.f;   // waves 0, 1: partials of column c over this wave's rows
   for (int k = 0; k < nb; ++k) {
     const int r0 = 32 * k;
     for (int e = tid; e < 32 * 32; e += kPostThreads) {
@@ -821,8 +826,8 @@ __global__ void __launch_bounds__(kPostThreads) gpk_lg_post_kernel(GpkPostArgs a
       lkk[i * kPS + m] = v;
     }
     __syncthreads();   // (also: tn / zb / the previous step's V rows)
-    // R = K*[rows r0 + 16 wave, cols t0..] - L[rows, :r0] V[:r0, :]
-    {
+    if (wave < 2) {
+      // R = K*[rows r0 + 16 wave, cols t0..] - L[rows, :r0] V[:r0, :]  -> V rows (LDS)
       const int rows = r0 + 16 * wave;
       const f32x4 dot = lg_gram_tile(X, N, rows, Xs, Ns, t0, mu, ils, D, lane);
       f32x4 acc;
@@ -862,30 +867,48 @@ __global__ void __launch_bounds__(kPostThreads) gpk_lg_post_kernel(GpkPostArgs a
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) V[(rows + 4 * g + r) * kVS + c] = acc[r];
-    }
-    __syncthreads();
-    // V_k = L_kk^-1 R (lanes 0..15 of wave 0: one test point each)
-    if (wave == 0 && lane < 16) {
-      float xv[32];
+    } else {
+      // wave 2, meanwhile: L_kk^-1 (column per lane) for the MFMA solve below
+      const int cr = lane & 31;
+      float x[32];
+      lg_inv32(lkk, cr, x);
+      if (lane < 32) {
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        float s = V[(r0 + i) * kVS + lane];
-#pragma unroll
-        for (int p = 0; p < i; ++p) s = fmaf(-lkk[i * kPS + p], xv[p], s);
-        xv[i] = s / lkk[i * kPS + i];
-      }
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        V[(r0 + i) * kVS + lane] = xv[i];
-        mp = fmaf(xv[i], zb[r0 + i], mp);
-        vp = fmaf(xv[i], xv[i], vp);
+        for (int i = 0; i < 32; ++i) linv[i * kPS + cr] = x[i];
       }
     }
     __syncthreads();
+    // V_k = L_kk^-1 R: rows 16 wave of the block, K = 32 (A: L_kk^-1 rows, B: R columns)
+    f32x4 yv = {0.f, 0.f, 0.f, 0.f};
+    if (wave < 2) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        yv = mfma4(linv[(16 * wave + il) * kPS + 8 * q + s], V[(r0 + 8 * q + s) * kVS + il], yv);
+    }
+    __syncthreads();   // every wave is done reading R before V_k overwrites it
+    if (wave < 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + 16 * wave + 4 * g + r;
+        V[row * kVS + c] = yv[r];
+        mp = fmaf(yv[r], zb[row], mp);
+        vp = fmaf(yv[r], yv[r], vp);
+      }
+    }
   }
-  if (wave == 0 && lane < 16 && t0 + lane < Ns) {
-    a.mean[(size_t)b * Ns + t0 + lane] = cmean + mp;
-    a.var[(size_t)b * Ns + t0 + lane] = s2 - vp;
+  // per-column totals: the four lane groups of each wave, then the two waves, in order
+  mp += __shfl_xor(mp, 16, 64);
+  mp += __shfl_xor(mp, 32, 64);
+  vp += __shfl_xor(vp, 16, 64);
+  vp += __shfl_xor(vp, 32, 64);
+  if (wave < 2 && lane < 16) {
+    red[wave * 32 + lane] = mp;
+    red[wave * 32 + 16 + lane] = vp;
+  }
+  __syncthreads();
+  if (tid < 16 && t0 + tid < Ns) {
+    a.mean[(size_t)b * Ns + t0 + tid] = cmean + (red[tid] + red[32 + tid]);
+    a.var[(size_t)b * Ns + t0 + tid] = s2 - (red[16 + tid] + red[48 + tid]);
   }
 }
 
