@@ -20,6 +20,8 @@ Side legs in the same JSON line (not the headline):
   backward     the exact path's analytic adjoint on the headline windows;
   posterior    the exact path's eval-mode posterior (mean + variance at N new points per
                window) from the headline windows' factor;
+  exact_large  B=512 windows of N=800 (256 < N <= 800, GPyTorch's Cholesky regime): the
+               blocked forward and backward of gpk_exact_large.hip;
   e2e_step     the cfg-3 forecast -> GP blur -> denoise train step, eager and HIP-graph
                captured (scripts/gp_step.py, graphs.GraphedStep);
   cpu_baseline the reference's CPU arithmetic (GPyTorch's torch-CPU calls restated in
@@ -406,6 +408,7 @@ def main():
     ap.add_argument("--no-grad", action="store_true", help="skip the backward side measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end train-step side leg")
     ap.add_argument("--no-cfg2", action="store_true", help="skip the B=128 N=128 side leg")
+    ap.add_argument("--no-large", action="store_true", help="skip the B=512 N=800 side leg")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the measurement-only variant builds (e.g. under rocprofv3)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
@@ -523,6 +526,29 @@ def main():
     else:                   # the timed loop itself was the eager one
         eager_kern_ms = kern_ms
 
+    # 256 < N <= 800 (GPyTorch's Cholesky regime, the blocked kernels of gpk_exact_large.hip):
+    # B=512 windows of N=800, forward and backward, eager back-to-back calls
+    large = None
+    if rank == 0 and not args.no_large:
+        BL, NL = 512, 800
+        XL, yL = make_inputs(BL, NL, D, dev, seed=17)
+        fl = ops.exact_mll(XL, yL, None, None, None, None, hyper=hyper, want_L=True, want_z=True)
+        goutL = torch.ones(BL, device=dev)
+        torch.cuda.synchronize()
+        fwd_l, _ = time_launches(lambda: ops.exact_mll(XL, yL, None, None, None, None, hyper=hyper), 5)
+        bwd_l, _ = time_launches(lambda: ops.exact_mll_grad(XL, fl.L, fl.z, hyper, goutL), 3)
+        fl_f = NL ** 3 / 3 + 2 * NL * NL * D + 2 * NL * NL      # Cholesky, _sq_dist Gram, solve
+        by_f = 4 * (NL * D + 2 * NL + NL * NL)                 # X, y in; L, z out
+        large = {"workload": "exact-GP windows B=512 N=800 D=32 (256 < N <= 800: GPyTorch's "
+                             "Cholesky regime), L written",
+                 "kernel": "gpk_exact_mll_f32 / gpk_exact_mll_grad_f32 (gpk_exact_large.hip)",
+                 "fwd_ms": fwd_l, "bwd_ms": bwd_l, "windows_per_s": BL / (fwd_l * 1e-3),
+                 "fwd_fp32_frac": fl_f * BL / (fwd_l * 1e-3) / FP32_PEAK,
+                 "fwd_hbm_frac_algorithmic": by_f * BL / (fwd_l * 1e-3) / HBM_PEAK,
+                 "info_max": int(fl.info.abs().max()),
+                 "note": "right-looking 32-wide panels with the window's matrix in HBM: bound by the "
+                         "trailing matrix's traffic (DESIGN.md 4.10); not the headline"}
+        del XL, yL, fl
     # BASELINE configs[1] (B=128, N=128, D=32): a side leg, same kernel, its own roofline
     cfg2 = None
     if rank == 0 and not args.no_cfg2:
@@ -642,6 +668,8 @@ def main():
                                  "note": "eval-mode exact posterior mean + variance; not the headline"}
         if cfg2 is not None:
             line["cfg2"] = cfg2
+        if large is not None:
+            line["exact_large"] = large
         if var is not None:
             line["variational"] = var
             line["elbo_rel_err_vs_fp64_oracle"] = var["elbo_rel_err_vs_fp64_oracle"]
