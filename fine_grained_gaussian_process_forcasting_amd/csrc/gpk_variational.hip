@@ -3327,161 +3327,6 @@ gpk_var_adj_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
   }
 }
 
-// ---------------------------------------------------------------------------
-// dL^{-1} of the register path (M <= 64) without the dA / K_ZX workspace. With
-// dA = gmean m^T-terms + 2 gvar (s^2 - 1) o A and A = L^{-1} K_ZX:
-//   dL^{-1} = sum_i dA_i K_i^T = vm u^T + 2 diag(s^2 - 1) L^{-1} G,
-//   u = sum_i gmean_i K_i,  G = sum_i gvar_i K_i K_i^T     (gvar clamp-masked by the adjoint)
-// so only K_ZX is needed, recomputed here in the TRANSPOSED orientation (points on the
-// rows of each f32 acc tile), which makes sum_s mfma(Q.reg[s], P.reg[s]) = Q^T P the
-// point contraction: the 10 lower 16 x 16 tiles of G accumulate in registers (fp32 per
-// wave, fp64 across waves / workgroups). Partials per workgroup:
-//   [G lower tiles (10 x 256, acc order) | u (64)].
-// ---------------------------------------------------------------------------
-template <int DQ>
-__global__ void __launch_bounds__(256, 2)
-gpk_var_kgram_r_kernel(const float* __restrict__ X, const float* __restrict__ Z,
-                       const float* __restrict__ vmean, const float* __restrict__ vstd,
-                       const float* __restrict__ hyp, const float* __restrict__ gmean,
-                       const float* __restrict__ wsgv, int B, int N, int M, int D,
-                       float* __restrict__ gpart) {
-  using L = RegLds<DQ>;
-  extern __shared__ __attribute__((aligned(16))) float vsm[];
-  const float s2 = hyp[0];
-  const float* ls = hyp + 4 + D;
-  stage_inducing(Z, ls, vmean, vstd, M, D, 64, DQ, L::ZS, vsm + L::zs, vsm + L::zn, vsm + L::cm,
-                 vsm + L::vm, vsm + L::sm1, vsm + L::li);
-  lds_barrier();
-  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
-  const int wave = tid >> 6;
-  float il[DQ / 4], cmv[DQ / 4], wv[DQ / 4];
-  dim_consts<DQ>(vsm, ls, nullptr, D, il, cmv, wv);
-  f32x4 G[kGTiles];
-#pragma unroll
-  for (int t = 0; t < kGTiles; ++t) G[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float u[4] = {0.f, 0.f, 0.f, 0.f};
-  const int nch = (N + 31) / 32;
-  const long long total = (long long)B * nch;
-  const long long stride = (long long)gridDim.x * 4;
-  // the next chunk's raw point values and weights are requested before this chunk's math
-  // (software pipeline over the wave's chunks: one memory latency per wave, not per chunk)
-  float rx[2][DQ / 4], gvr[2][4], gmr[2][4];
-  auto fetch = [&](long long t, float (&x)[2][DQ / 4], float (&gv)[2][4], float (&gm)[2][4]) {
-    const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
-    const size_t col0 = (size_t)b * N;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int i = i0 + 16 * q + c;
-      const float* xr = X + (col0 + (i < N ? i : 0)) * D;
-#pragma unroll
-      for (int s4 = 0; s4 < DQ / 4; ++s4) {
-        const int d = 4 * s4 + g;
-        x[q][s4] = xr[d < D ? d : 0];
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ii = i0 + 16 * q + 4 * g + r;
-        const size_t e = col0 + (ii < N ? ii : 0);
-        gv[q][r] = wsgv[e];
-        gm[q][r] = gmean[e];
-      }
-    }
-  };
-  long long t = (long long)blockIdx.x * 4 + wave;
-  if (t < total) fetch(t, rx, gvr, gmr);
-  for (; t < total; t += stride) {
-    const int b = (int)(t / nch), i0 = (int)(t - (long long)b * nch) * 32;
-    const float* sm = fresh_lds(vsm);
-    const float* zs = sm + L::zs;
-    const float* zn = sm + L::zn;
-    RegPoints<DQ> P;
-    float gvc[2][4], gmc[2][4];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int i = i0 + 16 * q + c;
-      float nn = 0.f;
-#pragma unroll
-      for (int s4 = 0; s4 < DQ / 4; ++s4) {
-        const int d = 4 * s4 + g;
-        const float v = (i < N && d < D) ? rx[q][s4] * il[s4] - cmv[s4] : 0.f;
-        P.xb[q][s4] = v;
-        nn = __builtin_fmaf(v, v, nn);
-      }
-      nn += __shfl_xor(nn, 16, 64);
-      nn += __shfl_xor(nn, 32, 64);
-      P.xn[q] = nn;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        gvc[q][r] = gvr[q][r];
-        gmc[q][r] = gmr[q][r];
-      }
-    }
-    if (t + stride < total) fetch(t + stride, rx, gvr, gmr);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      float xn[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) xn[r] = __shfl(P.xn[q], 4 * g + r, 64);
-      // K^T tiles: rows = points 16 q + 4 g + r, columns = inducing points 16 rt + c
-      f32x4 KT[4], W[4];
-#pragma unroll
-      for (int rt = 0; rt < 4; ++rt) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < DQ / 4; ++s) acc = mfma32(P.xb[q][s], zs[(16 * rt + c) * L::ZS + 4 * s + g], acc);
-        const int p = 16 * rt + c;
-        const float znp = zn[p];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = (i0 + 16 * q + 4 * g + r < N) && p < M;
-          const float d2 = __builtin_fmaxf(znp + xn[r] - 2.f * acc[r], 0.f);
-          const float kv = ok ? s2 * __builtin_amdgcn_exp2f(kNHalfLog2e * d2) : 0.f;
-          KT[rt][r] = kv;
-          W[rt][r] = kv * gvc[q][r];
-          u[rt] = __builtin_fmaf(gmc[q][r], kv, u[rt]);
-        }
-      }
-      // G(rt, rt') += K_rt diag(gv) K_rt'^T = sum_s mfma(KT_rt.reg[s], W_rt'.reg[s])
-#pragma unroll
-      for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-        for (int rp = 0; rp <= rt; ++rp)
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-            G[rt * (rt + 1) / 2 + rp] = mfma32(KT[rt][s], W[rp][s], G[rt * (rt + 1) / 2 + rp]);
-    }
-  }
-  // workgroup partial: the 4 waves summed in a fixed order through LDS (the staging area is free)
-#pragma unroll
-  for (int rt = 0; rt < 4; ++rt) {
-    u[rt] += __shfl_xor(u[rt], 16, 64);
-    u[rt] += __shfl_xor(u[rt], 32, 64);
-  }
-  float* red = vsm;   // kGPart floats
-  for (int wv2 = 0; wv2 < 4; ++wv2) {
-    lds_barrier();
-    if (wave == wv2) {
-#pragma unroll
-      for (int t2 = 0; t2 < kGTiles; ++t2)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int e = t2 * 256 + r * 64 + lane;
-          red[e] = (wv2 == 0 ? 0.f : red[e]) + G[t2][r];
-        }
-      if (g == 0) {
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          const int e = kGTiles * 256 + 16 * rt + c;
-          red[e] = (wv2 == 0 ? 0.f : red[e]) + u[rt];
-        }
-      }
-    }
-  }
-  lds_barrier();
-  float* po = gpart + (size_t)blockIdx.x * kGPart;
-  for (int e = tid; e < kGPart; e += 256) po[e] = red[e];
-}
-
 // dL^{-1}[p][k] = vm_p u_k + 2 (s_p^2 - 1) (L^{-1} G)[p][k]  (k <= p < M; upper zero) from the
 // reduced totals (fp64). One workgroup: G (symmetric, from its lower tiles) in LDS, wave w
 // forms the 16-row block w of L^{-1} G on fp64 MFMA with its L^{-1} operands requested up
@@ -3538,14 +3383,6 @@ GPK_DEVICE void var_gdl_block(const double* __restrict__ gtot, const double* __r
   }
 }
 
-__global__ void __launch_bounds__(256)
-gpk_var_gdl_kernel(const double* __restrict__ gtot, const double* __restrict__ Linv,
-                   const float* __restrict__ vmean, const float* __restrict__ vstd, int M,
-                   double* __restrict__ dLinv) {
-  __shared__ double Gs[64][65];
-  __shared__ double us[64];
-  var_gdl_block(gtot, Linv, vmean, vstd, M, dLinv, Gs, us);
-}
 
 // ---------------------------------------------------------------------------
 // launchers
@@ -3662,10 +3499,7 @@ struct AdjPlan {
 #define GPK_VAR_REG 1   // 0: A/B builds without the register-resident path
 #endif
 GPK_HOST_DEVICE_INLINE bool var_reg_path(int M, int D) { return GPK_VAR_REG && M <= 64 && D <= 32; }
-#ifndef GPK_VAR_FUSEG
-#define GPK_VAR_FUSEG 1   // 0: A/B builds with the separate gpk_var_kgram_r_kernel (4-wave adjoint)
-#endif
-constexpr int kAdjRWaves = GPK_VAR_FUSEG ? 8 : 4;   // waves per register-path adjoint workgroup
+constexpr int kAdjRWaves = 8;   // waves per register-path adjoint workgroup (K-Gram folded in)
 
 AdjPlan adj_plan_common(AdjPlan p, int B, int N, int M, int D);
 
@@ -3691,23 +3525,21 @@ AdjPlan adj_plan(int B, int N, int M, int D) {
     }
   }
   if (var_reg_path(M, D)) {
-    // workspace: masked gvar (BN) | K-Gram partials (nwg x kGPart) | adjoint partials | their
-    // fp64 totals | K-Gram totals. With the K-Gram folded in (GPK_VAR_FUSEG): the centre (64) |
-    // - | rows of [adjoint | K-Gram] partials | their fp64 totals (the K-Gram totals at + P) | -
+    // workspace (the K-Gram folded into the adjoint): the centre (64) | rows of
+    // [adjoint | K-Gram] partials | their fp64 totals (the K-Gram totals at + P)
     const long long nch = (long long)B * ((N + 31) / 32);
     p.nchunks = (int)nch;
-    // one workgroup per CU (8 waves, K-Gram folded in) or two (4 waves)
+    // one workgroup per CU (8 waves, K-Gram folded in)
     const long long nwg_max = 2048 / kAdjRWaves;
     p.nwg = (int)((nch + kAdjRWaves - 1) / kAdjRWaves < nwg_max ? (nch + kAdjRWaves - 1) / kAdjRWaves : nwg_max);
     p = adj_plan_common(p, B, N, M, D);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o = 0;
-    constexpr bool fg = GPK_VAR_FUSEG != 0;
-    p.off_dA = o; o = al(o + (fg ? 64 : (size_t)p.BN) * sizeof(float));
-    p.off_K = o; o = al(o + (fg ? 0 : (size_t)p.nwg * kGPart) * sizeof(float));
-    p.off_part = o; o = al(o + (size_t)p.nwg * (p.P + (fg ? kGPart : 0)) * sizeof(float));
-    p.off_tot = o; o = al(o + (size_t)(p.P + (fg ? kGPart : 0)) * sizeof(double));
-    p.off_dl = o; o = al(o + (fg ? 0 : (size_t)kGPart) * sizeof(double));
+    p.off_dA = o; o = al(o + 64 * sizeof(float));
+    p.off_K = o;
+    p.off_part = o; o = al(o + (size_t)p.nwg * (p.P + kGPart) * sizeof(float));
+    p.off_tot = o; o = al(o + (size_t)(p.P + kGPart) * sizeof(double));
+    p.off_dl = o;
     p.total = o;
     return p;
   }
@@ -3777,11 +3609,10 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
   if (var_reg_path(a.M, a.D)) {
     constexpr int RQ = DQ <= 16 ? 16 : 32;
     float* wsgv = wsdA;   // FG: the centre cm (D floats)
-    float* gpart = wsK;
     double* tot = (double*)(ws + p.off_tot);
     constexpr int NW = kAdjRWaves;
-    constexpr bool FG = GPK_VAR_FUSEG != 0;
-    double* gtot = FG ? tot + p.P : (double*)(ws + p.off_dl);
+    constexpr bool FG = true;   // the K-Gram folded into the adjoint (round 5)
+    double* gtot = tot + p.P;   // the K-Gram totals after the adjoint totals
     static_assert(RegLds<RQ, NW, FG>::adj_total * sizeof(float) <= 160 * 1024, "LDS per workgroup");
     const size_t lds = (size_t)RegLds<RQ, NW, FG>::adj_total * sizeof(float);
     set_lds_once<gpk_var_adj_r_kernel<RQ, NW, FG>>();
@@ -3790,32 +3621,13 @@ int launch_var_adj(const GpkVarAdjArgs& a, hipStream_t stream) {
                        wsgv, wspart, wsgv, a.dX);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    if constexpr (FG) {
-      // one fixed-order reduction of the [adjoint | K-Gram] rows; dL^{-1} in the output launch
-      const int PR = p.P + kGPart;
-      hipLaunchKernelGGL(gpk_var_red_kernel, dim3((PR + 31) / 32), dim3(256), 0, stream, wspart, p.nwg, PR,
-                         tot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
-      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-      const VarGdlArgs gd{gtot, a.Linv, a.vmean, a.vstd, a.dLinv, 0};
-      return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream, wsgv, &gd);
-    } else {
-      set_lds_once<gpk_var_kgram_r_kernel<RQ>>();
-      hipLaunchKernelGGL((gpk_var_kgram_r_kernel<RQ>), dim3(p.nwg), dim3(256),
-                         (size_t)RegLds<RQ>::fwd_total * sizeof(float), stream, a.X, a.Z, a.vmean, a.vstd,
-                         a.hyp, a.gmean, wsgv, a.B, a.N, a.M, a.D, gpart);
-      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    }
-    // fixed-order sums: K-Gram partials -> gtot, adjoint partials -> tot (section (a) only)
-    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((kGPart + 31) / 32), dim3(256), 0, stream, gpart, p.nwg,
-                       kGPart, gtot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
+    // one fixed-order reduction of the [adjoint | K-Gram] rows; dL^{-1} in the output launch
+    const int PR = p.P + kGPart;
+    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((PR + 31) / 32), dim3(256), 0, stream, wspart, p.nwg, PR,
+                       tot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(gpk_var_red_kernel, dim3((p.P + 31) / 32), dim3(256), 0, stream, wspart, p.nwg,
-                       p.P, tot, nullptr, 0, 0, 0, nullptr, nullptr, 0, nullptr);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(gpk_var_gdl_kernel, dim3(1), dim3(256), 0, stream, gtot, a.Linv, a.vmean, a.vstd,
-                       a.M, a.dLinv);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream);
+    const VarGdlArgs gd{gtot, a.Linv, a.vmean, a.vstd, a.dLinv, 0};
+    return launch_var_fin(a.Z, a.vstd, a.hyp, tot, a.M, a.D, a.dZ, a.dpar, stream, wsgv, &gd);
   }
   if constexpr (var_adj_lreg_fits<MB, DQ>()) {
     if (GPK_VAR_LREG && a.M > 64 && (long long)a.M * p.BN * 4 < (1LL << 31)) {
