@@ -1281,6 +1281,16 @@ GPK_DEVICE int worker_steps(f32x4 (&acc)[SLOTS], WorkerCtx& x) {
 // OCC = workgroups per CU the register budget is sized for: 2 (the B >= 2 x CUs
 // layout, two windows per CU) or 1 (small batches: one window per CU with W = 16
 // waves, twice the workers per window -- launch_exact_nb).
+// Role of physical wave p in the DIAG_ALONE layout (a permutation of 0..15): the waves of
+// SIMD 3 (p % 4 == 3) are the diagonal wave (p = 15 -> 12) and three idle waves (13..15);
+// the 12 waves of SIMDs 0-2 are workers 0..11. Every wave still joins the prologue and the
+// final reduction (the permutation keeps their per-wave LDS slots distinct).
+GPK_DEVICE int exact_role(int p) {
+  if (p == 15) return 12;
+  if ((p & 3) == 3) return 13 + (p >> 2);
+  return (p >> 2) * 3 + (p & 3);
+}
+
 template <int NB, int W, bool STAMPS, bool FULL, int OCC = 2>
 __global__ void __launch_bounds__(64 * W, (OCC * W) / 4)
 gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
@@ -1290,7 +1300,13 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
                  int* __restrict__ info, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int NT = ExactPlan<NB>::NT;
   const int N = FULL ? 16 * NB : N_in;  // FULL: no padded rows anywhere
-  constexpr int WK = W - 1;                  // worker waves; wave WK is the diagonal wave
+  // DIAG_ALONE (small-batch layout, 16 waves, NB <= 8): the diagonal wave gets a SIMD to
+  // itself -- waves are dealt to the 4 SIMDs round-robin, so the three other waves of its
+  // SIMD idle and 12 workers remain (see exact_role). Measured (profiles/r06_exact_alone_ab.txt):
+  // B=128 N=128 20.3 -> 19.2 us; at N=256 (136 tiles) the workers pace the steps and the same
+  // layout is 2 % slower, so NB > 8 keeps 15 workers.
+  constexpr bool ALONE = GPK_EXACT_DIAG_ALONE && OCC == 1 && W == 16 && NB <= 8;
+  constexpr int WK = ALONE ? 12 : W - 1;     // worker waves; wave WK is the diagonal wave
   constexpr bool COL = GPK_EXACT_COL && NB == 16 && WK == 7;   // column-ownership worker plan
   constexpr int SLOTS = COL ? kColSlots : (NT + WK - 1) / WK;
   constexpr int T = 64 * W;
@@ -1317,7 +1333,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, grp = lane >> 4;
-  const int wave = wave_id_uniform();
+  const int wave = ALONE ? exact_role(wave_id_uniform()) : wave_id_uniform();
   const int b = blockIdx.x;
   const int DP = DC * 16;
   const int NP = NB * 16;
@@ -1773,7 +1789,7 @@ gpk_exact_kernel(const float* __restrict__ X, const float* __restrict__ y,
     }
     if (GPK_TMO_DEBUG && lane == 0) vflag[24] = att_end;
     __builtin_amdgcn_s_setprio(0);
-  } else {
+  } else if (!ALONE || wave < WK) {
     // ================================================= worker program
     float diagval = (s2u + noise) * sigma2;
     double jit_prev = 0.0;

@@ -16,6 +16,10 @@
 #ifndef GPK_EXACT_SMALLB
 #define GPK_EXACT_SMALLB 1   // B <= CUs: one window per CU with 16 waves (launch_exact_nb)
 #endif
+#ifndef GPK_EXACT_DIAG_ALONE
+#define GPK_EXACT_DIAG_ALONE 1   // 1: small-batch layout (NB <= 8) with the diagonal wave alone on its SIMD
+                                 // (12 workers; 0: 15 workers, the round-5 layout)
+#endif
 #ifndef GPK_EXACT_PRIO_RHS
 #define GPK_EXACT_PRIO_RHS 1   // raise the worker priority already at the right-hand side (0: at the TRSM)
 #endif
